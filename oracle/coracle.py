@@ -1,0 +1,112 @@
+"""ctypes binding to the C parity oracle (oracle/libpnet_oracle.so).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and the
+cpu_baseline leg of bench.py — never by the libpnet_amd product package.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libpnet_oracle.so")
+
+REC_DTYPE = np.dtype([
+    ("status", "<u2"), ("ip_csum", "<u2"), ("l4_csum", "<u2"), ("ethertype", "<u2"),
+    ("ip_proto", "u1"), ("ttl", "u1"), ("l4_offset", "<u2"), ("l4_length", "<u2"),
+    ("src_port", "<u2"), ("dst_port", "<u2"), ("_pad", "<u2"),
+    ("src_ipv4", "<u4"), ("dst_ipv4", "<u4"),
+    ("src_ipv6", "u1", (16,)), ("dst_ipv6", "u1", (16,)),
+], align=True)
+
+_lib = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        u8p = ctypes.POINTER(ctypes.c_uint8)
+        L.oracle_sum_be_words.restype = ctypes.c_uint32
+        L.oracle_sum_be_words.argtypes = [u8p, ctypes.c_size_t, ctypes.c_size_t]
+        L.oracle_checksum.restype = ctypes.c_uint16
+        L.oracle_checksum.argtypes = [u8p, ctypes.c_size_t, ctypes.c_size_t]
+        for f in (L.oracle_ipv4_checksum, L.oracle_ipv6_checksum):
+            f.restype = ctypes.c_uint16
+            f.argtypes = [u8p, ctypes.c_size_t, ctypes.c_size_t, u8p, ctypes.c_size_t,
+                          u8p, u8p, ctypes.c_uint8]
+        L.oracle_rx_frame.restype = None
+        L.oracle_rx_frame.argtypes = [u8p, ctypes.c_size_t, ctypes.c_void_p]
+        L.oracle_rx_batch.restype = None
+        L.oracle_rx_batch.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
+                                      ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
+                                      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                      ctypes.c_int]
+        L.oracle_checksum_slices.restype = None
+        L.oracle_checksum_slices.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+        _lib = L
+    return _lib
+
+
+def _buf(b):
+    b = bytes(b)
+    arr = (ctypes.c_uint8 * max(1, len(b))).from_buffer_copy(b if b else b"\0")
+    return arr
+
+
+def sum_be_words(data, skipword):
+    return lib().oracle_sum_be_words(_buf(data), len(data), skipword)
+
+
+def checksum(data, skipword):
+    return lib().oracle_checksum(_buf(data), len(data), skipword)
+
+
+def ipv4_checksum(data, skipword, extra, src, dst, proto):
+    return lib().oracle_ipv4_checksum(_buf(data), len(data), skipword, _buf(extra), len(extra),
+                                      _buf(src), _buf(dst), proto)
+
+
+def ipv6_checksum(data, skipword, extra, src, dst, proto):
+    return lib().oracle_ipv6_checksum(_buf(data), len(data), skipword, _buf(extra), len(extra),
+                                      _buf(src), _buf(dst), proto)
+
+
+def rx_frame(frame):
+    rec = np.zeros(1, dtype=REC_DTYPE)
+    lib().oracle_rx_frame(_buf(frame), len(frame), rec.ctypes.data)
+    return rec[0]
+
+
+def rx_batch(buf, n, *, stride=0, frame_len=0, first=0, offsets=None, lengths=None,
+             nthreads=1):
+    """Oracle records for a frame batch held in a numpy uint8 array."""
+    buf = np.ascontiguousarray(buf, dtype=np.uint8)
+    out = np.zeros(n, dtype=REC_DTYPE)
+    offp = lenp = None
+    if stride == 0:
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        lengths = np.ascontiguousarray(lengths, dtype=np.uint32)
+        offp, lenp = offsets.ctypes.data, lengths.ctypes.data
+    lib().oracle_rx_batch(buf.ctypes.data, buf.size, n, first, stride, frame_len,
+                          offp, lenp, out.ctypes.data, nthreads)
+    return out
+
+
+def checksum_slices(buf, offsets, lengths, skipwords):
+    buf = np.ascontiguousarray(buf, dtype=np.uint8)
+    offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+    lengths = np.ascontiguousarray(lengths, dtype=np.uint32)
+    skipwords = np.ascontiguousarray(skipwords, dtype=np.uint32)
+    out = np.zeros(len(offsets), dtype=np.uint16)
+    lib().oracle_checksum_slices(buf.ctypes.data, len(offsets), offsets.ctypes.data,
+                                 lengths.ctypes.data, skipwords.ctypes.data, out.ctypes.data)
+    return out

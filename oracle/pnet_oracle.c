@@ -1,0 +1,277 @@
+/*
+ * pnet_oracle.c — CPU restatement of libpnet's receive path (parity oracle).
+ *
+ * TEST INFRASTRUCTURE ONLY (see pnet_oracle.h). Scalar and literal on
+ * purpose: each function follows the cited reference lines one-to-one so
+ * that a reader can check it against the Rust source. It is also the
+ * "port" CPU baseline timed by bench.py (cpu_baseline.kind = "port").
+ */
+#include "pnet_oracle.h"
+
+#include <pthread.h>
+#include <string.h>
+
+/* ---- pnet_packet/src/util.rs ------------------------------------------ */
+
+/* util.rs:158-181  fn sum_be_words(data: &[u8], skipword: usize) -> u32 */
+uint32_t oracle_sum_be_words(const uint8_t* data, size_t len, size_t skipword) {
+    if (len == 0) return 0;                       /* :159-161 */
+    const uint8_t* cur = data;
+    size_t cur_len = len;
+    uint32_t sum = 0;
+    size_t i = 0;
+    while (cur_len >= 2) {                        /* :166 */
+        if (i != skipword) {                      /* :167 */
+            sum += ((uint32_t)cur[0] << 8) | (uint32_t)cur[1];   /* :169 u16::from_be_bytes */
+        }
+        cur += 2;                                 /* :171 */
+        cur_len -= 2;
+        i += 1;                                   /* :172 */
+    }
+    if (i != skipword && (len & 1) != 0) {        /* :176 */
+        sum += (uint32_t)data[len - 1] << 8;      /* :177 */
+    }
+    return sum;
+}
+
+/* util.rs:84-89  fn finalize_checksum(mut sum: u32) -> u16be */
+uint16_t oracle_finalize_checksum(uint32_t sum) {
+    while ((sum >> 16) != 0) {
+        sum = (sum >> 16) + (sum & 0xFFFF);
+    }
+    return (uint16_t)~sum;
+}
+
+/* util.rs:76-82  pub fn checksum(data: &[u8], skipword: usize) -> u16be */
+uint16_t oracle_checksum(const uint8_t* data, size_t len, size_t skipword) {
+    if (len == 0) return 0;
+    return oracle_finalize_checksum(oracle_sum_be_words(data, len, skipword));
+}
+
+/* util.rs:119-122  fn ipv4_word_sum(ip: &Ipv4Addr) -> u32 */
+static uint32_t ipv4_word_sum(const uint8_t o[4]) {
+    return (((uint32_t)o[0] << 8) | o[1]) + (((uint32_t)o[2] << 8) | o[3]);
+}
+
+/* util.rs:152-154  fn ipv6_word_sum(ip: &Ipv6Addr) -> u32  (segments().sum()) */
+static uint32_t ipv6_word_sum(const uint8_t o[16]) {
+    uint32_t s = 0;
+    for (int k = 0; k < 8; ++k) s += ((uint32_t)o[2 * k] << 8) | o[2 * k + 1];
+    return s;
+}
+
+/* util.rs:92-117  pub fn ipv4_checksum(...) -> u16be */
+uint16_t oracle_ipv4_checksum(const uint8_t* data, size_t len, size_t skipword,
+                              const uint8_t* extra, size_t extra_len,
+                              const uint8_t src[4], const uint8_t dst[4], uint8_t proto) {
+    uint32_t sum = 0;
+    sum += ipv4_word_sum(src);                                    /* :103 */
+    sum += ipv4_word_sum(dst);                                    /* :104 */
+    sum += proto;                                                 /* :107 */
+    sum += (uint32_t)(len + extra_len);                           /* :109-110 */
+    sum += oracle_sum_be_words(data, len, skipword);              /* :113 */
+    sum += oracle_sum_be_words(extra, extra_len, extra_len / 2);  /* :114 */
+    return oracle_finalize_checksum(sum);                         /* :116 */
+}
+
+/* util.rs:125-150  pub fn ipv6_checksum(...) -> u16be */
+uint16_t oracle_ipv6_checksum(const uint8_t* data, size_t len, size_t skipword,
+                              const uint8_t* extra, size_t extra_len,
+                              const uint8_t src[16], const uint8_t dst[16], uint8_t proto) {
+    uint32_t sum = 0;
+    sum += ipv6_word_sum(src);                                    /* :136 */
+    sum += ipv6_word_sum(dst);                                    /* :137 */
+    sum += proto;                                                 /* :140 */
+    sum += (uint32_t)(len + extra_len);                           /* :142-143 */
+    sum += oracle_sum_be_words(data, len, skipword);              /* :146 */
+    sum += oracle_sum_be_words(extra, extra_len, extra_len / 2);  /* :147 */
+    return oracle_finalize_checksum(sum);                         /* :149 */
+}
+
+/* ---- generated accessors (pnet_macros/src/decorator.rs:1563-1670) ----- */
+
+static inline uint16_t be16(const uint8_t* p) { return (uint16_t)(((uint16_t)p[0] << 8) | p[1]); }
+static inline uint32_t be32(const uint8_t* p) {
+    return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
+}
+
+/* A borrowed byte slice, the PacketData::Borrowed of packet.rs:117-122. */
+typedef struct { const uint8_t* p; size_t len; } slice_t;
+
+/* ---- L4 handlers: packetdump.rs:31-98 plus the checksum wrappers ------- */
+
+/* udp.rs:23-31 (min size 8), udp.rs:34-56 / 104-126 (skipword 3) */
+/* tcp.rs:55-71 (min size 20), tcp.rs:239-286 (skipword 8)            */
+/* icmp.rs:55-67 (min size 4),  icmp.rs:70-75 (skipword 1, no pseudo)  */
+/* icmpv6.rs:68-77 (min size 4), icmpv6.rs:80-85 (IPv6 pseudo, skip 1) */
+static void l4_dispatch(oracle_rec* r, int is_v6, uint8_t proto, slice_t l4,
+                        const uint8_t* src, const uint8_t* dst) {
+    switch (proto) {
+    case 17: /* IpNextHeaderProtocols::Udp, ip.rs:79 */
+        r->status |= ORACLE_ST_L4_UDP;
+        if (l4.len < 8) { r->status |= ORACLE_ST_L4_MALFORMED; return; }  /* UdpPacket::new */
+        r->src_port = be16(l4.p + 0);
+        r->dst_port = be16(l4.p + 2);
+        r->l4_csum = is_v6 ? oracle_ipv6_checksum(l4.p, l4.len, 3, NULL, 0, src, dst, 17)
+                           : oracle_ipv4_checksum(l4.p, l4.len, 3, NULL, 0, src, dst, 17);
+        r->status |= ORACLE_ST_L4_CSUM_DONE;
+        if (r->l4_csum == be16(l4.p + 6)) r->status |= ORACLE_ST_L4_CSUM_OK;
+        return;
+    case 6: /* IpNextHeaderProtocols::Tcp, ip.rs:46 */
+        r->status |= ORACLE_ST_L4_TCP;
+        if (l4.len < 20) { r->status |= ORACLE_ST_L4_MALFORMED; return; }  /* TcpPacket::new */
+        r->src_port = be16(l4.p + 0);
+        r->dst_port = be16(l4.p + 2);
+        r->l4_csum = is_v6 ? oracle_ipv6_checksum(l4.p, l4.len, 8, NULL, 0, src, dst, 6)
+                           : oracle_ipv4_checksum(l4.p, l4.len, 8, NULL, 0, src, dst, 6);
+        r->status |= ORACLE_ST_L4_CSUM_DONE;
+        if (r->l4_csum == be16(l4.p + 16)) r->status |= ORACLE_ST_L4_CSUM_OK;
+        return;
+    case 1: /* IpNextHeaderProtocols::Icmp, ip.rs:31 */
+        r->status |= ORACLE_ST_L4_ICMP;
+        if (l4.len < 4) { r->status |= ORACLE_ST_L4_MALFORMED; return; }   /* IcmpPacket::new */
+        r->src_port = be16(l4.p + 0);                     /* icmp_type << 8 | icmp_code */
+        r->dst_port = l4.len >= 8 ? be16(l4.p + 4) : 0;   /* echo identifier, icmp.rs:221-232 */
+        r->l4_csum = oracle_checksum(l4.p, l4.len, 1);
+        r->status |= ORACLE_ST_L4_CSUM_DONE;
+        if (r->l4_csum == be16(l4.p + 2)) r->status |= ORACLE_ST_L4_CSUM_OK;
+        return;
+    case 58: /* IpNextHeaderProtocols::Icmpv6, ip.rs:205 */
+        r->status |= ORACLE_ST_L4_ICMPV6;
+        if (l4.len < 4) { r->status |= ORACLE_ST_L4_MALFORMED; return; }   /* Icmpv6Packet::new */
+        r->src_port = be16(l4.p + 0);
+        r->dst_port = l4.len >= 8 ? be16(l4.p + 4) : 0;
+        if (is_v6) { /* icmpv6::checksum needs IPv6 addresses; none exists over IPv4 */
+            r->l4_csum = oracle_ipv6_checksum(l4.p, l4.len, 1, NULL, 0, src, dst, 58);
+            r->status |= ORACLE_ST_L4_CSUM_DONE;
+            if (r->l4_csum == be16(l4.p + 2)) r->status |= ORACLE_ST_L4_CSUM_OK;
+        }
+        return;
+    default:
+        r->status |= ORACLE_ST_UNKNOWN_PROTO;             /* packetdump.rs:139-152 */
+        return;
+    }
+}
+
+/* packetdump.rs:155-168 handle_ipv4_packet */
+static void handle_ipv4(oracle_rec* r, slice_t ep) {
+    r->status |= ORACLE_ST_L3_IPV4;
+    if (ep.len < 20) { r->status |= ORACLE_ST_L3_MALFORMED; return; }  /* Ipv4Packet::new, min 20 */
+    const uint8_t* ip = ep.p;
+    unsigned ihl = ip[0] & 0x0F;                          /* header_length: u4 */
+    /* ipv4.rs:165-178: clamp IHL*4 to [minimum_packet_size, packet().len()] */
+    size_t hl = (size_t)ihl * 4;
+    if (hl < 20) hl = 20;
+    else if (hl > ep.len) hl = ep.len;
+    r->ip_csum = oracle_checksum(ip, hl, 5);
+    if (r->ip_csum == be16(ip + 10)) r->status |= ORACLE_ST_IP_CSUM_OK;
+
+    r->ttl = ip[8];
+    r->ip_proto = ip[9];
+    r->src_ipv4 = be32(ip + 12);
+    r->dst_ipv4 = be32(ip + 16);
+
+    /* payload(): start = 20 + ipv4_options_length (ipv4.rs:226-231, saturating),
+     * end = min(start + ipv4_payload_length (ipv4.rs:241-243), len)
+     * (decorator.rs:728-753); empty if len <= start. */
+    size_t opts = (size_t)ihl * 4 > 20 ? (size_t)ihl * 4 - 20 : 0;
+    size_t start = 20 + opts;
+    size_t total_length = be16(ip + 2);
+    size_t plen = total_length > (size_t)ihl * 4 ? total_length - (size_t)ihl * 4 : 0;
+    slice_t l4 = { NULL, 0 };
+    if (ep.len > start) {
+        size_t end = start + plen;
+        if (end > ep.len) end = ep.len;
+        l4.p = ip + start;
+        l4.len = end - start;
+        r->l4_offset = (uint16_t)(14 + start);
+        r->l4_length = (uint16_t)l4.len;
+    }
+    l4_dispatch(r, 0, ip[9], l4, ip + 12, ip + 16);
+}
+
+/* packetdump.rs:170-183 handle_ipv6_packet */
+static void handle_ipv6(oracle_rec* r, slice_t ep) {
+    r->status |= ORACLE_ST_L3_IPV6;
+    if (ep.len < 40) { r->status |= ORACLE_ST_L3_MALFORMED; return; }  /* Ipv6Packet::new, min 40 */
+    const uint8_t* ip = ep.p;
+    r->ip_proto = ip[6];                                  /* next_header */
+    r->ttl = ip[7];                                       /* hop_limit */
+    memcpy(r->src_ipv6, ip + 8, 16);
+    memcpy(r->dst_ipv6, ip + 24, 16);
+    /* payload bounded by payload_length (ipv6.rs:34-36, #[length = "payload_length"]) */
+    size_t payload_length = be16(ip + 4);
+    slice_t l4 = { NULL, 0 };
+    if (ep.len > 40) {
+        size_t end = 40 + payload_length;
+        if (end > ep.len) end = ep.len;
+        l4.p = ip + 40;
+        l4.len = end - 40;
+        r->l4_offset = 14 + 40;
+        r->l4_length = (uint16_t)l4.len;
+    }
+    l4_dispatch(r, 1, ip[6], l4, ip + 8, ip + 24);
+}
+
+/* packetdump.rs:200-217 handle_ethernet_frame */
+void oracle_rx_frame(const uint8_t* frame, size_t len, oracle_rec* r) {
+    memset(r, 0, sizeof(*r));
+    if (len < 14) { r->status = ORACLE_ST_ETH_MALFORMED; return; }  /* EthernetPacket::new, min 14 */
+    r->ethertype = be16(frame + 12);                      /* ethernet.rs:27-28 */
+    slice_t ep = { frame + 14, len - 14 };                /* payload: last field, unbounded */
+    switch (r->ethertype) {
+    case 0x0800: handle_ipv4(r, ep); break;              /* EtherTypes::Ipv4, ethernet.rs:68 */
+    case 0x86DD: handle_ipv6(r, ep); break;              /* EtherTypes::Ipv6, ethernet.rs:88 */
+    default: r->status |= ORACLE_ST_UNKNOWN_ETHERTYPE; break;
+    }
+}
+
+/* ---- batch drivers ------------------------------------------------------ */
+
+typedef struct {
+    const uint8_t* buf; uint64_t buf_len; uint64_t lo, hi;
+    uint64_t first; uint32_t stride, frame_len;
+    const uint64_t* offsets; const uint32_t* lengths; oracle_rec* out;
+} shard_t;
+
+static void* rx_shard(void* arg) {
+    shard_t* s = (shard_t*)arg;
+    for (uint64_t i = s->lo; i < s->hi; ++i) {
+        uint64_t off = s->stride ? s->first + i * (uint64_t)s->stride : s->offsets[i];
+        uint64_t len = s->stride ? s->frame_len : s->lengths[i];
+        if (off > s->buf_len || len > s->buf_len - off) {
+            memset(&s->out[i], 0, sizeof(oracle_rec));
+            s->out[i].status = ORACLE_ST_DESC_INVALID;
+            continue;
+        }
+        oracle_rx_frame(s->buf + off, (size_t)len, &s->out[i]);
+    }
+    return NULL;
+}
+
+void oracle_rx_batch(const uint8_t* buf, uint64_t buf_len, uint64_t n,
+                     uint64_t first, uint32_t stride, uint32_t frame_len,
+                     const uint64_t* offsets, const uint32_t* lengths,
+                     oracle_rec* out, int nthreads) {
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 256) nthreads = 256;
+    shard_t sh[256];
+    pthread_t th[256];
+    for (int t = 0; t < nthreads; ++t) {
+        shard_t s = { buf, buf_len, n * (uint64_t)t / nthreads, n * (uint64_t)(t + 1) / nthreads,
+                      first, stride, frame_len, offsets, lengths, out };
+        sh[t] = s;
+    }
+    if (nthreads == 1) { rx_shard(&sh[0]); return; }
+    for (int t = 0; t < nthreads; ++t) pthread_create(&th[t], NULL, rx_shard, &sh[t]);
+    for (int t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
+}
+
+void oracle_checksum_slices(const uint8_t* buf, uint64_t n, const uint64_t* offsets,
+                            const uint32_t* lengths, const uint32_t* skipwords,
+                            uint16_t* out) {
+    for (uint64_t i = 0; i < n; ++i)
+        out[i] = oracle_checksum(buf + offsets[i], lengths[i], skipwords[i]);
+}
+
+size_t oracle_rec_size(void) { return sizeof(oracle_rec); }

@@ -1,0 +1,150 @@
+"""Independent pure-Python restatement of the receive path (small cases only).
+
+TEST INFRASTRUCTURE ONLY. A second, separately written restatement of the
+reference semantics used to cross-check the C oracle (oracle/pnet_oracle.c) on
+random and edge-case frames. Written from the reference, not from the C file:
+
+  sum_be_words      pnet_packet/src/util.rs:158-181
+  finalize          pnet_packet/src/util.rs:84-89
+  checksum          pnet_packet/src/util.rs:76-82
+  ipv4/ipv6_checksum pnet_packet/src/util.rs:92-154
+  receive dispatch  examples/packetdump.rs:120-217 + the #[packet] layouts
+"""
+
+ST_L3_IPV4 = 0x0001
+ST_L3_IPV6 = 0x0002
+ST_L4_UDP = 1 << 2
+ST_L4_TCP = 2 << 2
+ST_L4_ICMP = 3 << 2
+ST_L4_ICMPV6 = 4 << 2
+ST_ETH_MALFORMED = 0x0020
+ST_L3_MALFORMED = 0x0040
+ST_L4_MALFORMED = 0x0080
+ST_IP_CSUM_OK = 0x0100
+ST_L4_CSUM_DONE = 0x0200
+ST_L4_CSUM_OK = 0x0400
+ST_UNKNOWN_ETHERTYPE = 0x0800
+ST_UNKNOWN_PROTO = 0x1000
+ST_DESC_INVALID = 0x8000
+
+FIELDS = ("status", "ip_csum", "l4_csum", "ethertype", "ip_proto", "ttl", "l4_offset",
+          "l4_length", "src_port", "dst_port", "src_ipv4", "dst_ipv4", "src_ipv6", "dst_ipv6")
+
+
+def sum_be_words(d, skip):
+    d = bytes(d)
+    if not d:
+        return 0
+    words = [(d[2 * i] << 8) | d[2 * i + 1] for i in range(len(d) // 2)]
+    s = sum(w for i, w in enumerate(words) if i != skip)
+    if len(d) % 2 and len(d) // 2 != skip:
+        s += d[-1] << 8
+    return s & 0xFFFFFFFF
+
+
+def finalize(s):
+    while s >> 16:
+        s = (s >> 16) + (s & 0xFFFF)
+    return (~s) & 0xFFFF
+
+
+def checksum(d, skip):
+    return 0 if len(d) == 0 else finalize(sum_be_words(d, skip))
+
+
+def _segsum(addr):
+    a = bytes(addr)
+    return sum((a[i] << 8) | a[i + 1] for i in range(0, len(a), 2))
+
+
+def ipv4_checksum(d, skip, extra, src, dst, proto):
+    s = _segsum(src) + _segsum(dst) + proto + len(d) + len(extra)
+    s += sum_be_words(d, skip) + sum_be_words(extra, len(extra) // 2)
+    return finalize(s & 0xFFFFFFFF)
+
+
+ipv6_checksum = ipv4_checksum  # identical arithmetic over 8 segments per address
+
+
+def _be16(b, i):
+    return (b[i] << 8) | b[i + 1]
+
+
+def rx_frame(frame):
+    f = bytes(frame)
+    r = dict.fromkeys(FIELDS, 0)
+    r["src_ipv6"] = bytes(16)
+    r["dst_ipv6"] = bytes(16)
+    if len(f) < 14:
+        r["status"] = ST_ETH_MALFORMED
+        return r
+    et = _be16(f, 12)
+    r["ethertype"] = et
+    ep = f[14:]
+    st = 0
+    if et == 0x0800:
+        st |= ST_L3_IPV4
+        if len(ep) < 20:
+            r["status"] = st | ST_L3_MALFORMED
+            return r
+        ihl = ep[0] & 15
+        hl = min(max(ihl * 4, 20), len(ep))
+        r["ip_csum"] = checksum(ep[:hl], 5)
+        if r["ip_csum"] == _be16(ep, 10):
+            st |= ST_IP_CSUM_OK
+        r["ttl"], r["ip_proto"] = ep[8], ep[9]
+        r["src_ipv4"] = int.from_bytes(ep[12:16], "big")
+        r["dst_ipv4"] = int.from_bytes(ep[16:20], "big")
+        start = 20 + max(ihl * 4 - 20, 0)
+        plen = max(_be16(ep, 2) - ihl * 4, 0)
+        l4 = b""
+        if len(ep) > start:
+            l4 = ep[start:min(start + plen, len(ep))]
+            r["l4_offset"], r["l4_length"] = 14 + start, len(l4)
+        src, dst, proto, v6 = ep[12:16], ep[16:20], ep[9], False
+    elif et == 0x86DD:
+        st |= ST_L3_IPV6
+        if len(ep) < 40:
+            r["status"] = st | ST_L3_MALFORMED
+            return r
+        r["ip_proto"], r["ttl"] = ep[6], ep[7]
+        r["src_ipv6"], r["dst_ipv6"] = ep[8:24], ep[24:40]
+        l4 = b""
+        if len(ep) > 40:
+            l4 = ep[40:min(40 + _be16(ep, 4), len(ep))]
+            r["l4_offset"], r["l4_length"] = 54, len(l4)
+        src, dst, proto, v6 = ep[8:24], ep[24:40], ep[6], True
+    else:
+        r["status"] = ST_UNKNOWN_ETHERTYPE
+        return r
+
+    table = {17: (ST_L4_UDP, 8, 3, 6), 6: (ST_L4_TCP, 20, 8, 16),
+             1: (ST_L4_ICMP, 4, 1, 2), 58: (ST_L4_ICMPV6, 4, 1, 2)}
+    if proto not in table:
+        r["status"] = st | ST_UNKNOWN_PROTO
+        return r
+    kind, minlen, skip, csum_at = table[proto]
+    st |= kind
+    if len(l4) < minlen:
+        r["status"] = st | ST_L4_MALFORMED
+        return r
+    r["src_port"] = _be16(l4, 0)
+    if proto in (17, 6):
+        r["dst_port"] = _be16(l4, 2)
+    else:
+        r["dst_port"] = _be16(l4, 4) if len(l4) >= 8 else 0
+    c = None
+    if proto == 1:
+        c = checksum(l4, 1)
+    elif proto == 58:
+        if v6:
+            c = ipv6_checksum(l4, 1, b"", src, dst, 58)
+    else:
+        c = ipv4_checksum(l4, skip, b"", src, dst, proto)
+    if c is not None:
+        r["l4_csum"] = c
+        st |= ST_L4_CSUM_DONE
+        if c == _be16(l4, csum_at):
+            st |= ST_L4_CSUM_OK
+    r["status"] = st
+    return r
