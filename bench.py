@@ -1,0 +1,292 @@
+#!/usr/bin/env python3
+"""Benchmark: device-resident receive-path throughput (parse + verify) on MI355X.
+
+BASELINE.json metric: "device-resident Mpkts/s & GB/s, checksum+parse, 64B & 1500B,
+1/2/4/8 GPU". One step = one pnetgpu_rx_process launch over a resident batch:
+  primary   configs[1]  64-B Eth/IPv4/UDP, 2^24 frames (1 GiB) per GPU  -> `value`
+  secondary configs[2]  1500-B Eth/IPv4/TCP, 2^20 frames (1.5 GiB) per GPU
+Both write the full IPv4 record (status, both checksums, ethertype, proto, ttl,
+L4 offset/length, ports, addresses) plus counters. Multi-GPU: one process per
+GPU (torchrun), each with its own shard (weak scaling, no data-path collective);
+RCCL only all-reduces the counters once at the end and takes the max time.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu] [--no-e2e]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import libpnet_amd as lp  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (/opt/skills/guides/MI355X_MICROARCH.md:36)
+METRIC = "device-resident Mpkts/s & GB/s, checksum+parse, 64B & 1500B, 1/2/4/8 GPU"
+WORKLOADS = {
+    "udp64": {"n": 1 << 24, "desc": "configs[1]: 64B UDP/IPv4/Ethernet, checksum verify + header extract, "
+                                    "device-resident batch"},
+    "tcp1500": {"n": 1 << 20, "desc": "configs[2]: 1500B TCP/IPv4/Ethernet, full-MTU ones-complement sum over "
+                                      "pseudo-header+payload"},
+}
+KERNEL_NAME = "rx_kernel"
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+class Shard:
+    """One workload resident on this rank's GPU, with its result buffers."""
+
+    def __init__(self, name, n, seed, device):
+        self.name, self.n = name, n
+        w = lp.synth.make(name, n, seed=seed, corrupt_ppm=10000)
+        self.w = w
+        self.data = torch.from_numpy(w.buf).to(device)
+        self.offsets = self.lengths = None
+        if not w.stride:
+            self.offsets = torch.from_numpy(w.offsets.view(np.int64)).to(device)
+            self.lengths = torch.from_numpy(w.lengths.view(np.int32)).to(device)
+        self.res = lp.RxResult(n, device, lp.IPV4_COLUMNS, counters=True)
+        self.frame_bytes = w.expect["bytes"]
+        self.result_bytes = lp.column_bytes(lp.IPV4_COLUMNS)
+        self.desc_bytes = 0 if w.stride else 12          # u64 offset + u32 length
+        # algorithmic bytes per launch: frames read once + result columns written + descriptors
+        self.alg_bytes = self.frame_bytes + n * (self.result_bytes + self.desc_bytes)
+
+    def step(self, stream):
+        if self.w.stride:
+            lp.rx_process(self.data, stride=self.w.stride, frame_len=self.w.frame_len, n_frames=self.n,
+                          out=self.res, stream=stream)
+        else:
+            lp.rx_process(self.data, offsets=self.offsets, lengths=self.lengths, out=self.res, stream=stream)
+
+
+def time_shard(sh, steps, warmup, stream, dist_on):
+    for _ in range(warmup):
+        sh.step(stream)
+    stream.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    if dist_on:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for a, b in ev:
+        a.record(stream)
+        sh.step(stream)
+        b.record(stream)
+    stream.synchronize()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    if dist_on:
+        torch.distributed.barrier()
+    kern_ms = [a.elapsed_time(b) for a, b in ev]
+    return wall, kern_ms
+
+
+def check_counters(sh):
+    """Size-independent property: every planted corruption found, nothing else."""
+    sh.res.counters.zero_()
+    sh.step(torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    c = sh.res.counter_dict()
+    ok = (c["frames"] == sh.n and c["bytes"] == sh.w.expect["bytes"] and c["ip_csum_bad"] == sh.w.expect["ip_bad"]
+          and c["l4_csum_bad"] == sh.w.expect["l4_bad"] and c["malformed"] == 0 and c["unknown"] == 0)
+    return ok, c
+
+
+def cpu_baseline(sh, budget_cpu_s=12.0):
+    """The oracle (scalar C restatement, 'port') on this host's cores over a bounded sample."""
+    from oracle import coracle  # checker / baseline only
+    nthreads = min(16, os.cpu_count() or 1)
+    n = min(sh.n, 1 << 21)
+    w = sh.w
+    frames = 0
+    t0 = time.perf_counter()
+    reps = 0
+    while True:
+        if w.stride:
+            coracle.rx_batch(w.buf, n, stride=w.stride, frame_len=w.frame_len, nthreads=nthreads)
+        else:
+            coracle.rx_batch(w.buf, n, offsets=w.offsets[:n], lengths=w.lengths[:n], nthreads=nthreads)
+        frames += n
+        reps += 1
+        el = time.perf_counter() - t0
+        if el * nthreads >= budget_cpu_s or el > 30:
+            break
+    mpps = frames / el / 1e6
+    return {"value": round(mpps, 2), "unit": "Mpkts/s", "cores": nthreads, "kind": "port",
+            "gbps": round(frames * (w.expect["bytes"] / sh.n) / el / 1e9, 2),
+            "sample": f"first {n} frames of the same {sh.name} batch x{reps} passes ({el:.1f} s wall, "
+                      f"{nthreads} threads, oracle/pnet_oracle.c scalar per-frame restatement)"}
+
+
+def e2e_rate(sh, device, chunks=16, reps=3):
+    """PCIe-inclusive rate: pinned host frames -> H2D -> kernel -> D2H of the results,
+    double-buffered on two streams. Reported beside `value`, never as `value`."""
+    if not sh.w.stride:
+        return None
+    n, stride = sh.n, sh.w.stride
+    host = torch.from_numpy(sh.w.buf[: n * stride]).pin_memory()
+    per = n // chunks
+    streams = [torch.cuda.Stream(device), torch.cuda.Stream(device)]
+    dbuf = [torch.empty(per * stride + 32, dtype=torch.uint8, device=device) for _ in range(2)]
+    res = [lp.RxResult(per, device, lp.IPV4_COLUMNS, counters=False) for _ in range(2)]
+    hout = {c: torch.empty_like(t, device="cpu").pin_memory() for c, t in res[0].columns.items()}
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        for k in range(chunks):
+            s, j = streams[k % 2], k % 2
+            with torch.cuda.stream(s):
+                dbuf[j][: per * stride].copy_(host[k * per * stride:(k + 1) * per * stride], non_blocking=True)
+                lp.rx_process(dbuf[j], stride=stride, frame_len=stride, n_frames=per, out=res[j], stream=s)
+                for c, t in res[j].columns.items():
+                    hout[c].copy_(t, non_blocking=True)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    frames = reps * chunks * per
+    return {"mpkts_s": round(frames / el / 1e6, 1), "gb_s": round(frames * stride / el / 1e9, 2),
+            "note": "pinned host batch -> hipMemcpyAsync H2D -> rx kernel -> D2H of result columns, "
+                    f"{chunks} chunks double-buffered on 2 streams"}
+
+
+def load_traffic(workload):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/), if present."""
+    p = os.path.join(ROOT, "profiles", f"pmc_{workload}.json")
+    if not os.path.exists(p):
+        return None
+    try:
+        with open(p) as fh:
+            d = json.load(fh)
+        return d.get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workloads", default="udp64,tcp1500")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--seed", type=int, default=1)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist_on = world > 1
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+    if dist_on:
+        import datetime
+        torch.distributed.init_process_group("nccl", timeout=datetime.timedelta(minutes=10))
+
+    names = [w for w in args.workloads.split(",") if w]
+    results = {}
+    primary = names[0]
+    for name in names:
+        cfg = WORKLOADS[name]
+        t = time.perf_counter()
+        sh = Shard(name, cfg["n"], args.seed * 1000 + rank, device)
+        if rank == 0:
+            log(f"[bench] {name}: built {sh.n} frames ({sh.frame_bytes / 2**30:.2f} GiB) in {time.perf_counter() - t:.1f}s")
+        ok, ctr = check_counters(sh)
+        stream = torch.cuda.Stream(device)
+        wall, kern_ms = time_shard(sh, args.steps, args.warmup, stream, dist_on)
+        # counters: one RCCL all-reduce at the end (the "final throughput reduction")
+        ctr_t = torch.tensor([ctr[k] for k in lp.COUNTER_NAMES] + [int(ok)], dtype=torch.int64, device=device)
+        wall_t = torch.tensor([wall], dtype=torch.float64, device=device)
+        if dist_on:
+            torch.distributed.all_reduce(ctr_t, op=torch.distributed.ReduceOp.SUM)
+            torch.distributed.all_reduce(wall_t, op=torch.distributed.ReduceOp.MAX)
+        wall = float(wall_t.item())
+        frames_all = sh.n * world * args.steps
+        avg_ms = float(np.mean(kern_ms))
+        achieved = sh.alg_bytes / (avg_ms * 1e-3) / 1e9
+        results[name] = {
+            "sh": sh, "wall": wall, "ms_per_step": wall / args.steps * 1e3,
+            "mpkts_s": frames_all / wall / 1e6,
+            "gb_s": sh.frame_bytes * world * args.steps / wall / 1e9,
+            "kernel_avg_ms": avg_ms, "kernel_min_ms": float(np.min(kern_ms)),
+            "achieved_gbs": achieved, "counters_ok": bool(ctr_t[-1].item() == world),
+            "counters": {k: int(v) for k, v in zip(lp.COUNTER_NAMES, ctr_t[:-1].tolist())},
+        }
+        if rank == 0:
+            r = results[name]
+            log(f"[bench] {name}: {r['mpkts_s']:.1f} Mpkts/s, {r['gb_s']:.1f} GB/s frames, kernel avg "
+                f"{avg_ms:.3f} ms -> {achieved:.0f} GB/s algorithmic ({achieved / HBM_PEAK_GBS:.1%} of 8 TB/s), "
+                f"counters ok={r['counters_ok']}")
+
+    if rank == 0:
+        p = results[primary]
+        sh = p["sh"]
+        line = {
+            "metric": METRIC,
+            "value": round(p["mpkts_s"], 1),
+            "unit": "Mpkts/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(p["ms_per_step"], 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (seeded splitmix64 frames, 1% with one flipped byte; built by libpnet_amd.synth)",
+            "config": {
+                "workload": WORKLOADS[primary]["desc"],
+                "frames_per_gpu": sh.n,
+                "frame_bytes": sh.w.frame_len,
+                "batch_bytes_per_gpu": sh.frame_bytes,
+                "mode": "fixed-stride" if sh.w.stride else "descriptor",
+                "result_bytes_per_frame": sh.result_bytes,
+                "parallelism": f"shard-by-index x{world}",
+            },
+            "gb_s": round(p["gb_s"], 1),
+            "roofline": {
+                "bound": "hbm",
+                "achieved": round(p["achieved_gbs"], 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(p["achieved_gbs"] / HBM_PEAK_GBS, 4),
+                "traffic": load_traffic(primary),
+                "kernel": KERNEL_NAME,
+                "kernel_avg_ms": round(p["kernel_avg_ms"], 4),
+                "alg_bytes_per_launch": sh.alg_bytes,
+            },
+            "counters_ok": p["counters_ok"],
+            "workloads": {},
+        }
+        for name, r in results.items():
+            line["workloads"][name] = {
+                "mpkts_s": round(r["mpkts_s"], 1), "gb_s": round(r["gb_s"], 1),
+                "kernel_avg_ms": round(r["kernel_avg_ms"], 4),
+                "roofline_frac": round(r["achieved_gbs"] / HBM_PEAK_GBS, 4),
+                "achieved_gbs": round(r["achieved_gbs"], 1), "counters_ok": r["counters_ok"],
+                "traffic": load_traffic(name),
+            }
+        if world == 1 and not args.no_cpu:
+            line["cpu_baseline"] = cpu_baseline(sh)
+            for name, r in results.items():
+                if name != primary:
+                    line["workloads"][name]["cpu_baseline"] = cpu_baseline(r["sh"], budget_cpu_s=6.0)
+        if world == 1 and not args.no_e2e:
+            line["e2e_pcie"] = e2e_rate(sh, device)
+        print(json.dumps(line), flush=True)
+    if dist_on:
+        torch.distributed.barrier()
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,174 @@
+/*
+ * pnetgpu.h — C-ABI of the MI355X packet parse-and-checksum engine.
+ *
+ * This is the drop-in boundary for libpnet's per-packet receive hot path
+ * (SURVEY.md §8(b)). Plain pointers and sizes only: no HIP, torch or C++
+ * types in any signature (streams are passed as `void*` = hipStream_t).
+ *
+ * Which reference interface each entry point replaces:
+ *
+ *   pnetgpu_rx_process        the per-frame receive chain a libpnet user runs on
+ *                             every `DataLinkReceiver::next()` frame
+ *                             (pnet_datalink/src/lib.rs:227-230):
+ *                             EthernetPacket::new → get_ethertype →
+ *                             Ipv4Packet::new / Ipv6Packet::new → ipv4::checksum →
+ *                             payload() → UdpPacket/TcpPacket/IcmpPacket::new →
+ *                             udp|tcp::ipv4_checksum / ipv6_checksum, icmp::checksum,
+ *                             icmpv6::checksum  — examples/packetdump.rs:120-217,
+ *                             pnet_packet/src/ipv4.rs:165-178, udp.rs:34-56,104-126,
+ *                             tcp.rs:239-286, icmp.rs:70-75, icmpv6.rs:80-85,
+ *                             generated accessors pnet_macros/src/decorator.rs:1563-1670,
+ *                             payload bounds decorator.rs:713-769.
+ *   pnetgpu_checksum_slices   pnet_packet::util::checksum (pnet_packet/src/util.rs:76-82),
+ *                             re-exported as pnet::util::checksum (src/util.rs:11-12),
+ *                             over a batch of slices.
+ *   pnetgpu_ipv4_checksum_slices  pnet_packet::util::ipv4_checksum with empty
+ *                             extra_data (util.rs:92-117), batched.
+ *   pnetgpu_ipv6_checksum_slices  pnet_packet::util::ipv6_checksum with empty
+ *                             extra_data (util.rs:125-150), batched.
+ *
+ * Semantics are bit-exact with the reference: every
+ * checksum word and extracted field equals what the Rust code returns for the
+ * same bytes, including its clamps and saturations (IHL clamp, payload bounds
+ * min(start+len, buffer), odd trailing byte as high byte, skipped word).
+ *
+ * Conventions
+ *   - Return: 0 on success, a negative PNETGPU_E* code otherwise. No exceptions
+ *     cross the ABI. Work is enqueued on `stream` (NULL = the device's null
+ *     stream) and is complete only once that stream is synchronised.
+ *   - Ownership: the caller owns every buffer; the library never frees caller
+ *     memory. Device pointers must be device-accessible on the context's GPU.
+ *   - Granule rule: the engine reads frame bytes in aligned 16-byte granules,
+ *     so the allocation behind `data` must be readable up to
+ *     round_up(data + data_bytes, 16). (hipMalloc'd buffers always are.)
+ *   - Threading: a context is bound to one device; calls on one context may be
+ *     issued from one host thread at a time. Distinct contexts are independent.
+ *   - Malformed input never faults: frames whose descriptor falls outside
+ *     [0, data_bytes) get PNET_ST_DESC_INVALID, short frames get the
+ *     *_MALFORMED bits (the reference's `new()` returning None).
+ */
+#ifndef PNETGPU_H
+#define PNETGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PNETGPU_ABI_VERSION 1
+
+/* ---- return codes ------------------------------------------------------- */
+#define PNETGPU_OK        0
+#define PNETGPU_EINVAL   (-1)  /* bad argument (NULL, size overflow, ...)      */
+#define PNETGPU_ENODEV   (-2)  /* no HIP device / device index out of range    */
+#define PNETGPU_EHIP     (-3)  /* a HIP runtime call or kernel launch failed   */
+#define PNETGPU_ENOMEM   (-4)
+
+/* ---- per-frame status word (rx columns .status) ------------------------- */
+#define PNET_ST_L3_MASK           0x0003u  /* 1 = IPv4 (ethertype 0x0800), 2 = IPv6 (0x86DD) */
+#define PNET_ST_L3_IPV4           0x0001u
+#define PNET_ST_L3_IPV6           0x0002u
+#define PNET_ST_L4_SHIFT          2
+#define PNET_ST_L4_MASK           0x001Cu  /* dispatch on next_level_protocol / next_header */
+#define PNET_ST_L4_UDP            (1u << PNET_ST_L4_SHIFT)  /* 17 */
+#define PNET_ST_L4_TCP            (2u << PNET_ST_L4_SHIFT)  /* 6  */
+#define PNET_ST_L4_ICMP           (3u << PNET_ST_L4_SHIFT)  /* 1  */
+#define PNET_ST_L4_ICMPV6         (4u << PNET_ST_L4_SHIFT)  /* 58 */
+#define PNET_ST_ETH_MALFORMED     0x0020u  /* EthernetPacket::new == None (len < 14)   */
+#define PNET_ST_L3_MALFORMED      0x0040u  /* Ipv4Packet::new (< 20) / Ipv6Packet::new (< 40) == None */
+#define PNET_ST_L4_MALFORMED      0x0080u  /* Udp (< 8) / Tcp (< 20) / Icmp(v6) (< 4) new == None */
+#define PNET_ST_IP_CSUM_OK        0x0100u  /* ipv4::checksum(&ip) == ip.get_checksum() */
+#define PNET_ST_L4_CSUM_DONE      0x0200u  /* an L4 checksum was computed (l4_csum valid) */
+#define PNET_ST_L4_CSUM_OK        0x0400u  /* computed L4 checksum == stored field       */
+#define PNET_ST_UNKNOWN_ETHERTYPE 0x0800u
+#define PNET_ST_UNKNOWN_PROTO     0x1000u
+#define PNET_ST_DESC_INVALID      0x8000u  /* descriptor outside [0, data_bytes): not read */
+
+/* ---- batch-wide counters (rx columns .counters, uint64 each, accumulated) */
+#define PNETGPU_CTR_FRAMES        0  /* frames with a valid descriptor            */
+#define PNETGPU_CTR_BYTES         1  /* sum of their lengths                      */
+#define PNETGPU_CTR_IPV4          2
+#define PNETGPU_CTR_IPV6          3
+#define PNETGPU_CTR_IP_CSUM_BAD   4  /* IPv4 parsed and header checksum mismatch  */
+#define PNETGPU_CTR_L4_CSUM_BAD   5  /* L4 checksum computed and mismatch         */
+#define PNETGPU_CTR_MALFORMED     6  /* any *_MALFORMED or DESC_INVALID           */
+#define PNETGPU_CTR_UNKNOWN       7  /* unknown ethertype or protocol             */
+#define PNETGPU_NCOUNTERS         8
+
+typedef struct pnetgpu_ctx pnetgpu_ctx;
+
+/*
+ * A batch of Ethernet frames (no FCS) resident in device memory.
+ *   stride > 0 : fixed-stride mode, frame i = data[first_offset + i*stride, +frame_len)
+ *   stride == 0: descriptor mode,  frame i = data[offsets[i], +lengths[i])
+ */
+typedef struct pnetgpu_batch {
+    const uint8_t*  data;         /* device pointer to frame bytes                 */
+    uint64_t        data_bytes;   /* bytes of `data` frames may occupy             */
+    uint64_t        n_frames;
+    uint64_t        first_offset; /* stride mode only                              */
+    uint32_t        stride;       /* > 0 selects fixed-stride mode                 */
+    uint32_t        frame_len;    /* stride mode: length of every frame            */
+    const uint64_t* offsets;      /* descriptor mode: device array [n_frames]      */
+    const uint32_t* lengths;      /* descriptor mode: device array [n_frames]      */
+} pnetgpu_batch;
+
+/*
+ * Result columns (struct of arrays, one element per frame, device pointers).
+ * Any column may be NULL (not written). Field values are those of the
+ * reference's generated getters for the view the dispatch reached, 0 otherwise.
+ */
+typedef struct pnetgpu_rx_columns {
+    uint16_t* status;     /* PNET_ST_* bits                                        */
+    uint16_t* ip_csum;    /* ipv4::checksum(&ip) (IPv4 only)                       */
+    uint16_t* l4_csum;    /* udp/tcp ipv4|ipv6_checksum, icmp::checksum, icmpv6::checksum */
+    uint16_t* ethertype;  /* EthernetPacket::get_ethertype                         */
+    uint8_t*  ip_proto;   /* get_next_level_protocol (v4) / get_next_header (v6)   */
+    uint8_t*  ttl;        /* get_ttl (v4) / get_hop_limit (v6)                     */
+    uint16_t* l4_offset;  /* frame offset of ip.payload() (0 when it is empty)     */
+    uint16_t* l4_length;  /* ip.payload().len()                                    */
+    uint16_t* src_port;   /* UDP/TCP get_source; ICMP(v6): type<<8 | code          */
+    uint16_t* dst_port;   /* UDP/TCP get_destination; ICMP(v6): BE16 at +4 if len>=8 */
+    uint32_t* src_ipv4;   /* get_source octets as a big-endian-valued u32          */
+    uint32_t* dst_ipv4;
+    uint8_t*  src_ipv6;   /* [n_frames][16] Ipv6 get_source octets (16-B aligned)   */
+    uint8_t*  dst_ipv6;   /* [n_frames][16]                                        */
+    uint64_t* counters;   /* [PNETGPU_NCOUNTERS], atomically accumulated           */
+} pnetgpu_rx_columns;
+
+int         pnetgpu_abi_version(void);
+const char* pnetgpu_strerror(int code);
+int         pnetgpu_device_count(int* count);
+
+int  pnetgpu_ctx_create(int device, pnetgpu_ctx** out);
+void pnetgpu_ctx_destroy(pnetgpu_ctx* ctx);
+
+/* Receive path: parse + verify every frame of `batch`, write `cols`. */
+int pnetgpu_rx_process(pnetgpu_ctx* ctx, const pnetgpu_batch* batch,
+                       const pnetgpu_rx_columns* cols, void* stream);
+
+/* out[i] = util::checksum(data[offsets[i], +lengths[i]), skipwords[i]) */
+int pnetgpu_checksum_slices(pnetgpu_ctx* ctx, const uint8_t* data, uint64_t data_bytes,
+                            uint64_t n, const uint64_t* offsets, const uint32_t* lengths,
+                            const uint32_t* skipwords, uint16_t* out, void* stream);
+
+/* out[i] = util::ipv4_checksum(slice_i, skipwords[i], &[], src_i, dst_i, protos[i]);
+ * addrs: [n][8] = src octets || dst octets. */
+int pnetgpu_ipv4_checksum_slices(pnetgpu_ctx* ctx, const uint8_t* data, uint64_t data_bytes,
+                                 uint64_t n, const uint64_t* offsets, const uint32_t* lengths,
+                                 const uint32_t* skipwords, const uint8_t* addrs,
+                                 const uint8_t* protos, uint16_t* out, void* stream);
+
+/* out[i] = util::ipv6_checksum(slice_i, skipwords[i], &[], src_i, dst_i, protos[i]);
+ * addrs: [n][32] = src octets || dst octets. */
+int pnetgpu_ipv6_checksum_slices(pnetgpu_ctx* ctx, const uint8_t* data, uint64_t data_bytes,
+                                 uint64_t n, const uint64_t* offsets, const uint32_t* lengths,
+                                 const uint32_t* skipwords, const uint8_t* addrs,
+                                 const uint8_t* protos, uint16_t* out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PNETGPU_H */

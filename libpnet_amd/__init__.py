@@ -1,0 +1,14 @@
+"""libpnet_amd — MI355X-native engine for libpnet's per-packet receive hot path.
+
+Ethernet/IPv4/IPv6 header extraction + ones-complement Internet checksums
+(UDP/TCP/ICMP/ICMPv6) over device-resident frame batches, bit-exact with
+pnet_packet. The product is libpnetgpu.so (HIP kernels behind the C-ABI in
+include/pnetgpu.h); this package is its Python host binding.
+"""
+from ._lib import DEFS, LIB_PATH, PnetGpuError, lib  # noqa: F401  (fails loudly if the .so is absent)
+from . import synth  # noqa: F401
+from .engine import (ALL_COLUMNS, COUNTER_NAMES, IPV4_COLUMNS, Context, RxResult,  # noqa: F401
+                     checksum_slices, column_bytes, context, ipv4_checksum_slices,
+                     ipv6_checksum_slices, rx_process)
+
+__version__ = "0.1.0"

@@ -1,0 +1,98 @@
+"""ctypes binding of libpnetgpu.so (include/pnetgpu.h, include/pnetgpu_synth.h).
+
+The in-tree shared library is the only implementation: if it is missing or
+fails to load, importing libpnet_amd raises — there is no CPU fallback.
+"""
+import ctypes
+import os
+import re
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG_DIR)
+LIB_PATH = os.path.join(PKG_DIR, "libpnetgpu.so")
+HEADERS = [os.path.join(ROOT, "include", "pnetgpu.h"), os.path.join(ROOT, "include", "pnetgpu_synth.h")]
+
+
+class PnetGpuError(RuntimeError):
+    def __init__(self, code, what=""):
+        self.code = code
+        msg = _lib.pnetgpu_strerror(code).decode() if _lib is not None else str(code)
+        super().__init__(f"{what}: pnetgpu error {code} ({msg})")
+
+
+def _header_defines():
+    """Integer #define constants of the public headers (the ABI's numbers)."""
+    out = {}
+    for h in HEADERS:
+        with open(h) as fh:
+            for line in fh:
+                m = re.match(r"#define\s+(P[A-Z0-9_]+)\s+([^/]+?)\s*(/\*.*)?$", line)
+                if not m:
+                    continue
+                expr = re.sub(r"\b(0[xX][0-9a-fA-F]+|\d+)[uU]\b", r"\1", m.group(2))
+                if not re.fullmatch(r"[\w\s()<>|+-]+", expr):
+                    continue
+                try:
+                    out[m.group(1)] = int(eval(expr, {"__builtins__": {}}, dict(out)))
+                except Exception:
+                    pass
+    return out
+
+
+DEFS = _header_defines()
+
+
+class Batch(ctypes.Structure):
+    _fields_ = [("data", ctypes.c_void_p), ("data_bytes", ctypes.c_uint64), ("n_frames", ctypes.c_uint64),
+                ("first_offset", ctypes.c_uint64), ("stride", ctypes.c_uint32), ("frame_len", ctypes.c_uint32),
+                ("offsets", ctypes.c_void_p), ("lengths", ctypes.c_void_p)]
+
+
+COLUMN_NAMES = ("status", "ip_csum", "l4_csum", "ethertype", "ip_proto", "ttl", "l4_offset", "l4_length",
+                "src_port", "dst_port", "src_ipv4", "dst_ipv4", "src_ipv6", "dst_ipv6")
+
+
+class RxColumns(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_void_p) for n in COLUMN_NAMES] + [("counters", ctypes.c_void_p)]
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"libpnet_amd: native library {LIB_PATH} is not built "
+                          "(run `python -c 'import __graft_entry__ as g; g.build()'` or `make -C libpnet_amd`)")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, u64, u32, i32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int
+    L.pnetgpu_abi_version.restype = i32
+    L.pnetgpu_strerror.restype = ctypes.c_char_p
+    L.pnetgpu_strerror.argtypes = [i32]
+    L.pnetgpu_device_count.restype = i32
+    L.pnetgpu_device_count.argtypes = [ctypes.POINTER(i32)]
+    L.pnetgpu_ctx_create.restype = i32
+    L.pnetgpu_ctx_create.argtypes = [i32, ctypes.POINTER(vp)]
+    L.pnetgpu_ctx_destroy.restype = None
+    L.pnetgpu_ctx_destroy.argtypes = [vp]
+    L.pnetgpu_rx_process.restype = i32
+    L.pnetgpu_rx_process.argtypes = [vp, ctypes.POINTER(Batch), ctypes.POINTER(RxColumns), vp]
+    L.pnetgpu_checksum_slices.restype = i32
+    L.pnetgpu_checksum_slices.argtypes = [vp, vp, u64, u64, vp, vp, vp, vp, vp]
+    for f in (L.pnetgpu_ipv4_checksum_slices, L.pnetgpu_ipv6_checksum_slices):
+        f.restype = i32
+        f.argtypes = [vp, vp, u64, u64, vp, vp, vp, vp, vp, vp, vp]
+    L.pnetgpu_synth_layout.restype = i32
+    L.pnetgpu_synth_layout.argtypes = [i32, u64, u64, ctypes.POINTER(u64), ctypes.POINTER(u32),
+                                       ctypes.POINTER(u32)]
+    L.pnetgpu_synth_fill.restype = i32
+    L.pnetgpu_synth_fill.argtypes = [i32, u64, u64, u32, vp, u64, vp, vp, vp, i32]
+    if L.pnetgpu_abi_version() != DEFS["PNETGPU_ABI_VERSION"]:
+        raise ImportError("libpnet_amd: libpnetgpu.so ABI version does not match include/pnetgpu.h")
+    return L
+
+
+_lib = None
+_lib = _load()
+lib = _lib
+
+
+def check(rc, what):
+    if rc != 0:
+        raise PnetGpuError(rc, what)

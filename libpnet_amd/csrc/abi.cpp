@@ -1,0 +1,178 @@
+// abi.cpp — C-ABI entry points of libpnetgpu.so (include/pnetgpu.h).
+//
+// Validates arguments, binds the context's device, sizes the persistent grid
+// and launches the HIP kernels of rx_kernel.hip. No compute happens on the
+// host: there is no CPU fallback path in this library.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <new>
+
+#include "pnetgpu.h"
+#include "rx_internal.h"
+
+struct pnetgpu_ctx {
+    int device;
+    int cus;
+};
+
+namespace {
+
+constexpr int kBlock = 256;
+constexpr int kRunFrames = 64;      // frames per wave-run
+constexpr int kWavesPerBlock = 4;
+
+int set_device(const pnetgpu_ctx* ctx) {
+    return hipSetDevice(ctx->device) == hipSuccess ? PNETGPU_OK : PNETGPU_EHIP;
+}
+
+// Aligns the frame base down to 16 B; offsets are shifted by the remainder.
+void align_base(const uint8_t* data, uint64_t bytes, const uint8_t** al, uint64_t* delta,
+                uint64_t* limit) {
+    const uintptr_t p = reinterpret_cast<uintptr_t>(data);
+    *delta = p & 15u;
+    *al = reinterpret_cast<const uint8_t*>(p - *delta);
+    *limit = bytes + *delta;
+}
+
+}  // namespace
+
+extern "C" {
+
+int pnetgpu_abi_version(void) { return PNETGPU_ABI_VERSION; }
+
+const char* pnetgpu_strerror(int code) {
+    switch (code) {
+        case PNETGPU_OK: return "ok";
+        case PNETGPU_EINVAL: return "invalid argument";
+        case PNETGPU_ENODEV: return "no such HIP device";
+        case PNETGPU_EHIP: return "HIP runtime or kernel launch failure";
+        case PNETGPU_ENOMEM: return "out of memory";
+        default: return "unknown pnetgpu error";
+    }
+}
+
+int pnetgpu_device_count(int* count) {
+    if (!count) return PNETGPU_EINVAL;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) {
+        *count = 0;
+        return PNETGPU_ENODEV;
+    }
+    *count = n;
+    return PNETGPU_OK;
+}
+
+int pnetgpu_ctx_create(int device, pnetgpu_ctx** out) {
+    if (!out) return PNETGPU_EINVAL;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return PNETGPU_ENODEV;
+    if (hipSetDevice(device) != hipSuccess) return PNETGPU_EHIP;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return PNETGPU_EHIP;
+    auto* c = new (std::nothrow) pnetgpu_ctx;
+    if (!c) return PNETGPU_ENOMEM;
+    c->device = device;
+    c->cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+    *out = c;
+    return PNETGPU_OK;
+}
+
+void pnetgpu_ctx_destroy(pnetgpu_ctx* ctx) { delete ctx; }
+
+int pnetgpu_rx_process(pnetgpu_ctx* ctx, const pnetgpu_batch* b, const pnetgpu_rx_columns* cols,
+                       void* stream) {
+    if (!ctx || !b || !cols) return PNETGPU_EINVAL;
+    if (b->n_frames == 0) return PNETGPU_OK;
+    if (!b->data) return PNETGPU_EINVAL;
+    if (b->stride == 0 && (!b->offsets || !b->lengths)) return PNETGPU_EINVAL;
+    if ((cols->src_ipv6 && (reinterpret_cast<uintptr_t>(cols->src_ipv6) & 15)) ||
+        (cols->dst_ipv6 && (reinterpret_cast<uintptr_t>(cols->dst_ipv6) & 15)))
+        return PNETGPU_EINVAL;
+    if (b->n_frames > (UINT64_MAX - kRunFrames) / 2) return PNETGPU_EINVAL;
+    int rc = set_device(ctx);
+    if (rc) return rc;
+
+    pnetgpu::RxArgs a{};
+    align_base(b->data, b->data_bytes, &a.data, &a.delta, &a.limit);
+    a.n = b->n_frames;
+    a.first = b->first_offset;
+    a.stride = b->stride;
+    a.frame_len = b->frame_len;
+    a.offsets = b->offsets;
+    a.lengths = b->lengths;
+    a.cols = *cols;
+    a.nruns = (a.n + kRunFrames - 1) / kRunFrames;
+
+    // Window width: 4 granules when every frame spans at most 64 aligned bytes
+    // (fixed stride, known alignment), else 8 (covers the longest header, 94 B).
+    int nw = 8, g = 16;
+    if (b->stride) {
+        const uint64_t sh = (a.delta + b->first_offset) & 15u;
+        const bool sh_fixed = (b->stride % 16) == 0;
+        const uint64_t worst_sh = sh_fixed ? sh : 15u;
+        const uint64_t span = b->frame_len ? (worst_sh + b->frame_len + 15) / 16 : 0;
+        if (span <= 4) nw = 4;
+        if (b->frame_len >= 4096) g = 64;
+        else if (b->frame_len <= 256) g = 4;
+    }
+    const int per_cu = pnetgpu::rx_blocks_per_cu(nw, g);
+    const uint64_t want = (a.nruns + kWavesPerBlock - 1) / kWavesPerBlock;
+    const uint64_t cap = (uint64_t)ctx->cus * (uint64_t)per_cu;
+    const int blocks = (int)std::max<uint64_t>(1, std::min(want, cap));
+    if (pnetgpu::launch_rx(a, nw, g, blocks, static_cast<hipStream_t>(stream)) != 0) return PNETGPU_EHIP;
+    return PNETGPU_OK;
+}
+
+static int slices_common(pnetgpu_ctx* ctx, const uint8_t* data, uint64_t data_bytes, uint64_t n,
+                         const uint64_t* offsets, const uint32_t* lengths, const uint32_t* skipwords,
+                         const uint8_t* addrs, const uint8_t* protos, uint16_t* out, int pseudo,
+                         void* stream) {
+    if (!ctx) return PNETGPU_EINVAL;
+    if (n == 0) return PNETGPU_OK;
+    if (!data || !offsets || !lengths || !skipwords || !out) return PNETGPU_EINVAL;
+    if (pseudo && (!addrs || !protos)) return PNETGPU_EINVAL;
+    int rc = set_device(ctx);
+    if (rc) return rc;
+    pnetgpu::SliceArgs a{};
+    align_base(data, data_bytes, &a.data, &a.delta, &a.limit);
+    a.n = n;
+    a.offsets = offsets;
+    a.lengths = lengths;
+    a.skipwords = skipwords;
+    a.addrs = addrs;
+    a.protos = protos;
+    a.out = out;
+    const uint64_t groups_per_block = kBlock / 16;
+    const uint64_t want = (n + groups_per_block - 1) / groups_per_block;
+    const int blocks = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)ctx->cus * 8));
+    if (pnetgpu::launch_slices(a, pseudo, blocks, static_cast<hipStream_t>(stream)) != 0) return PNETGPU_EHIP;
+    return PNETGPU_OK;
+}
+
+int pnetgpu_checksum_slices(pnetgpu_ctx* ctx, const uint8_t* data, uint64_t data_bytes, uint64_t n,
+                            const uint64_t* offsets, const uint32_t* lengths, const uint32_t* skipwords,
+                            uint16_t* out, void* stream) {
+    return slices_common(ctx, data, data_bytes, n, offsets, lengths, skipwords, nullptr, nullptr, out, 0,
+                         stream);
+}
+
+int pnetgpu_ipv4_checksum_slices(pnetgpu_ctx* ctx, const uint8_t* data, uint64_t data_bytes, uint64_t n,
+                                 const uint64_t* offsets, const uint32_t* lengths,
+                                 const uint32_t* skipwords, const uint8_t* addrs, const uint8_t* protos,
+                                 uint16_t* out, void* stream) {
+    return slices_common(ctx, data, data_bytes, n, offsets, lengths, skipwords, addrs, protos, out, 4,
+                         stream);
+}
+
+int pnetgpu_ipv6_checksum_slices(pnetgpu_ctx* ctx, const uint8_t* data, uint64_t data_bytes, uint64_t n,
+                                 const uint64_t* offsets, const uint32_t* lengths,
+                                 const uint32_t* skipwords, const uint8_t* addrs, const uint8_t* protos,
+                                 uint16_t* out, void* stream) {
+    return slices_common(ctx, data, data_bytes, n, offsets, lengths, skipwords, addrs, protos, out, 16,
+                         stream);
+}
+
+}  // extern "C"

@@ -1,0 +1,43 @@
+// rx_internal.h — launch arguments shared by the C-ABI layer and the kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "pnetgpu.h"
+
+namespace pnetgpu {
+
+// `data` is 16-B aligned; every descriptor offset is shifted by `delta` (the
+// caller pointer's misalignment) and must satisfy off + len <= limit.
+struct RxArgs {
+    const uint8_t* data;
+    uint64_t delta;
+    uint64_t limit;
+    uint64_t n;
+    uint64_t first;
+    uint32_t stride;
+    uint32_t frame_len;
+    const uint64_t* offsets;
+    const uint32_t* lengths;
+    uint64_t nruns;          // ceil(n / 64): one wave per run of 64 frames
+    pnetgpu_rx_columns cols;
+};
+
+struct SliceArgs {
+    const uint8_t* data;
+    uint64_t delta;
+    uint64_t limit;
+    uint64_t n;
+    const uint64_t* offsets;
+    const uint32_t* lengths;
+    const uint32_t* skipwords;
+    const uint8_t* addrs;
+    const uint8_t* protos;
+    uint16_t* out;
+};
+
+int rx_blocks_per_cu(int nw, int g);
+int launch_rx(const RxArgs& args, int nw, int g, int blocks, hipStream_t stream);
+int launch_slices(const SliceArgs& args, int pseudo, int blocks, hipStream_t stream);
+
+}  // namespace pnetgpu

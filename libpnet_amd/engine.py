@@ -1,0 +1,196 @@
+"""Host-side engine over the C-ABI: the batched receive path and batched checksums.
+
+Mirrors the reference's operator surface for this path:
+
+  rx_process(...)            — the per-frame chain packetdump.rs:120-217 runs
+                               (EthernetPacket::new → Ipv4/Ipv6Packet::new →
+                               ipv4::checksum → payload() → Udp/Tcp/IcmpPacket::new →
+                               udp/tcp::ipv4_checksum|ipv6_checksum, icmp(v6)::checksum),
+                               for a whole device-resident batch at once.
+  checksum_slices(...)       — pnet_packet::util::checksum           (util.rs:76-82)
+  ipv4_checksum_slices(...)  — pnet_packet::util::ipv4_checksum      (util.rs:92-117)
+  ipv6_checksum_slices(...)  — pnet_packet::util::ipv6_checksum      (util.rs:125-150)
+
+Device memory and streams come from PyTorch (plumbing only); all compute is the
+HIP kernels of libpnetgpu.so. Unsigned columns are stored in signed torch dtypes
+of the same width; RxResult.numpy() returns the unsigned views.
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from ._lib import COLUMN_NAMES, DEFS, Batch, RxColumns, check, lib
+
+# column -> (torch storage dtype, numpy view dtype, trailing shape)
+COLUMNS = {
+    "status": (torch.int16, np.uint16, ()),
+    "ip_csum": (torch.int16, np.uint16, ()),
+    "l4_csum": (torch.int16, np.uint16, ()),
+    "ethertype": (torch.int16, np.uint16, ()),
+    "ip_proto": (torch.uint8, np.uint8, ()),
+    "ttl": (torch.uint8, np.uint8, ()),
+    "l4_offset": (torch.int16, np.uint16, ()),
+    "l4_length": (torch.int16, np.uint16, ()),
+    "src_port": (torch.int16, np.uint16, ()),
+    "dst_port": (torch.int16, np.uint16, ()),
+    "src_ipv4": (torch.int32, np.uint32, ()),
+    "dst_ipv4": (torch.int32, np.uint32, ()),
+    "src_ipv6": (torch.uint8, np.uint8, (16,)),
+    "dst_ipv6": (torch.uint8, np.uint8, (16,)),
+}
+assert tuple(COLUMNS) == COLUMN_NAMES
+
+#: every IPv4-relevant column: the bench's "checksum verify + header extract" record
+IPV4_COLUMNS = tuple(c for c in COLUMN_NAMES if not c.endswith("ipv6"))
+ALL_COLUMNS = COLUMN_NAMES
+NCOUNTERS = DEFS["PNETGPU_NCOUNTERS"]
+COUNTER_NAMES = ("frames", "bytes", "ipv4", "ipv6", "ip_csum_bad", "l4_csum_bad", "malformed", "unknown")
+
+
+def column_bytes(columns):
+    """Result bytes written per frame for a column set (the R of the roofline)."""
+    out = 0
+    for c in columns:
+        dt, npdt, shape = COLUMNS[c]
+        out += np.dtype(npdt).itemsize * int(np.prod(shape or (1,)))
+    return out
+
+
+class Context:
+    """One pnetgpu_ctx bound to a HIP device."""
+
+    def __init__(self, device=0):
+        self.device = int(device)
+        h = ctypes.c_void_p()
+        check(lib.pnetgpu_ctx_create(self.device, ctypes.byref(h)), "pnetgpu_ctx_create")
+        self.handle = h
+
+    def close(self):
+        if getattr(self, "handle", None):
+            lib.pnetgpu_ctx_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+_contexts = {}
+
+
+def context(device=None):
+    if device is None:
+        device = torch.cuda.current_device()
+    device = torch.device("cuda", device).index if not isinstance(device, int) else device
+    if device not in _contexts:
+        _contexts[device] = Context(device)
+    return _contexts[device]
+
+
+def _stream_handle(stream, device):
+    s = stream if stream is not None else torch.cuda.current_stream(device)
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+class RxResult:
+    """Device-resident result columns of one rx_process call."""
+
+    def __init__(self, n, device, columns=IPV4_COLUMNS, counters=True):
+        self.n = n
+        self.columns = {}
+        for c in columns:
+            dt, _, shape = COLUMNS[c]
+            self.columns[c] = torch.empty((n,) + shape, dtype=dt, device=device)
+        self.counters = torch.zeros(NCOUNTERS, dtype=torch.int64, device=device) if counters else None
+
+    def c_struct(self):
+        cols = RxColumns()
+        for c in COLUMN_NAMES:
+            setattr(cols, c, self.columns[c].data_ptr() if c in self.columns else 0)
+        cols.counters = self.counters.data_ptr() if self.counters is not None else 0
+        return cols
+
+    def numpy(self):
+        out = {}
+        for c, t in self.columns.items():
+            out[c] = t.cpu().numpy().view(COLUMNS[c][1])
+        return out
+
+    def counter_dict(self):
+        if self.counters is None:
+            return {}
+        v = self.counters.cpu().numpy().view(np.uint64)
+        return dict(zip(COUNTER_NAMES, (int(x) for x in v)))
+
+
+def _check_u8_cuda(t, what):
+    if not (isinstance(t, torch.Tensor) and t.is_cuda and t.dtype == torch.uint8 and t.is_contiguous()):
+        raise TypeError(f"{what} must be a contiguous torch.uint8 CUDA tensor")
+
+
+def rx_process(data, *, n_frames=None, stride=0, frame_len=None, first_offset=0, offsets=None, lengths=None,
+               columns=IPV4_COLUMNS, counters=True, out=None, stream=None, data_bytes=None):
+    """Parse + verify every frame of a device-resident batch.
+
+    Fixed-stride mode: stride > 0, frame i = data[first_offset + i*stride, +frame_len).
+    Descriptor mode:   offsets (int64) / lengths (int32) CUDA tensors, frame i = data[off_i, +len_i).
+    Returns an RxResult (device columns, accumulated counters)."""
+    _check_u8_cuda(data, "data")
+    if stride:
+        if n_frames is None:
+            n_frames = (data.numel() - first_offset) // stride
+        if frame_len is None:
+            frame_len = stride
+    else:
+        if offsets is None or lengths is None:
+            raise ValueError("descriptor mode needs offsets and lengths")
+        if n_frames is None:
+            n_frames = offsets.numel()
+        if offsets.dtype != torch.int64 or lengths.dtype != torch.int32 or not offsets.is_cuda:
+            raise TypeError("offsets must be int64 and lengths int32 CUDA tensors")
+        frame_len = 0
+    if out is None:
+        out = RxResult(n_frames, data.device, columns, counters)
+    b = Batch(data.data_ptr(), data.numel() if data_bytes is None else data_bytes, n_frames, first_offset,
+              stride, frame_len, offsets.data_ptr() if offsets is not None else 0,
+              lengths.data_ptr() if lengths is not None else 0)
+    cols = out.c_struct()
+    ctx = context(data.device.index)
+    check(lib.pnetgpu_rx_process(ctx.handle, ctypes.byref(b), ctypes.byref(cols),
+                                 _stream_handle(stream, data.device)), "pnetgpu_rx_process")
+    return out
+
+
+def _slices(fn_name, data, offsets, lengths, skipwords, addrs=None, protos=None, stream=None):
+    _check_u8_cuda(data, "data")
+    n = offsets.numel()
+    out = torch.empty(n, dtype=torch.int16, device=data.device)
+    ctx = context(data.device.index)
+    args = [ctx.handle, _ptr(data), data.numel(), n, _ptr(offsets), _ptr(lengths), _ptr(skipwords)]
+    if addrs is not None:
+        args += [_ptr(addrs), _ptr(protos)]
+    args += [_ptr(out), _stream_handle(stream, data.device)]
+    check(getattr(lib, fn_name)(*args), fn_name)
+    return out
+
+
+def checksum_slices(data, offsets, lengths, skipwords, stream=None):
+    """out[i] = util::checksum(data[off_i, +len_i), skipwords[i]) (uint16 in an int16 tensor)."""
+    return _slices("pnetgpu_checksum_slices", data, offsets, lengths, skipwords, stream=stream)
+
+
+def ipv4_checksum_slices(data, offsets, lengths, skipwords, addrs, protos, stream=None):
+    """util::ipv4_checksum per slice; addrs uint8 [n, 8] (src||dst), protos uint8 [n]."""
+    return _slices("pnetgpu_ipv4_checksum_slices", data, offsets, lengths, skipwords, addrs, protos, stream)
+
+
+def ipv6_checksum_slices(data, offsets, lengths, skipwords, addrs, protos, stream=None):
+    """util::ipv6_checksum per slice; addrs uint8 [n, 32] (src||dst), protos uint8 [n]."""
+    return _slices("pnetgpu_ipv6_checksum_slices", data, offsets, lengths, skipwords, addrs, protos, stream)

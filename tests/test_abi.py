@@ -1,0 +1,74 @@
+"""CPU checks of the drop-in boundary: the C-ABI library loads, exports every
+function the public headers declare, agrees with the oracle on the status/record
+constants, and rejects bad arguments — without making any compute call."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+import libpnet_amd as lp
+from libpnet_amd import _lib
+from oracle import coracle
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_functions():
+    names = set()
+    for h in _lib.HEADERS:
+        src = open(h).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        names |= set(re.findall(r"\b(pnetgpu_\w+)\s*\(", src))
+    return sorted(names)
+
+
+def test_exports_every_declared_symbol():
+    out = subprocess.run(["nm", "-D", "--defined-only", lp.LIB_PATH], capture_output=True, text=True,
+                         check=True).stdout
+    exported = set(re.findall(r"\bT (\w+)", out))
+    decl = declared_functions()
+    assert len(decl) >= 11
+    missing = [d for d in decl if d not in exported]
+    assert not missing, missing
+    for d in decl:
+        assert hasattr(lp.lib, d)
+
+
+def test_abi_version_and_strerror():
+    assert lp.lib.pnetgpu_abi_version() == lp.DEFS["PNETGPU_ABI_VERSION"] == 1
+    for code in (0, -1, -2, -3, -4, -99):
+        assert lp.lib.pnetgpu_strerror(code)
+
+
+def test_status_constants_match_oracle():
+    hdr = open(os.path.join(ROOT, "oracle", "pnet_oracle.h")).read()
+    for name, val in re.findall(r"#define (ORACLE_ST_\w+)\s+(0x[0-9a-fA-F]+)u", hdr):
+        assert lp.DEFS["PNET_ST_" + name[len("ORACLE_ST_"):]] == int(val, 16), name
+
+
+def test_column_dtypes_match_oracle_record():
+    from libpnet_amd.engine import COLUMNS
+    for c, (_, npdt, shape) in COLUMNS.items():
+        f = coracle.REC_DTYPE.fields[c][0]
+        assert f.base.itemsize == __import__("numpy").dtype(npdt).itemsize, c
+        assert tuple(f.shape) == tuple(shape), c
+
+
+def test_argument_validation_without_gpu():
+    L = lp.lib
+    assert L.pnetgpu_ctx_create(0, None) == lp.DEFS["PNETGPU_EINVAL"]
+    assert L.pnetgpu_device_count(None) == lp.DEFS["PNETGPU_EINVAL"]
+    assert L.pnetgpu_rx_process(None, None, None, None) == lp.DEFS["PNETGPU_EINVAL"]
+    assert L.pnetgpu_checksum_slices(None, None, 0, 0, None, None, None, None, None) == lp.DEFS["PNETGPU_EINVAL"]
+    h = ctypes.c_void_p()
+    rc = L.pnetgpu_ctx_create(10 ** 6, ctypes.byref(h))
+    assert rc == lp.DEFS["PNETGPU_ENODEV"] and not h.value
+    L.pnetgpu_ctx_destroy(None)
+
+
+def test_include_headers_compile_as_c():
+    for h in ("pnetgpu.h", "pnetgpu_synth.h"):
+        subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-fsyntax-only", "-x", "c",
+                        os.path.join(ROOT, "include", h)], check=True)
