@@ -7,6 +7,11 @@ import ctypes
 import os
 import re
 
+# PyTorch-ROCm bundles its own libamdhip64.so.7. Import it first so that the
+# dynamic loader resolves libpnetgpu.so's libamdhip64.so.7 (same SONAME) to the
+# runtime already in the process: one HIP runtime, shared device pointers/streams.
+import torch  # noqa: F401
+
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG_DIR)
 LIB_PATH = os.path.join(PKG_DIR, "libpnetgpu.so")
