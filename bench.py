@@ -29,12 +29,11 @@ import libpnet_amd as lp  # noqa: E402
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (/opt/skills/guides/MI355X_MICROARCH.md:36)
 METRIC = "device-resident Mpkts/s & GB/s, checksum+parse, 64B & 1500B, 1/2/4/8 GPU"
 WORKLOADS = {
-    "udp64": {"n": 1 << 24, "desc": "configs[1]: 64B UDP/IPv4/Ethernet, checksum verify + header extract, "
+    "udp64": {"n": 1 << 24, "kernel": "rx_small_kernel", "desc": "configs[1]: 64B UDP/IPv4/Ethernet, checksum verify + header extract, "
                                     "device-resident batch"},
-    "tcp1500": {"n": 1 << 20, "desc": "configs[2]: 1500B TCP/IPv4/Ethernet, full-MTU ones-complement sum over "
+    "tcp1500": {"n": 1 << 20, "kernel": "rx_kernel<8, 8, 4, false>", "desc": "configs[2]: 1500B TCP/IPv4/Ethernet, full-MTU ones-complement sum over "
                                       "pseudo-header+payload"},
 }
-KERNEL_NAME = "rx_kernel"
 
 
 def log(*a):
@@ -260,7 +259,7 @@ def main():
                 "unit": "GB/s",
                 "frac": round(p["achieved_gbs"] / HBM_PEAK_GBS, 4),
                 "traffic": load_traffic(primary),
-                "kernel": KERNEL_NAME,
+                "kernel": WORKLOADS[primary]["kernel"],
                 "kernel_avg_ms": round(p["kernel_avg_ms"], 4),
                 "alg_bytes_per_launch": sh.alg_bytes,
             },
@@ -273,7 +272,7 @@ def main():
                 "kernel_avg_ms": round(r["kernel_avg_ms"], 4),
                 "roofline_frac": round(r["achieved_gbs"] / HBM_PEAK_GBS, 4),
                 "achieved_gbs": round(r["achieved_gbs"], 1), "counters_ok": r["counters_ok"],
-                "traffic": load_traffic(name),
+                "traffic": load_traffic(name), "kernel": WORKLOADS[name]["kernel"],
             }
         if world == 1 and not args.no_cpu:
             line["cpu_baseline"] = cpu_baseline(sh)

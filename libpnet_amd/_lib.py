@@ -14,7 +14,8 @@ import torch  # noqa: F401
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG_DIR)
-LIB_PATH = os.path.join(PKG_DIR, "libpnetgpu.so")
+# PNETGPU_LIB selects an alternative build of the same library (tuning A/B runs)
+LIB_PATH = os.environ.get("PNETGPU_LIB") or os.path.join(PKG_DIR, "libpnetgpu.so")
 HEADERS = [os.path.join(ROOT, "include", "pnetgpu.h"), os.path.join(ROOT, "include", "pnetgpu_synth.h")]
 
 

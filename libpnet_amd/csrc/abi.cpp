@@ -6,6 +6,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <cstdint>
 #include <new>
 
@@ -106,23 +108,38 @@ int pnetgpu_rx_process(pnetgpu_ctx* ctx, const pnetgpu_batch* b, const pnetgpu_r
     a.cols = *cols;
     a.nruns = (a.n + kRunFrames - 1) / kRunFrames;
 
-    // Window width: 4 granules when every frame spans at most 64 aligned bytes
-    // (fixed stride, known alignment), else 8 (covers the longest header, 94 B).
-    int nw = 8, g = 16;
+    // Kernel choice. Small: fixed stride, every frame 16-B aligned, at most 64 B,
+    // inside the buffer (the 64-B configs). Generic otherwise; its tail group
+    // width G follows the typical frame size.
+    int kind = pnetgpu::kKindGeneric, g = 8;
     if (b->stride) {
-        const uint64_t sh = (a.delta + b->first_offset) & 15u;
-        const bool sh_fixed = (b->stride % 16) == 0;
-        const uint64_t worst_sh = sh_fixed ? sh : 15u;
-        const uint64_t span = b->frame_len ? (worst_sh + b->frame_len + 15) / 16 : 0;
-        if (span <= 4) nw = 4;
+        const uint64_t base_sh = (a.delta + b->first_offset) & 15u;
+        const uint64_t last_end = a.delta + b->first_offset + (b->n_frames - 1) * (uint64_t)b->stride + b->frame_len;
+        const bool fits = b->n_frames <= (UINT64_MAX - a.delta - b->first_offset - b->frame_len) / b->stride &&
+                          last_end <= a.limit;
+        if (base_sh == 0 && b->stride % 16 == 0 && b->frame_len <= 64 && fits) kind = pnetgpu::kKindSmall;
         if (b->frame_len >= 4096) g = 64;
-        else if (b->frame_len <= 256) g = 4;
     }
-    const int per_cu = pnetgpu::rx_blocks_per_cu(nw, g);
+    if (const char* e = std::getenv("PNETGPU_TAIL_GROUP")) {      // tuning override
+        const int v = std::atoi(e);
+        if (v == 8 || v == 16 || v == 64) g = v;
+    }
+    int numregs = 0, lds = 0;
+    int per_cu = pnetgpu::rx_blocks_per_cu(kind, g, &numregs, &lds);
+    if (per_cu <= 0) return PNETGPU_EHIP;
+    if (const char* e = std::getenv("PNETGPU_BLOCKS_PER_CU")) {   // tuning override
+        const int v = std::atoi(e);
+        if (v > 0) per_cu = v;
+    }
+    if (const char* e = std::getenv("PNETGPU_DEBUG")) {
+        if (*e == '1')
+            std::fprintf(stderr, "[pnetgpu] rx kind=%d g=%d regs=%d lds=%d blocks/cu=%d cus=%d\n", kind, g, numregs,
+                         lds, per_cu, ctx->cus);
+    }
     const uint64_t want = (a.nruns + kWavesPerBlock - 1) / kWavesPerBlock;
     const uint64_t cap = (uint64_t)ctx->cus * (uint64_t)per_cu;
     const int blocks = (int)std::max<uint64_t>(1, std::min(want, cap));
-    if (pnetgpu::launch_rx(a, nw, g, blocks, static_cast<hipStream_t>(stream)) != 0) return PNETGPU_EHIP;
+    if (pnetgpu::launch_rx(a, kind, g, blocks, static_cast<hipStream_t>(stream)) != 0) return PNETGPU_EHIP;
     return PNETGPU_OK;
 }
 

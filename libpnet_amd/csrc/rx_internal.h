@@ -36,8 +36,13 @@ struct SliceArgs {
     uint16_t* out;
 };
 
-int rx_blocks_per_cu(int nw, int g);
-int launch_rx(const RxArgs& args, int nw, int g, int blocks, hipStream_t stream);
+// Kernel kinds: the register-resident small-frame kernel (fixed stride, frames
+// 16-B aligned, span <= 64 B, every descriptor valid) or the generic one.
+constexpr int kKindSmall = 1;
+constexpr int kKindGeneric = 0;
+
+int rx_blocks_per_cu(int kind, int g, int* numregs, int* lds);
+int launch_rx(const RxArgs& args, int kind, int g, int blocks, hipStream_t stream);
 int launch_slices(const SliceArgs& args, int pseudo, int blocks, hipStream_t stream);
 
 }  // namespace pnetgpu

@@ -3,33 +3,41 @@
 //
 // What it computes is libpnet's per-frame receive chain (examples/packetdump.rs:120-217
 // over pnet_packet's views and checksums, pnet_packet/src/util.rs:76-181); see
-// include/pnetgpu.h for the exact contract and DESIGN.md for the layout.
+// include/pnetgpu.h for the contract and DESIGN.md for layouts and rooflines.
 //
-// Execution model (one wavefront = 64 lanes owns a run of 64 consecutive frames):
-//   1. descriptor : lane l computes frame l's (offset, length).
-//   2. window     : the wave loads the first NW aligned 16-B granules of each of
-//                   its 64 frames (NW*64 coalesced global_load_dwordx4, all issued
-//                   before any is consumed) into a wave-private LDS slot per frame.
-//   3. parse      : lane l parses frame l out of its LDS slot (byte reads, padded
-//                   slots => conflict-free) and derives the two checksum ranges.
-//   4. window sum : lane l sums its frame's window bytes under byte masks into two
-//                   u32 accumulators with v_sad_u16 (one op per dword).
-//   5. tail       : frames longer than the window are summed by groups of G lanes
-//                   streaming coalesced 16-B granules straight from HBM, reduced
-//                   with cross-lane shuffles, handed back through LDS.
-//   6. finalize   : fold, byte-order fix-up, pseudo-header, compare, coalesced SoA
-//                   stores; per-wave ballot counters, one atomic set per block.
+// Two kernels, one wavefront (64 lanes) per run of 64 consecutive frames:
 //
-// Checksum arithmetic (why the sums are bit-exact without byte swapping loads):
+//  rx_small_kernel  fixed-stride batches whose frames sit 16-B aligned and span
+//                   at most 64 B (the 64-B configs). The run's 4 KiB arrive as
+//                   four coalesced 1-KiB dwordx4 wave loads, are transposed
+//                   through 16-B-aligned LDS slots (conflict-free ds_read_b128),
+//                   and lane l then holds frame l in 16 VGPRs. The next run's
+//                   loads are issued before the current run is processed
+//                   (software pipelining). IPv4 with IHL 5 (and every trivially
+//                   classified frame) takes a register-only fast path with
+//                   compile-time field positions; anything else (IPv6, IPv4
+//                   options) takes the generic parse on its LDS slot.
+//
+//  rx_kernel        everything else (descriptor mode, any alignment, any size).
+//                   Window phase: the first NW=8 aligned 16-B granules of each
+//                   frame are loaded coalesced (8 loads in flight per lane) into
+//                   a padded LDS slot; lane l parses frame l there and sums the
+//                   window bytes. Tail phase: frames longer than the window go
+//                   on a per-wave work list served by groups of G lanes that
+//                   stream coalesced granules straight from HBM (U loads in
+//                   flight per lane), each group taking the next frame as soon
+//                   as it finishes one; partial sums are reduced with shuffles.
+//
+// Checksum arithmetic (why the sums are bit-exact without byte-swapping loads):
 //   The reference sums big-endian 16-bit words relative to the start of the slice
 //   (util.rs:158-181) into an exact u32 and folds with end-around carry. The fold
 //   depends only on the sum mod 0xFFFF and on whether it is zero. Summing the
-//   little-endian halves of aligned dwords weights byte b at absolute address a by
-//   256^(a&1); since 65536 == 1 (mod 0xFFFF) that equals the BE weight up to one
-//   factor 256, i.e. a byte swap of the folded result when the slice starts at an
-//   even absolute address (every range here starts at an even frame offset, so
-//   parity = frame offset parity). All partial sums are exact non-negative
-//   integers, so "zero iff every in-range byte is zero" is preserved too.
+//   little-endian halves of aligned dwords (v_sad_u16) weights byte b at absolute
+//   address a by 256^(a&1); since 65536 == 1 (mod 0xFFFF) that equals the BE
+//   weight up to one factor 256, i.e. a byte swap of the folded result when the
+//   slice starts at an even absolute address (every range here starts at an even
+//   frame offset, so parity = frame offset parity). All partial sums are exact
+//   non-negative integers, so "zero iff every in-range byte is zero" holds too.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -44,6 +52,7 @@ constexpr int kWave = 64;
 constexpr int kWavesPerBlock = 4;
 constexpr int kBlock = kWave * kWavesPerBlock;
 
+// ---- arithmetic helpers ----------------------------------------------------
 __device__ __forceinline__ uint32_t fold16(uint32_t x) {
     x = (x & 0xFFFFu) + (x >> 16);
     x = (x & 0xFFFFu) + (x >> 16);
@@ -51,29 +60,35 @@ __device__ __forceinline__ uint32_t fold16(uint32_t x) {
 }
 __device__ __forceinline__ uint32_t bswap16(uint32_t x) { return ((x & 0xFFu) << 8) | ((x >> 8) & 0xFFu); }
 // mask of the first x bytes of a dword, x in [0, 4]
-__device__ __forceinline__ uint32_t first_bytes(int x) {
-    return (uint32_t)(0xFFFFFFFFull >> (32 - 8 * x));
-}
+__device__ __forceinline__ uint32_t first_bytes(int x) { return (uint32_t)(0xFFFFFFFFull >> (32 - 8 * x)); }
 __device__ __forceinline__ int clamp04(int v) { return min(max(v, 0), 4); }
 // LE 16-bit halves of d added to acc (v_sad_u16 with a zero operand)
-__device__ __forceinline__ uint32_t sad(uint32_t d, uint32_t acc) {
-    return __builtin_amdgcn_sad_u16(d, 0u, acc);
+__device__ __forceinline__ uint32_t sad(uint32_t d, uint32_t acc) { return __builtin_amdgcn_sad_u16(d, 0u, acc); }
+// 16-B streaming load (read once: non-temporal hint)
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 load16_nt(const void* p) {
+    const u32x4_t v = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
 }
+// 16-B load with the default cache policy (granules other lanes/instructions
+// of the same wave touch again: windows, strided per-lane frames)
+__device__ __forceinline__ uint4 load16(const void* p) { return *reinterpret_cast<const uint4*>(p); }
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
+
+// ---- LDS byte access ---------------------------------------------------------
 __device__ __forceinline__ uint32_t ld8(const uint8_t* w, int p) { return w[p]; }
 __device__ __forceinline__ uint32_t ld16be(const uint8_t* w, int p) { return (ld8(w, p) << 8) | ld8(w, p + 1); }
 __device__ __forceinline__ uint32_t ld32be(const uint8_t* w, int p) { return (ld16be(w, p) << 16) | ld16be(w, p + 2); }
 
-// 16 bytes of a frame-relative run [p, p+16) read from an LDS slot at any
-// alignment, as 4 little-endian dwords (memory order).
+// 16 bytes of a run [p, p+16) of an LDS slot at any alignment, as 4 LE dwords.
 __device__ __forceinline__ uint4 lds_read16_unaligned(const uint8_t* slot, int p) {
     const uint32_t* s32 = reinterpret_cast<const uint32_t*>(slot);
-    int q = p >> 2, sh = (p & 3);
-    uint32_t d0 = s32[q], d1 = s32[q + 1], d2 = s32[q + 2], d3 = s32[q + 3], d4 = s32[q + 4];
+    const int q = p >> 2, sh = (p & 3);
+    const uint32_t d0 = s32[q], d1 = s32[q + 1], d2 = s32[q + 2], d3 = s32[q + 3], d4 = s32[q + 4];
     uint4 r;
     r.x = __builtin_amdgcn_alignbyte(d1, d0, sh);
     r.y = __builtin_amdgcn_alignbyte(d2, d1, sh);
@@ -82,25 +97,428 @@ __device__ __forceinline__ uint4 lds_read16_unaligned(const uint8_t* slot, int p
     return r;
 }
 
-// Per-wave LDS: 64 frame slots of NW granules (+4 B pad so lane l's byte p sits
-// in bank (l*SLOT/4 + p/4) % 32: conflict-free for the parse reads), plus the
-// per-frame hand-off words used by the tail phase.
+// ---- the reference's receive dispatch, restated for one lane ---------------
+// Fields of one frame plus the two summed ranges A=[r0,m) (IPv4 header, or the
+// IPv6 pseudo-header addresses) and B=[m,e) (the L4 slice), frame-relative.
+struct Parsed {
+    uint32_t st, et, proto, ttl, l4off, l4len, sp, dp, s4, d4, ipstored, l4stored, pseudo;
+    int r0, m, e;
+    bool is_v4, l4do, v6pseudo;
+};
+
+// Generic parse of a frame held in LDS at W (frame byte 0), `len` bytes.
+// packetdump.rs:155-217 + ipv4.rs:165-178,226-243 + ipv6.rs:21-37 + udp/tcp/icmp
+// layouts and minimum sizes (decorator.rs:593-600) + payload bounds (decorator.rs:713-769).
+__device__ __forceinline__ Parsed parse_lds(const uint8_t* W, uint32_t len) {
+    Parsed P{};
+    if (len < 14) {
+        P.st = PNET_ST_ETH_MALFORMED;                  // EthernetPacket::new == None
+        return P;
+    }
+    P.et = ld16be(W, 12);
+    const uint32_t eplen = len - 14;                   // Ethernet payload: unbounded
+    bool l3ok = false, has_l4 = false, v6 = false;
+    uint32_t l4s = 0;
+    if (P.et == 0x0800u) {
+        P.st |= PNET_ST_L3_IPV4;
+        if (eplen < 20) {
+            P.st |= PNET_ST_L3_MALFORMED;
+        } else {
+            l3ok = true;
+            P.is_v4 = true;
+            const uint32_t ihl4 = (ld8(W, 14) & 15u) * 4u;
+            const uint32_t hl = min(max(ihl4, 20u), eplen);   // ipv4.rs:169-175
+            const uint32_t tl = ld16be(W, 16);
+            P.ttl = ld8(W, 22);
+            P.proto = ld8(W, 23);
+            P.ipstored = ld16be(W, 24);
+            P.s4 = ld32be(W, 26);
+            P.d4 = ld32be(W, 30);
+            P.r0 = 14;
+            P.m = 14 + (int)hl;
+            const uint32_t start = max(20u, ihl4);             // 20 + ipv4_options_length
+            const uint32_t plen = tl > ihl4 ? tl - ihl4 : 0u;  // ipv4_payload_length
+            if (eplen > start) {
+                has_l4 = true;
+                l4s = 14 + start;
+                P.l4len = min(start + plen, eplen) - start;
+            }
+        }
+    } else if (P.et == 0x86DDu) {
+        P.st |= PNET_ST_L3_IPV6;
+        if (eplen < 40) {
+            P.st |= PNET_ST_L3_MALFORMED;
+        } else {
+            l3ok = true;
+            v6 = true;
+            P.proto = ld8(W, 20);
+            P.ttl = ld8(W, 21);
+            const uint32_t pl = ld16be(W, 18);
+            if (eplen > 40) {                                  // #[length = "payload_length"]
+                has_l4 = true;
+                l4s = 54;
+                P.l4len = min(40u + pl, eplen) - 40u;
+            }
+        }
+    } else {
+        P.st |= PNET_ST_UNKNOWN_ETHERTYPE;
+    }
+    if (has_l4) P.l4off = l4s;
+    if (l3ok) {
+        uint32_t kind = 0, minlen = 0;
+        int soff = 0;
+        switch (P.proto) {
+            case 17: kind = PNET_ST_L4_UDP; minlen = 8; soff = 6; break;
+            case 6: kind = PNET_ST_L4_TCP; minlen = 20; soff = 16; break;
+            case 1: kind = PNET_ST_L4_ICMP; minlen = 4; soff = 2; break;
+            case 58: kind = PNET_ST_L4_ICMPV6; minlen = 4; soff = 2; break;
+            default: break;
+        }
+        if (!kind) {
+            P.st |= PNET_ST_UNKNOWN_PROTO;
+        } else {
+            P.st |= kind;
+            if (P.l4len < minlen) {
+                P.st |= PNET_ST_L4_MALFORMED;
+            } else {
+                const int p = (int)l4s;
+                P.sp = ld16be(W, p);
+                if (P.proto == 17 || P.proto == 6) P.dp = ld16be(W, p + 2);
+                else P.dp = P.l4len >= 8 ? ld16be(W, p + 4) : 0u;
+                P.l4stored = ld16be(W, p + soff);
+                if (P.proto == 1) {                            // icmp::checksum: no pseudo-header
+                    P.l4do = true;
+                    if (v6) { P.r0 = 54; P.m = 54; }
+                } else if (v6) {                               // util::ipv6_checksum
+                    P.l4do = true;
+                    P.v6pseudo = true;
+                    P.r0 = 22; P.m = 54;                       // pseudo-header address bytes
+                    P.pseudo = P.proto + P.l4len;
+                } else if (P.proto != 58) {                    // util::ipv4_checksum
+                    P.l4do = true;
+                    P.pseudo = (P.s4 >> 16) + (P.s4 & 0xFFFFu) + (P.d4 >> 16) + (P.d4 & 0xFFFFu) +
+                               P.proto + P.l4len;
+                }
+                if (P.l4do) P.e = p + (int)P.l4len;            // B = [l4s, l4s+len), l4s == m
+            }
+        }
+    }
+    if (!P.is_v4 && !P.l4do) { P.r0 = 0; P.m = 0; P.e = 0; }
+    if (P.is_v4 && !P.l4do) P.e = P.m;
+    return P;
+}
+
+// Window sums of one lane's LDS slot: tA over [rs,ms), tB over [ms,ew) in slot
+// coordinates, rs <= ms <= ew (all zero: nothing to sum). With P(x) = weighted
+// sum of the slot bytes in [4*(rs>>2), x): tA = P(ms) - P(rs), tB = P(ew) - P(ms).
+// One runtime loop over whole dwords (v_sad_u16 each) plus three masked partial
+// dwords; the slot has a readable pad dword so ew>>2 may equal the dword count.
+__device__ __forceinline__ void window_sums(const uint8_t* slot, int rs, int ms, int ew, uint32_t& tA,
+                                            uint32_t& tB) {
+    const uint32_t* s32 = reinterpret_cast<const uint32_t*>(slot);
+    const int k0 = rs >> 2, km = ms >> 2, ke = ew >> 2;
+    uint32_t acc = 0, pm = 0;
+#pragma unroll 1
+    for (int k = k0; k < ke; ++k) {
+        if (k == km) pm = acc;
+        acc = sad(s32[k], acc);
+    }
+    if (km >= ke) pm = acc;
+    const uint32_t p_rs = sad(s32[k0] & first_bytes(rs & 3), 0u);
+    const uint32_t p_ms = sad(s32[km] & first_bytes(ms & 3), pm);
+    const uint32_t p_ew = sad(s32[ke] & first_bytes(ew & 3), acc);
+    tA += p_ms - p_rs;
+    tB += p_ew - p_ms;
+}
+
+// Skip-word removal, fold, byte-order fix-up, pseudo-header, compare.
+// odd = frame offset parity. Returns ip and l4 checksums through P.
+__device__ __forceinline__ void finalize(Parsed& P, uint32_t tA, uint32_t tB, bool odd, uint32_t& ipc,
+                                         uint32_t& l4c) {
+    ipc = 0;
+    l4c = 0;
+    if (P.is_v4) tA -= odd ? P.ipstored : bswap16(P.ipstored);    // skipword 5 (ipv4.rs:177)
+    if (P.l4do) tB -= odd ? P.l4stored : bswap16(P.l4stored);     // skipword 3 / 8 / 1
+    uint32_t pA = fold16(tA), pB = fold16(tB);
+    if (!odd) { pA = bswap16(pA); pB = bswap16(pB); }
+    if (P.is_v4) {
+        ipc = (~pA) & 0xFFFFu;
+        if (ipc == P.ipstored) P.st |= PNET_ST_IP_CSUM_OK;
+    }
+    if (P.l4do) {
+        l4c = (~fold16(pB + P.pseudo + (P.v6pseudo ? pA : 0u))) & 0xFFFFu;
+        P.st |= PNET_ST_L4_CSUM_DONE;
+        if (l4c == P.l4stored) P.st |= PNET_ST_L4_CSUM_OK;
+    }
+}
+
+// Per-wave counters (ballots: wave-uniform) and coalesced column stores.
+struct Counters {
+    uint32_t frames = 0, v4 = 0, v6 = 0, ipbad = 0, l4bad = 0, malf = 0, unk = 0;
+    uint64_t bytes = 0;
+    __device__ __forceinline__ void add(bool valid, uint32_t len, uint32_t st) {
+        frames += (uint32_t)__popcll(__ballot(valid));
+        bytes += len;
+        v4 += (uint32_t)__popcll(__ballot((st & PNET_ST_L3_MASK) == PNET_ST_L3_IPV4));
+        v6 += (uint32_t)__popcll(__ballot((st & PNET_ST_L3_MASK) == PNET_ST_L3_IPV6));
+        ipbad += (uint32_t)__popcll(__ballot((st & (PNET_ST_L3_MASK | PNET_ST_L3_MALFORMED | PNET_ST_IP_CSUM_OK)) ==
+                                             PNET_ST_L3_IPV4));
+        l4bad += (uint32_t)__popcll(__ballot((st & (PNET_ST_L4_CSUM_DONE | PNET_ST_L4_CSUM_OK)) ==
+                                             PNET_ST_L4_CSUM_DONE));
+        malf += (uint32_t)__popcll(__ballot((st & (PNET_ST_ETH_MALFORMED | PNET_ST_L3_MALFORMED |
+                                                   PNET_ST_L4_MALFORMED | PNET_ST_DESC_INVALID)) != 0));
+        unk += (uint32_t)__popcll(__ballot((st & (PNET_ST_UNKNOWN_ETHERTYPE | PNET_ST_UNKNOWN_PROTO)) != 0));
+    }
+    // one atomic set per block (all waves must call)
+    __device__ __forceinline__ void flush(uint64_t* out, uint64_t (*blk)[PNETGPU_NCOUNTERS], int wv, int lane) {
+        for (int o = 32; o >= 1; o >>= 1) {
+            uint32_t lo = (uint32_t)bytes, hi = (uint32_t)(bytes >> 32);
+            lo = __shfl_xor(lo, o);
+            hi = __shfl_xor(hi, o);
+            bytes += ((uint64_t)hi << 32) | lo;
+        }
+        if (lane == 0) {
+            blk[wv][PNETGPU_CTR_FRAMES] = frames;
+            blk[wv][PNETGPU_CTR_BYTES] = bytes;
+            blk[wv][PNETGPU_CTR_IPV4] = v4;
+            blk[wv][PNETGPU_CTR_IPV6] = v6;
+            blk[wv][PNETGPU_CTR_IP_CSUM_BAD] = ipbad;
+            blk[wv][PNETGPU_CTR_L4_CSUM_BAD] = l4bad;
+            blk[wv][PNETGPU_CTR_MALFORMED] = malf;
+            blk[wv][PNETGPU_CTR_UNKNOWN] = unk;
+        }
+        __syncthreads();
+        if (threadIdx.x < PNETGPU_NCOUNTERS) {
+            uint64_t v = 0;
+            for (int w = 0; w < kWavesPerBlock; ++w) v += blk[w][threadIdx.x];
+            if (v) atomicAdd(reinterpret_cast<unsigned long long*>(out + threadIdx.x), (unsigned long long)v);
+        }
+    }
+};
+
+// Column stores for the frames of one run: the base is wave-uniform (SGPR) and
+// the lane adds its index, so each store is one coalesced wave instruction.
+__device__ __forceinline__ void store_columns(const pnetgpu_rx_columns& C, uint64_t f0, int lane, bool in_batch,
+                                              const Parsed& P, uint32_t ipc, uint32_t l4c, const uint8_t* slot,
+                                              int sh) {
+    if (!in_batch) return;
+    if (C.status) C.status[f0 + lane] = (uint16_t)P.st;
+    if (C.ip_csum) C.ip_csum[f0 + lane] = (uint16_t)ipc;
+    if (C.l4_csum) C.l4_csum[f0 + lane] = (uint16_t)l4c;
+    if (C.ethertype) C.ethertype[f0 + lane] = (uint16_t)P.et;
+    if (C.ip_proto) C.ip_proto[f0 + lane] = (uint8_t)P.proto;
+    if (C.ttl) C.ttl[f0 + lane] = (uint8_t)P.ttl;
+    if (C.l4_offset) C.l4_offset[f0 + lane] = (uint16_t)P.l4off;
+    if (C.l4_length) C.l4_length[f0 + lane] = (uint16_t)P.l4len;
+    if (C.src_port) C.src_port[f0 + lane] = (uint16_t)P.sp;
+    if (C.dst_port) C.dst_port[f0 + lane] = (uint16_t)P.dp;
+    if (C.src_ipv4) C.src_ipv4[f0 + lane] = P.s4;
+    if (C.dst_ipv4) C.dst_ipv4[f0 + lane] = P.d4;
+    if (C.src_ipv6 || C.dst_ipv6) {
+        const bool v6ok = (P.st & (PNET_ST_L3_MASK | PNET_ST_L3_MALFORMED)) == PNET_ST_L3_IPV6;
+        uint4 sv = make_uint4(0, 0, 0, 0), dv = make_uint4(0, 0, 0, 0);
+        if (v6ok) {
+            sv = lds_read16_unaligned(slot, sh + 22);
+            dv = lds_read16_unaligned(slot, sh + 38);
+        }
+        if (C.src_ipv6) reinterpret_cast<uint4*>(C.src_ipv6)[f0 + lane] = sv;
+        if (C.dst_ipv6) reinterpret_cast<uint4*>(C.dst_ipv6)[f0 + lane] = dv;
+    }
+}
+
+// ============================================================================
+// rx_small_kernel: fixed stride, frames 16-B aligned, span <= 64 B.
+// ============================================================================
+constexpr int kSmallSlot = 80;   // 16-B aligned slots; ds_read_b128 conflict-free (20l mod 64 distinct per 16 lanes)
+
+struct SmallRun {
+    uint4 g[4];
+};
+
+// Coalesced: instruction i, lane L loads granule L%4 of frame 16i + L/4 (for
+// stride 64 that is one contiguous 1-KiB wave load); transposed through LDS.
+__device__ __forceinline__ SmallRun small_load(const RxArgs& a, uint64_t run, int lane) {
+    SmallRun r;
+    const uint32_t span = (a.frame_len + 15u) >> 4;
+    const uint32_t c = (uint32_t)(lane & 3);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint64_t f = run * kWave + 16 * i + (lane >> 2);
+        r.g[i] = make_uint4(0, 0, 0, 0);
+        if (f < a.n && c < span)
+            r.g[i] = load16(a.data + (a.first + a.delta) + f * a.stride + 16u * c);
+    }
+    return r;
+}
+
+__global__ __launch_bounds__(kBlock, 5) void rx_small_kernel(RxArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds_slots[kWavesPerBlock][kWave * kSmallSlot];
+    __shared__ uint64_t blk_ctr[kWavesPerBlock][PNETGPU_NCOUNTERS];
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wv = threadIdx.x / kWave;
+    uint8_t* slot = lds_slots[wv] + lane * kSmallSlot;
+    Counters K;
+
+    const uint64_t wave_stride = (uint64_t)gridDim.x * kWavesPerBlock;
+    uint64_t run = (uint64_t)blockIdx.x * kWavesPerBlock + wv;
+    SmallRun cur = run < a.nruns ? small_load(a, run, lane) : SmallRun{};
+    for (; run < a.nruns; run += wave_stride) {
+        // software pipelining: the next run's loads are in flight while this one is processed
+        const uint64_t nrun = run + wave_stride;
+        SmallRun nxt = nrun < a.nruns ? small_load(a, nrun, lane) : SmallRun{};
+
+        const uint64_t f0 = run * kWave;
+        const bool in_batch = f0 + lane < a.n;
+        const uint32_t len = in_batch ? a.frame_len : 0u;
+        {
+            // granule (frame 16i + lane/4, chunk lane%4) -> that frame's slot; read back own frame
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                *reinterpret_cast<uint4*>(lds_slots[wv] + (16 * i + (lane >> 2)) * kSmallSlot + 16 * (lane & 3)) =
+                    cur.g[i];
+            wave_sync();
+#pragma unroll
+            for (int c = 0; c < 4; ++c) cur.g[c] = *reinterpret_cast<const uint4*>(slot + 16 * c);
+        }
+        [[maybe_unused]] const uint32_t w0 = cur.g[0].x, w1 = cur.g[0].y, w2 = cur.g[0].z;
+        const uint32_t w3 = cur.g[0].w;
+        const uint32_t w4 = cur.g[1].x, w5 = cur.g[1].y, w6 = cur.g[1].z, w7 = cur.g[1].w;
+        const uint32_t w8 = cur.g[2].x, w9 = cur.g[2].y, w10 = cur.g[2].z, w11 = cur.g[2].w;
+        const uint32_t w12 = cur.g[3].x, w13 = cur.g[3].y, w14 = cur.g[3].z, w15 = cur.g[3].w;
+
+        Parsed P{};
+        uint32_t ipc = 0, l4c = 0;
+        bool slow = false;
+        if (in_batch) {
+            if (len < 14) {
+                P.st = PNET_ST_ETH_MALFORMED;
+            } else {
+                P.et = bswap16(w3 & 0xFFFFu);
+                if (P.et == 0x0800u) {
+                    if (len < 34) {
+                        P.st = PNET_ST_L3_IPV4 | PNET_ST_L3_MALFORMED;
+                    } else if (((w3 >> 16) & 0xFu) != 5u) {
+                        slow = true;                       // IPv4 options / IHL clamp: generic path
+                    } else {
+                        // ---- fast path: IPv4, IHL 5; every position below is static ----
+                        P.st = PNET_ST_L3_IPV4;
+                        P.is_v4 = true;
+                        const uint32_t eplen = len - 14;
+                        const uint32_t tl = bswap16(w4 & 0xFFFFu);
+                        P.ttl = (w5 >> 16) & 0xFFu;
+                        P.proto = w5 >> 24;
+                        P.ipstored = bswap16(w6 & 0xFFFFu);
+                        P.s4 = (bswap16(w6 >> 16) << 16) | bswap16(w7 & 0xFFFFu);   // bytes 26..29
+                        P.d4 = (bswap16(w7 >> 16) << 16) | bswap16(w8 & 0xFFFFu);   // bytes 30..33
+                        // header sum [14,34) without the checksum word (bytes 24,25)
+                        uint32_t tA = sad(w3 & 0xFFFF0000u, 0u);
+                        tA = sad(w4, tA);
+                        tA = sad(w5, tA);
+                        tA = sad(w6 & 0xFFFF0000u, tA);
+                        tA = sad(w7, tA);
+                        tA = sad(w8 & 0x0000FFFFu, tA);
+                        ipc = (~bswap16(fold16(tA))) & 0xFFFFu;
+                        if (ipc == P.ipstored) P.st |= PNET_ST_IP_CSUM_OK;
+                        const uint32_t plen = tl > 20u ? tl - 20u : 0u;
+                        if (eplen > 20u) {
+                            P.l4off = 34;
+                            P.l4len = min(20u + plen, eplen) - 20u;
+                        }
+                        uint32_t kind = 0, minlen = 0;
+                        switch (P.proto) {
+                            case 17: kind = PNET_ST_L4_UDP; minlen = 8; break;
+                            case 6: kind = PNET_ST_L4_TCP; minlen = 20; break;
+                            case 1: kind = PNET_ST_L4_ICMP; minlen = 4; break;
+                            case 58: kind = PNET_ST_L4_ICMPV6; minlen = 4; break;
+                            default: break;
+                        }
+                        if (!kind) {
+                            P.st |= PNET_ST_UNKNOWN_PROTO;
+                        } else {
+                            P.st |= kind;
+                            if (P.l4len < minlen) {
+                                P.st |= PNET_ST_L4_MALFORMED;
+                            } else {
+                                P.sp = bswap16(w8 >> 16);                            // bytes 34,35
+                                uint32_t stored_le;
+                                if (P.proto == 17) {
+                                    P.dp = bswap16(w9 & 0xFFFFu);
+                                    stored_le = w10 & 0xFFFFu;                       // bytes 40,41
+                                } else if (P.proto == 6) {
+                                    P.dp = bswap16(w9 & 0xFFFFu);
+                                    stored_le = w12 >> 16;                           // bytes 50,51
+                                } else {
+                                    P.dp = P.l4len >= 8 ? bswap16(w9 >> 16) : 0u;    // bytes 38,39
+                                    stored_le = w9 & 0xFFFFu;                        // bytes 36,37
+                                }
+                                P.l4stored = bswap16(stored_le);
+                                if (P.proto != 58) {       // ICMPv6 over IPv4: no checksum defined
+                                    const int e = 34 + (int)P.l4len;
+                                    uint32_t tB = sad(w8 & 0xFFFF0000u, 0u);
+                                    tB = sad(w9 & first_bytes(clamp04(e - 36)), tB);
+                                    tB = sad(w10 & first_bytes(clamp04(e - 40)), tB);
+                                    tB = sad(w11 & first_bytes(clamp04(e - 44)), tB);
+                                    tB = sad(w12 & first_bytes(clamp04(e - 48)), tB);
+                                    tB = sad(w13 & first_bytes(clamp04(e - 52)), tB);
+                                    tB = sad(w14 & first_bytes(clamp04(e - 56)), tB);
+                                    tB = sad(w15 & first_bytes(clamp04(e - 60)), tB);
+                                    tB -= stored_le;
+                                    uint32_t pseudo = 0;
+                                    if (P.proto != 1)
+                                        pseudo = (P.s4 >> 16) + (P.s4 & 0xFFFFu) + (P.d4 >> 16) + (P.d4 & 0xFFFFu) +
+                                                 P.proto + P.l4len;
+                                    l4c = (~fold16(bswap16(fold16(tB)) + pseudo)) & 0xFFFFu;
+                                    P.st |= PNET_ST_L4_CSUM_DONE;
+                                    if (l4c == P.l4stored) P.st |= PNET_ST_L4_CSUM_OK;
+                                }
+                            }
+                        }
+                    }
+                } else if (P.et == 0x86DDu) {
+                    slow = true;
+                } else {
+                    P.st = PNET_ST_UNKNOWN_ETHERTYPE;
+                }
+            }
+        }
+        // ---- generic path through LDS for the lanes the fast path did not take ----
+        const bool need_v6 = a.cols.src_ipv6 || a.cols.dst_ipv6;
+        if (__ballot(slow) || need_v6) {
+            if (slow) {
+                P = parse_lds(slot, len);
+                uint32_t tA = 0, tB = 0;
+                window_sums(slot, P.r0, P.m, P.e, tA, tB);
+                finalize(P, tA, tB, false, ipc, l4c);
+            }
+        }
+        store_columns(a.cols, f0, lane, in_batch, P, ipc, l4c, slot, 0);
+        if (a.cols.counters) K.add(in_batch, len, P.st);
+        wave_sync();
+        cur = nxt;
+    }
+    if (a.cols.counters) K.flush(a.cols.counters, blk_ctr, wv, lane);
+}
+
+// ============================================================================
+// rx_kernel: generic (descriptor mode, any alignment, any length).
+// ============================================================================
 template <int NW>
 struct WaveLds {
-    static constexpr int kSlot = NW * 16 + 4;
-    uint8_t  win[kWave * kSlot];
+    static constexpr int kSlot = NW * 16 + 4;   // +4 B pad: conflict-free parse reads
+    uint8_t win[kWave * kSlot];
     uint64_t base[kWave];     // aligned byte offset of granule 0 of each frame
     uint32_t end[kWave];      // slot-relative end of the summed range
     uint32_t tail[kWave];     // tail-phase partial sum per frame
+    uint8_t list[kWave];      // frames with a tail, in lane order
 };
 
-template <int NW, int G>
-__global__ __launch_bounds__(kBlock) void rx_kernel(RxArgs a) {
-    static_assert(NW == 4 || NW == 8, "window granules");
+template <int NW, int G, int U, bool NT>
+__global__ __launch_bounds__(kBlock, 4) void rx_kernel(RxArgs a) {
+    static_assert(NW == 8, "window granules");
     static_assert(G == 4 || G == 8 || G == 16 || G == 32 || G == 64, "tail group");
     constexpr int kSlot = WaveLds<NW>::kSlot;
-    constexpr int kWin = NW * 16;           // window bytes per frame
-    constexpr int kFps = kWave / G;         // frames per tail set
+    constexpr int kWin = NW * 16;
+    constexpr int kGroups = kWave / G;
 
     __shared__ WaveLds<NW> lds_all[kWavesPerBlock];
     __shared__ uint64_t blk_ctr[kWavesPerBlock][PNETGPU_NCOUNTERS];
@@ -109,14 +527,13 @@ __global__ __launch_bounds__(kBlock) void rx_kernel(RxArgs a) {
     const int wv = threadIdx.x / kWave;
     WaveLds<NW>& L = lds_all[wv];
     uint8_t* slot = L.win + lane * kSlot;
-
-    uint32_t c_frames = 0, c_v4 = 0, c_v6 = 0, c_ipbad = 0, c_l4bad = 0, c_malf = 0, c_unk = 0;
-    uint64_t c_bytes = 0;
+    Counters K;
 
     const uint64_t wave_stride = (uint64_t)gridDim.x * kWavesPerBlock;
     for (uint64_t run = (uint64_t)blockIdx.x * kWavesPerBlock + wv; run < a.nruns; run += wave_stride) {
         // ---- 1. descriptor -------------------------------------------------
-        const uint64_t f = run * kWave + lane;
+        const uint64_t f0 = run * kWave;
+        const uint64_t f = f0 + lane;
         const bool in_batch = f < a.n;
         uint64_t off = 0;
         uint32_t len = 0;
@@ -135,9 +552,8 @@ __global__ __launch_bounds__(kBlock) void rx_kernel(RxArgs a) {
         const int sh = (int)(off & 15);
         const uint64_t base = off - (uint64_t)sh;
         const uint32_t span = len ? (uint32_t)((sh + (uint64_t)len + 15) >> 4) : 0u;
-        const uint32_t nwin = span < (uint32_t)NW ? span : (uint32_t)NW;
         L.base[lane] = base;
-        L.end[lane] = nwin;   // temporarily: granules to load into the window
+        L.end[lane] = span < (uint32_t)NW ? span : (uint32_t)NW;   // granules to load into the window
         wave_sync();
 
         // ---- 2. window: NW*64 granule loads, all in flight before any store --
@@ -147,9 +563,8 @@ __global__ __launch_bounds__(kBlock) void rx_kernel(RxArgs a) {
             const int q = i * kWave + lane;
             const int fl = q / NW, c = q % NW;
             g[i] = make_uint4(0, 0, 0, 0);
-            if ((uint32_t)c < L.end[fl]) {
-                g[i] = *reinterpret_cast<const uint4*>(a.data + L.base[fl] + 16u * c);
-            }
+            if ((uint32_t)c < L.end[fl])
+                g[i] = load16(a.data + L.base[fl] + 16u * c);
         }
 #pragma unroll
         for (int i = 0; i < NW; ++i) {
@@ -160,262 +575,93 @@ __global__ __launch_bounds__(kBlock) void rx_kernel(RxArgs a) {
         }
         wave_sync();
 
-        // ---- 3. parse (lane l <-> frame l) ---------------------------------
-        const uint8_t* W = slot + sh;
-        uint32_t st = 0, et = 0, proto = 0, ttl = 0, l4off = 0, l4len = 0, sp = 0, dp = 0;
-        uint32_t s4 = 0, d4 = 0, ipstored = 0, l4stored = 0, pseudo = 0;
-        int r0 = 0, m = 0, e = 0;      // frame-relative range bounds: A=[r0,m), B=[m,e)
-        int l4skip_at = 0;
-        bool is_v4 = false, l4do = false, v6pseudo = false;
-        if (desc_bad) {
-            st = PNET_ST_DESC_INVALID;
-        } else if (in_batch) {
-            if (len < 14) {
-                st = PNET_ST_ETH_MALFORMED;               // EthernetPacket::new == None
-            } else {
-                et = ld16be(W, 12);
-                const uint32_t eplen = len - 14;          // Ethernet payload: unbounded
-                bool l3ok = false, has_l4 = false, v6 = false;
-                uint32_t l4s = 0;
-                if (et == 0x0800u) {
-                    st |= PNET_ST_L3_IPV4;
-                    if (eplen < 20) {
-                        st |= PNET_ST_L3_MALFORMED;
-                    } else {
-                        l3ok = true;
-                        is_v4 = true;
-                        const uint32_t ihl4 = (ld8(W, 14) & 15u) * 4u;
-                        // ipv4.rs:169-175 clamp to [20, packet().len()]
-                        const uint32_t hl = min(max(ihl4, 20u), eplen);
-                        const uint32_t tl = ld16be(W, 16);
-                        ttl = ld8(W, 22);
-                        proto = ld8(W, 23);
-                        ipstored = ld16be(W, 24);
-                        s4 = ld32be(W, 26);
-                        d4 = ld32be(W, 30);
-                        r0 = 14;
-                        m = 14 + (int)hl;
-                        // decorator.rs:728-753 with ipv4.rs:226-243
-                        const uint32_t start = max(20u, ihl4);
-                        const uint32_t plen = tl > ihl4 ? tl - ihl4 : 0u;
-                        if (eplen > start) {
-                            has_l4 = true;
-                            l4s = 14 + start;
-                            l4len = min(start + plen, eplen) - start;
-                        }
-                    }
-                } else if (et == 0x86DDu) {
-                    st |= PNET_ST_L3_IPV6;
-                    if (eplen < 40) {
-                        st |= PNET_ST_L3_MALFORMED;
-                    } else {
-                        l3ok = true;
-                        v6 = true;
-                        proto = ld8(W, 20);
-                        ttl = ld8(W, 21);
-                        const uint32_t pl = ld16be(W, 18);
-                        if (eplen > 40) {                  // ipv6.rs:34-36 #[length = "payload_length"]
-                            has_l4 = true;
-                            l4s = 54;
-                            l4len = min(40u + pl, eplen) - 40u;
-                        }
-                    }
-                } else {
-                    st |= PNET_ST_UNKNOWN_ETHERTYPE;
-                }
-                if (has_l4) l4off = l4s;
-                if (l3ok) {
-                    uint32_t kind = 0, minlen = 0;
-                    int soff = 0;
-                    switch (proto) {
-                        case 17: kind = PNET_ST_L4_UDP; minlen = 8; soff = 6; break;
-                        case 6: kind = PNET_ST_L4_TCP; minlen = 20; soff = 16; break;
-                        case 1: kind = PNET_ST_L4_ICMP; minlen = 4; soff = 2; break;
-                        case 58: kind = PNET_ST_L4_ICMPV6; minlen = 4; soff = 2; break;
-                        default: break;
-                    }
-                    if (!kind) {
-                        st |= PNET_ST_UNKNOWN_PROTO;
-                    } else {
-                        st |= kind;
-                        if (l4len < minlen) {
-                            st |= PNET_ST_L4_MALFORMED;
-                        } else {
-                            const int p = (int)l4s;
-                            sp = ld16be(W, p);
-                            if (proto == 17 || proto == 6) dp = ld16be(W, p + 2);
-                            else dp = l4len >= 8 ? ld16be(W, p + 4) : 0u;
-                            l4skip_at = p + soff;
-                            l4stored = ld16be(W, l4skip_at);
-                            if (proto == 1) {                       // icmp::checksum: no pseudo-header
-                                l4do = true;
-                                if (v6) { r0 = 54; m = 54; }
-                            } else if (v6) {                        // util::ipv6_checksum
-                                l4do = true;
-                                v6pseudo = true;
-                                r0 = 22; m = 54;                   // pseudo-header address bytes
-                                pseudo = proto + l4len;
-                            } else if (proto != 58) {               // util::ipv4_checksum
-                                l4do = true;
-                                pseudo = (s4 >> 16) + (s4 & 0xFFFFu) + (d4 >> 16) + (d4 & 0xFFFFu) +
-                                         proto + l4len;
-                            }
-                            if (l4do) e = p + (int)l4len;           // B = [l4s, l4s+len), l4s == m
-                        }
-                    }
-                }
-                if (!is_v4 && !l4do) { r0 = 0; m = 0; e = 0; }
-                if (is_v4 && !l4do) e = m;
-            }
-        }
-
-        // ---- 4. window sums: A=[r0,m), B=[m,min(e,win)) in slot coordinates --
-        const int rs = r0 ? r0 + sh : 0;
-        const int ms = m ? m + sh : 0;
-        const int es = e ? e + sh : ms;
-        const int ew = min(es, kWin);
+        // ---- 3. parse + window sums (lane l <-> frame l) -------------------
+        Parsed P{};
+        if (desc_bad) P.st = PNET_ST_DESC_INVALID;
+        else if (in_batch) P = parse_lds(slot + sh, len);
+        const int rs = P.r0 ? P.r0 + sh : 0;
+        const int ms = P.m ? P.m + sh : 0;
+        const int es = P.e ? P.e + sh : ms;
         uint32_t tA = 0, tB = 0;
-        {
-            const uint32_t* s32 = reinterpret_cast<const uint32_t*>(slot);
-#pragma unroll
-            for (int k = 0; k < NW * 4; ++k) {
-                const uint32_t d = s32[k];
-                const int t = 4 * k;
-                const uint32_t f0 = first_bytes(clamp04(rs - t));
-                const uint32_t f1 = first_bytes(clamp04(ms - t));
-                const uint32_t f2 = first_bytes(clamp04(ew - t));
-                tA = sad(d & f1 & ~f0, tA);
-                tB = sad(d & f2 & ~f1, tB);
-            }
-        }
+        window_sums(slot, rs, ms, min(es, kWin), tA, tB);
 
-        // ---- 5. tail: granules [NW, ceil(es/16)) by groups of G lanes ------
-        const uint64_t need_tail = __ballot(es > kWin);
-        if (need_tail) {
-            L.end[lane] = (uint32_t)es;
+        // ---- 4. tail: frames longer than the window, via a per-wave work list --
+        const bool has_tail = es > kWin;
+        const uint64_t tmask = __ballot(has_tail);
+        if (tmask) {
+            const int count = __popcll(tmask);
+            if (has_tail) {
+                const int pos = __popcll(tmask & ((1ull << lane) - 1ull));
+                L.list[pos] = (uint8_t)lane;
+                L.end[lane] = (uint32_t)es;
+            }
             wave_sync();
-            const int j = lane % G;
-#pragma unroll 1
-            for (int s = 0; s < G; ++s) {
-                const uint64_t setmask = (kFps == 64 ? ~0ull : ((1ull << kFps) - 1ull)) << (s * kFps);
-                if (!(need_tail & setmask)) continue;      // wave-uniform
-                const int fl = s * kFps + lane / G;
-                const uint32_t fe = L.end[fl];
-                const uint8_t* fb = a.data + L.base[fl];
-                const uint32_t nneed = (fe + 15u) >> 4;
-                uint32_t acc = 0;
-                constexpr int U = 4;
-#pragma unroll 1
-                for (uint32_t c0 = NW + j; c0 < nneed; c0 += U * G) {
+            const int grp = lane / G, j = lane % G;
+            int idx = grp;
+            int fl = 0;
+            uint32_t fe = 0, nneed = 0, c0 = 0, acc = 0;
+            const uint8_t* fb = a.data;
+            if (idx < count) {
+                fl = L.list[idx];
+                fe = L.end[fl];
+                fb = a.data + L.base[fl];
+                nneed = (fe + 15u) >> 4;
+                c0 = NW + j;
+            }
+            while (__ballot(idx < count)) {
+                if (idx < count) {
                     uint4 v[U];
 #pragma unroll
                     for (int u = 0; u < U; ++u) {
                         const uint32_t c = c0 + u * G;
-                        v[u] = c < nneed ? *reinterpret_cast<const uint4*>(fb + 16u * c) : make_uint4(0, 0, 0, 0);
+                        v[u] = c < nneed ? (NT ? load16_nt(fb + 16u * c) : load16(fb + 16u * c))
+                                         : make_uint4(0, 0, 0, 0);
                     }
 #pragma unroll
                     for (int u = 0; u < U; ++u) {
-                        const int p = (int)(16u * (c0 + u * G));
-                        const uint32_t dw[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+                        const uint32_t c = c0 + u * G;
+                        uint32_t x = v[u].x, y = v[u].y, z = v[u].z, w = v[u].w;
+                        if (c + 1 == nneed && (fe & 15u)) {   // last granule: drop bytes past the end
+                            const int r = (int)(fe & 15u);
+                            x &= first_bytes(clamp04(r));
+                            y &= first_bytes(clamp04(r - 4));
+                            z &= first_bytes(clamp04(r - 8));
+                            w &= first_bytes(clamp04(r - 12));
+                        }
+                        acc = sad(x, acc);
+                        acc = sad(y, acc);
+                        acc = sad(z, acc);
+                        acc = sad(w, acc);
+                    }
+                    c0 += U * G;
+                    if (c0 - j >= nneed) {                      // group-uniform: frame done
 #pragma unroll
-                        for (int t = 0; t < 4; ++t) acc = sad(dw[t] & first_bytes(clamp04((int)fe - p - 4 * t)), acc);
+                        for (int o = G / 2; o >= 1; o >>= 1) acc += __shfl_xor(acc, o);
+                        if (j == 0) L.tail[fl] = acc;
+                        acc = 0;
+                        idx += kGroups;
+                        if (idx < count) {
+                            fl = L.list[idx];
+                            fe = L.end[fl];
+                            fb = a.data + L.base[fl];
+                            nneed = (fe + 15u) >> 4;
+                            c0 = NW + j;
+                        }
                     }
                 }
-#pragma unroll
-                for (int o = G / 2; o >= 1; o >>= 1) acc += __shfl_xor(acc, o);
-                if (j == 0) L.tail[fl] = acc;
             }
             wave_sync();
-            if (es > kWin) tB += L.tail[lane];
+            if (has_tail) tB += L.tail[lane];
         }
 
-        // ---- 6. finalize ---------------------------------------------------
-        const bool odd = (off & 1) != 0;
+        // ---- 5. finalize + stores ------------------------------------------
         uint32_t ipc = 0, l4c = 0;
-        if (is_v4) {
-            tA -= odd ? ipstored : bswap16(ipstored);      // skipword 5 (ipv4.rs:177)
-        }
-        if (l4do) {
-            tB -= odd ? l4stored : bswap16(l4stored);      // skipword 3 / 8 / 1
-        }
-        uint32_t pA = fold16(tA), pB = fold16(tB);
-        if (!odd) { pA = bswap16(pA); pB = bswap16(pB); }
-        if (is_v4) {
-            ipc = (~pA) & 0xFFFFu;
-            if (ipc == ipstored) st |= PNET_ST_IP_CSUM_OK;
-        }
-        if (l4do) {
-            const uint32_t sum = pB + pseudo + (v6pseudo ? pA : 0u);
-            l4c = (~fold16(sum)) & 0xFFFFu;
-            st |= PNET_ST_L4_CSUM_DONE;
-            if (l4c == l4stored) st |= PNET_ST_L4_CSUM_OK;
-        }
-
-        if (in_batch) {
-            const pnetgpu_rx_columns& C = a.cols;
-            if (C.status) C.status[f] = (uint16_t)st;
-            if (C.ip_csum) C.ip_csum[f] = (uint16_t)ipc;
-            if (C.l4_csum) C.l4_csum[f] = (uint16_t)l4c;
-            if (C.ethertype) C.ethertype[f] = (uint16_t)et;
-            if (C.ip_proto) C.ip_proto[f] = (uint8_t)proto;
-            if (C.ttl) C.ttl[f] = (uint8_t)ttl;
-            if (C.l4_offset) C.l4_offset[f] = (uint16_t)l4off;
-            if (C.l4_length) C.l4_length[f] = (uint16_t)l4len;
-            if (C.src_port) C.src_port[f] = (uint16_t)sp;
-            if (C.dst_port) C.dst_port[f] = (uint16_t)dp;
-            if (C.src_ipv4) C.src_ipv4[f] = s4;
-            if (C.dst_ipv4) C.dst_ipv4[f] = d4;
-            if (C.src_ipv6 || C.dst_ipv6) {
-                const bool v6ok = (st & (PNET_ST_L3_MASK | PNET_ST_L3_MALFORMED)) == PNET_ST_L3_IPV6;
-                uint4 sv = make_uint4(0, 0, 0, 0), dv = make_uint4(0, 0, 0, 0);
-                if (v6ok) {
-                    sv = lds_read16_unaligned(slot, sh + 22);
-                    dv = lds_read16_unaligned(slot, sh + 38);
-                }
-                if (C.src_ipv6) reinterpret_cast<uint4*>(C.src_ipv6)[f] = sv;
-                if (C.dst_ipv6) reinterpret_cast<uint4*>(C.dst_ipv6)[f] = dv;
-            }
-        }
-        if (a.cols.counters) {
-            c_frames += (uint32_t)__popcll(__ballot(in_batch && !desc_bad));
-            c_bytes += len;
-            c_v4 += (uint32_t)__popcll(__ballot((st & PNET_ST_L3_MASK) == PNET_ST_L3_IPV4));
-            c_v6 += (uint32_t)__popcll(__ballot((st & PNET_ST_L3_MASK) == PNET_ST_L3_IPV6));
-            c_ipbad += (uint32_t)__popcll(__ballot(is_v4 && !(st & PNET_ST_IP_CSUM_OK)));
-            c_l4bad += (uint32_t)__popcll(__ballot(l4do && !(st & PNET_ST_L4_CSUM_OK)));
-            c_malf += (uint32_t)__popcll(__ballot((st & (PNET_ST_ETH_MALFORMED | PNET_ST_L3_MALFORMED |
-                                                         PNET_ST_L4_MALFORMED | PNET_ST_DESC_INVALID)) != 0));
-            c_unk += (uint32_t)__popcll(__ballot((st & (PNET_ST_UNKNOWN_ETHERTYPE | PNET_ST_UNKNOWN_PROTO)) != 0));
-        }
-        wave_sync();   // slots are rewritten by the next run
+        finalize(P, tA, tB, (off & 1) != 0, ipc, l4c);
+        store_columns(a.cols, f0, lane, in_batch, P, ipc, l4c, slot, sh);
+        if (a.cols.counters) K.add(in_batch && !desc_bad, len, P.st);
+        wave_sync();   // slots and lists are rewritten by the next run
     }
-
-    if (a.cols.counters) {
-        // bytes: per-lane u64 -> wave sum; the ballot counters are already wave-uniform
-        for (int o = 32; o >= 1; o >>= 1) {
-            uint32_t lo = (uint32_t)c_bytes, hi = (uint32_t)(c_bytes >> 32);
-            lo = __shfl_xor(lo, o);
-            hi = __shfl_xor(hi, o);
-            c_bytes += ((uint64_t)hi << 32) | lo;
-        }
-        if (lane == 0) {
-            blk_ctr[wv][PNETGPU_CTR_FRAMES] = c_frames;
-            blk_ctr[wv][PNETGPU_CTR_BYTES] = c_bytes;
-            blk_ctr[wv][PNETGPU_CTR_IPV4] = c_v4;
-            blk_ctr[wv][PNETGPU_CTR_IPV6] = c_v6;
-            blk_ctr[wv][PNETGPU_CTR_IP_CSUM_BAD] = c_ipbad;
-            blk_ctr[wv][PNETGPU_CTR_L4_CSUM_BAD] = c_l4bad;
-            blk_ctr[wv][PNETGPU_CTR_MALFORMED] = c_malf;
-            blk_ctr[wv][PNETGPU_CTR_UNKNOWN] = c_unk;
-        }
-        __syncthreads();
-        if (threadIdx.x < PNETGPU_NCOUNTERS) {
-            uint64_t v = 0;
-            for (int w = 0; w < kWavesPerBlock; ++w) v += blk_ctr[w][threadIdx.x];
-            if (v) atomicAdd(reinterpret_cast<unsigned long long*>(a.cols.counters + threadIdx.x),
-                             (unsigned long long)v);
-        }
-    }
+    if (a.cols.counters) K.flush(a.cols.counters, blk_ctr, wv, lane);
 }
 
 // ---------------------------------------------------------------------------
@@ -433,15 +679,10 @@ __global__ __launch_bounds__(kBlock) void slice_kernel(SliceArgs a) {
     // groups are 16-lane aligned, so every shuffle below stays inside one group,
     // whose lanes share i (and therefore control flow)
     for (uint64_t i = gid; i < a.n; i += ngroups) {
-        const bool active = true;
-        uint64_t off = 0;
-        uint32_t len = 0, skip = 0xFFFFFFFFu;
-        if (active) {
-            off = a.offsets[i] + a.delta;
-            len = a.lengths[i];
-            skip = a.skipwords[i];
-        }
-        const bool bad = active && (off > a.limit || (uint64_t)len > a.limit - off);
+        uint64_t off = a.offsets[i] + a.delta;
+        uint32_t len = a.lengths[i];
+        const uint32_t skip = a.skipwords[i];
+        const bool bad = off > a.limit || (uint64_t)len > a.limit - off;
         if (bad) len = 0;
         const int sh = (int)(off & 15);
         const uint8_t* fb = a.data + (off - (uint64_t)sh);
@@ -461,7 +702,7 @@ __global__ __launch_bounds__(kBlock) void slice_kernel(SliceArgs a) {
         }
 #pragma unroll
         for (int o = G / 2; o >= 1; o >>= 1) acc += __shfl_xor(acc, o);
-        if (j == 0 && active) {
+        if (j == 0) {
             // skipped word: bytes [2*skip, 2*skip+2) of the slice that exist (util.rs:166-178)
             const uint8_t* sb = a.data + off;
             if ((uint64_t)skip * 2 < len) {
@@ -491,30 +732,51 @@ __global__ __launch_bounds__(kBlock) void slice_kernel(SliceArgs a) {
     }
 }
 
-template <int NW, int G>
-int launch_rx_t(const RxArgs& args, int blocks, hipStream_t stream) {
-    hipLaunchKernelGGL((rx_kernel<NW, G>), dim3(blocks), dim3(kBlock), 0, stream, args);
-    return hipGetLastError() == hipSuccess ? 0 : -1;
+// Resident 256-thread blocks per CU for a kernel, from its register and LDS
+// footprint (a 256-thread block places one wave on each of the 4 SIMDs).
+static int resident_blocks(const void* fn) {
+    hipFuncAttributes fa;
+    if (hipFuncGetAttributes(&fa, fn) != hipSuccess) return -1;
+    const int vgpr = fa.numRegs > 0 ? ((fa.numRegs + 7) / 8) * 8 : 128;
+    int by_vgpr = vgpr > 0 ? 512 / vgpr : 1;
+    if (by_vgpr > 8) by_vgpr = 8;
+    const int lds = (int)fa.sharedSizeBytes;
+    const int by_lds = lds > 0 ? (160 * 1024) / lds : 8;
+    const int nb = by_vgpr < by_lds ? by_vgpr : by_lds;
+    return nb > 0 ? nb : 1;
+}
+
+template <int G>
+const void* rx_fn() {
+    return reinterpret_cast<const void*>(rx_kernel<8, G, 4, (G >= 64)>);
 }
 
 }  // namespace
 
-int rx_blocks_per_cu(int nw, int g) {
-    int nb = 0;
-    hipError_t err = hipSuccess;
-#define PNET_OCC(NW_, G_)                                                                     \
-    if (nw == NW_ && g == G_)                                                                 \
-        err = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, rx_kernel<NW_, G_>, kBlock, 0);
-    PNET_OCC(4, 16) PNET_OCC(8, 4) PNET_OCC(8, 16) PNET_OCC(8, 64)
-#undef PNET_OCC
-    return err == hipSuccess && nb > 0 ? nb : 1;
+int rx_blocks_per_cu(int kind, int g, int* numregs, int* lds) {
+    const void* fn = kind == kKindSmall ? reinterpret_cast<const void*>(rx_small_kernel)
+                     : g == 64          ? rx_fn<64>()
+                     : g == 16          ? rx_fn<16>()
+                                        : rx_fn<8>();
+    hipFuncAttributes fa;
+    if (hipFuncGetAttributes(&fa, fn) == hipSuccess) {
+        if (numregs) *numregs = fa.numRegs;
+        if (lds) *lds = (int)fa.sharedSizeBytes;
+    }
+    return resident_blocks(fn);
 }
 
-int launch_rx(const RxArgs& args, int nw, int g, int blocks, hipStream_t stream) {
-    if (nw == 4) return launch_rx_t<4, 16>(args, blocks, stream);
-    if (g == 4) return launch_rx_t<8, 4>(args, blocks, stream);
-    if (g == 64) return launch_rx_t<8, 64>(args, blocks, stream);
-    return launch_rx_t<8, 16>(args, blocks, stream);
+int launch_rx(const RxArgs& args, int kind, int g, int blocks, hipStream_t stream) {
+    if (kind == kKindSmall) {
+        hipLaunchKernelGGL(rx_small_kernel, dim3(blocks), dim3(kBlock), 0, stream, args);
+    } else if (g == 64) {
+        hipLaunchKernelGGL((rx_kernel<8, 64, 4, true>), dim3(blocks), dim3(kBlock), 0, stream, args);
+    } else if (g == 16) {
+        hipLaunchKernelGGL((rx_kernel<8, 16, 4, false>), dim3(blocks), dim3(kBlock), 0, stream, args);
+    } else {
+        hipLaunchKernelGGL((rx_kernel<8, 8, 4, false>), dim3(blocks), dim3(kBlock), 0, stream, args);
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 int launch_slices(const SliceArgs& args, int pseudo, int blocks, hipStream_t stream) {

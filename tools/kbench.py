@@ -1,0 +1,60 @@
+#!/usr/bin/env python3
+"""Kernel tuning harness: times pnetgpu_rx_process per workload under several
+env settings (e.g. PNETGPU_BLOCKS_PER_CU) in ONE process, interleaved rounds.
+
+  python tools/kbench.py --workloads udp64,tcp1500 --env PNETGPU_BLOCKS_PER_CU=1,2,3,4,6,8
+"""
+import argparse
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import libpnet_amd as lp  # noqa: E402
+from bench import Shard, HBM_PEAK_GBS, WORKLOADS  # noqa: E402
+
+EXTRA = {"imix": 1 << 22, "udp6_jumbo": 1 << 17}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--workloads", default="udp64,tcp1500")
+    ap.add_argument("--env", default="")
+    ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--rounds", type=int, default=3)
+    a = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    key, vals = (a.env.split("=") + [""])[:2] if a.env else ("", "")
+    vals = vals.split(",") if vals else [None]
+    s = torch.cuda.Stream()
+    for name in a.workloads.split(","):
+        n = WORKLOADS[name]["n"] if name in WORKLOADS else EXTRA[name]
+        sh = Shard(name, n, 1, dev)
+        times = {v: [] for v in vals}
+        for _ in range(a.rounds):
+            for v in vals:
+                if key:
+                    os.environ[key] = v
+                for _ in range(2):
+                    sh.step(s)
+                evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.reps)]
+                for e0, e1 in evs:
+                    e0.record(s)
+                    sh.step(s)
+                    e1.record(s)
+                s.synchronize()
+                times[v] += [e0.elapsed_time(e1) for e0, e1 in evs]
+        for v in vals:
+            t = np.array(times[v])
+            med = float(np.median(t))
+            print(f"{name:10s} {key}={v}: median {med*1e3:8.1f} us  min {t.min()*1e3:8.1f} us  "
+                  f"alg {sh.alg_bytes/med/1e6:7.0f} GB/s ({sh.alg_bytes/med/1e6/HBM_PEAK_GBS:.1%})  "
+                  f"{sh.n/med/1e3:9.0f} Mpkts/s", flush=True)
+        del sh
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()
