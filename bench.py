@@ -25,6 +25,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 import libpnet_amd as lp  # noqa: E402
+from libpnet_amd import shard  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (/opt/skills/guides/MI355X_MICROARCH.md:36)
 METRIC = "device-resident Mpkts/s & GB/s, checksum+parse, 64B & 1500B, 1/2/4/8 GPU"
@@ -33,6 +34,11 @@ WORKLOADS = {
                                     "device-resident batch"},
     "tcp1500": {"n": 1 << 20, "kernel": "rx_kernel<8, 8, 4, false>", "desc": "configs[2]: 1500B TCP/IPv4/Ethernet, full-MTU ones-complement sum over "
                                       "pseudo-header+payload"},
+    # not in the default run: the 8-GPU configs, per-GPU shard sizes (weak scaling)
+    "imix": {"n": 1 << 22, "kernel": "rx_kernel<8, 8, 4, false>",
+             "desc": "configs[3]: IMIX 64/576/1500B 7:4:1 Eth/IPv4/{UDP,TCP,ICMP}, descriptor mode, per-GPU shard"},
+    "udp6_jumbo": {"n": 1 << 17, "kernel": "rx_kernel<8, 64, 4, true>",
+                   "desc": "configs[4]: 9000B IPv6/UDP jumbo frames, IPv6 pseudo-header checksum, per-GPU shard"},
 }
 
 
@@ -204,11 +210,8 @@ def main():
         wall, kern_ms = time_shard(sh, args.steps, args.warmup, stream, dist_on)
         # counters: one RCCL all-reduce at the end (the "final throughput reduction")
         ctr_t = torch.tensor([ctr[k] for k in lp.COUNTER_NAMES] + [int(ok)], dtype=torch.int64, device=device)
-        wall_t = torch.tensor([wall], dtype=torch.float64, device=device)
-        if dist_on:
-            torch.distributed.all_reduce(ctr_t, op=torch.distributed.ReduceOp.SUM)
-            torch.distributed.all_reduce(wall_t, op=torch.distributed.ReduceOp.MAX)
-        wall = float(wall_t.item())
+        shard.all_reduce_counters(ctr_t)
+        wall = shard.all_reduce_max(wall, device)
         frames_all = sh.n * world * args.steps
         avg_ms = float(np.mean(kern_ms))
         achieved = sh.alg_bytes / (avg_ms * 1e-3) / 1e9
