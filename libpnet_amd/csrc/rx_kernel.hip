@@ -296,24 +296,34 @@ struct Counters {
     }
 };
 
+// Column element store (streaming: written once, never re-read by the kernel)
+template <class T>
+__device__ __forceinline__ void put(T* col, uint64_t i, T v) {
+#ifdef PNET_PLAIN_STORES
+    col[i] = v;
+#else
+    __builtin_nontemporal_store(v, col + i);
+#endif
+}
+
 // Column stores for the frames of one run: the base is wave-uniform (SGPR) and
 // the lane adds its index, so each store is one coalesced wave instruction.
 __device__ __forceinline__ void store_columns(const pnetgpu_rx_columns& C, uint64_t f0, int lane, bool in_batch,
                                               const Parsed& P, uint32_t ipc, uint32_t l4c, const uint8_t* slot,
                                               int sh) {
     if (!in_batch) return;
-    if (C.status) C.status[f0 + lane] = (uint16_t)P.st;
-    if (C.ip_csum) C.ip_csum[f0 + lane] = (uint16_t)ipc;
-    if (C.l4_csum) C.l4_csum[f0 + lane] = (uint16_t)l4c;
-    if (C.ethertype) C.ethertype[f0 + lane] = (uint16_t)P.et;
-    if (C.ip_proto) C.ip_proto[f0 + lane] = (uint8_t)P.proto;
-    if (C.ttl) C.ttl[f0 + lane] = (uint8_t)P.ttl;
-    if (C.l4_offset) C.l4_offset[f0 + lane] = (uint16_t)P.l4off;
-    if (C.l4_length) C.l4_length[f0 + lane] = (uint16_t)P.l4len;
-    if (C.src_port) C.src_port[f0 + lane] = (uint16_t)P.sp;
-    if (C.dst_port) C.dst_port[f0 + lane] = (uint16_t)P.dp;
-    if (C.src_ipv4) C.src_ipv4[f0 + lane] = P.s4;
-    if (C.dst_ipv4) C.dst_ipv4[f0 + lane] = P.d4;
+    if (C.status) put<uint16_t>(C.status, f0 + lane, (uint16_t)P.st);
+    if (C.ip_csum) put<uint16_t>(C.ip_csum, f0 + lane, (uint16_t)ipc);
+    if (C.l4_csum) put<uint16_t>(C.l4_csum, f0 + lane, (uint16_t)l4c);
+    if (C.ethertype) put<uint16_t>(C.ethertype, f0 + lane, (uint16_t)P.et);
+    if (C.ip_proto) put<uint8_t>(C.ip_proto, f0 + lane, (uint8_t)P.proto);
+    if (C.ttl) put<uint8_t>(C.ttl, f0 + lane, (uint8_t)P.ttl);
+    if (C.l4_offset) put<uint16_t>(C.l4_offset, f0 + lane, (uint16_t)P.l4off);
+    if (C.l4_length) put<uint16_t>(C.l4_length, f0 + lane, (uint16_t)P.l4len);
+    if (C.src_port) put<uint16_t>(C.src_port, f0 + lane, (uint16_t)P.sp);
+    if (C.dst_port) put<uint16_t>(C.dst_port, f0 + lane, (uint16_t)P.dp);
+    if (C.src_ipv4) put<uint32_t>(C.src_ipv4, f0 + lane, P.s4);
+    if (C.dst_ipv4) put<uint32_t>(C.dst_ipv4, f0 + lane, P.d4);
     if (C.src_ipv6 || C.dst_ipv6) {
         const bool v6ok = (P.st & (PNET_ST_L3_MASK | PNET_ST_L3_MALFORMED)) == PNET_ST_L3_IPV6;
         uint4 sv = make_uint4(0, 0, 0, 0), dv = make_uint4(0, 0, 0, 0);
@@ -346,7 +356,7 @@ __device__ __forceinline__ SmallRun small_load(const RxArgs& a, uint64_t run, in
         const uint64_t f = run * kWave + 16 * i + (lane >> 2);
         r.g[i] = make_uint4(0, 0, 0, 0);
         if (f < a.n && c < span)
-            r.g[i] = load16(a.data + (a.first + a.delta) + f * a.stride + 16u * c);
+            r.g[i] = load16_nt(a.data + (a.first + a.delta) + f * a.stride + 16u * c);
     }
     return r;
 }

@@ -1,0 +1,98 @@
+// sol.hip — speed-of-light micro-benchmarks for the receive path's traffic mix
+// on MI355X: how fast can a kernel that does NO parsing move the same bytes?
+//   read      : stream 1 GiB with coalesced dwordx4 loads, fold into one word/wave
+//   read+cols : the same reads + 26 B/frame of SoA column stores (64-B frames)
+//   copy      : float4 copy 1 GiB -> 1 GiB (the guide's 6.29 TB/s reference point)
+// Build: hipcc --offload-arch=gfx950 -O3 -o tools/sol tools/sol.hip
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdint>
+#include <vector>
+#include <algorithm>
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s at %d\n", hipGetErrorString(e), __LINE__); return 1; } } while (0)
+
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+
+template <int UNROLL, bool NT>
+__global__ __launch_bounds__(256) void read_kernel(const uint4* __restrict__ in, size_t n16, uint32_t* out) {
+    uint32_t acc = 0;
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (; i + (UNROLL - 1) * stride < n16; i += UNROLL * stride) {
+        uint4 v[UNROLL];
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) {
+            if (NT) { u32x4_t t = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(in + i + u * stride)); v[u] = make_uint4(t.x, t.y, t.z, t.w); }
+            else v[u] = in[i + u * stride];
+        }
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) acc += v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+    }
+    for (; i < n16; i += stride) { uint4 t = in[i]; acc += t.x ^ t.y ^ t.z ^ t.w; }
+    if (acc == 0x12345678u) out[0] = acc;   // keep the loads alive
+}
+
+// 64-B frames: wave loads 4 KiB (64 frames) coalesced, writes 26 B/frame of columns
+__global__ __launch_bounds__(256) void read_cols_kernel(const uint4* __restrict__ in, size_t nframes, uint16_t* c16,
+                                                        uint32_t* c32, uint8_t* c8) {
+    const int lane = threadIdx.x & 63;
+    const size_t wave = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const size_t nwaves = ((size_t)gridDim.x * blockDim.x) >> 6;
+    for (size_t run = wave; run * 64 < nframes; run += nwaves) {
+        const uint4* p = in + run * 256;
+        uint4 v0 = p[lane], v1 = p[64 + lane], v2 = p[128 + lane], v3 = p[192 + lane];
+        uint32_t x = v0.x ^ v1.y ^ v2.z ^ v3.w;
+        const size_t f = run * 64 + lane;
+        // 8 x u16 columns + 2 x u32 + 2 x u8 = 26 B
+#pragma unroll
+        for (int k = 0; k < 8; ++k) c16[(size_t)k * nframes + f] = (uint16_t)(x + k);
+        c32[f] = x;
+        c32[nframes + f] = x ^ 1;
+        c8[f] = (uint8_t)x;
+        c8[nframes + f] = (uint8_t)(x >> 8);
+    }
+}
+
+__global__ __launch_bounds__(256) void copy_kernel(const uint4* __restrict__ in, uint4* __restrict__ out, size_t n16) {
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += stride) out[i] = in[i];
+}
+
+template <class F>
+float time_it(F f, int reps) {
+    hipEvent_t a, b;
+    hipEventCreate(&a); hipEventCreate(&b);
+    f(); f();
+    std::vector<float> t;
+    for (int r = 0; r < reps; ++r) {
+        hipEventRecord(a); f(); hipEventRecord(b); hipEventSynchronize(b);
+        float ms; hipEventElapsedTime(&ms, a, b); t.push_back(ms);
+    }
+    std::sort(t.begin(), t.end());
+    return t[t.size() / 2];
+}
+
+int main() {
+    const size_t bytes = 1ull << 30, n16 = bytes / 16, nframes = bytes / 64;
+    uint4 *in, *out; uint32_t* o; uint16_t* c16; uint32_t* c32; uint8_t* c8;
+    CK(hipMalloc(&in, bytes)); CK(hipMalloc(&out, bytes)); CK(hipMalloc(&o, 64));
+    CK(hipMalloc(&c16, nframes * 16)); CK(hipMalloc(&c32, nframes * 8)); CK(hipMalloc(&c8, nframes * 2));
+    CK(hipMemset(in, 1, bytes));
+    int cus = 256;
+    for (int bpc : {4, 8, 16}) {
+        const int grid = cus * bpc;
+        float ms = time_it([&] { read_kernel<4, false><<<grid, 256>>>(in, n16, o); }, 20);
+        printf("read    plain U4 grid=%5d: %7.1f us  %6.0f GB/s\n", grid, ms * 1e3, bytes / ms / 1e6);
+        ms = time_it([&] { read_kernel<4, true><<<grid, 256>>>(in, n16, o); }, 20);
+        printf("read    nt    U4 grid=%5d: %7.1f us  %6.0f GB/s\n", grid, ms * 1e3, bytes / ms / 1e6);
+        ms = time_it([&] { read_kernel<8, false><<<grid, 256>>>(in, n16, o); }, 20);
+        printf("read    plain U8 grid=%5d: %7.1f us  %6.0f GB/s\n", grid, ms * 1e3, bytes / ms / 1e6);
+        ms = time_it([&] { read_cols_kernel<<<grid, 256>>>(in, nframes, c16, c32, c8); }, 20);
+        printf("read+26B cols  grid=%5d: %7.1f us  %6.0f GB/s (alg %zu B)\n", grid, ms * 1e3,
+               (bytes + nframes * 26) / ms / 1e6, bytes + nframes * 26);
+        ms = time_it([&] { copy_kernel<<<grid, 256>>>(in, out, n16); }, 20);
+        printf("copy           grid=%5d: %7.1f us  %6.0f GB/s (r+w)\n", grid, ms * 1e3, 2.0 * bytes / ms / 1e6);
+    }
+    return 0;
+}
