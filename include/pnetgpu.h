@@ -19,6 +19,9 @@
  *                             tcp.rs:239-286, icmp.rs:70-75, icmpv6.rs:80-85,
  *                             generated accessors pnet_macros/src/decorator.rs:1563-1670,
  *                             payload bounds decorator.rs:713-769.
+ *   pnetgpu_tx_fill_checksums the sender side: set_checksum(ipv4::checksum(..)),
+ *                             set_checksum(udp|tcp::ipv4_checksum(..)) etc. as
+ *                             benches/rs_sender.rs:38-39,70-71 does per frame.
  *   pnetgpu_checksum_slices   pnet_packet::util::checksum (pnet_packet/src/util.rs:76-82),
  *                             re-exported as pnet::util::checksum (src/util.rs:11-12),
  *                             over a batch of slices.
@@ -148,6 +151,17 @@ void pnetgpu_ctx_destroy(pnetgpu_ctx* ctx);
 /* Receive path: parse + verify every frame of `batch`, write `cols`. */
 int pnetgpu_rx_process(pnetgpu_ctx* ctx, const pnetgpu_batch* batch,
                        const pnetgpu_rx_columns* cols, void* stream);
+
+/* Transmit side: for every checksum the receive path computes (IPv4 header;
+ * UDP/TCP over IPv4/IPv6; ICMP; ICMPv6 over IPv6), write the computed value
+ * big-endian into the frame's stored field, in place — the
+ * MutableIpv4Packet/MutableUdpPacket/... set_checksum(checksum(..)) calls of the
+ * reference's packet builders (benches/rs_sender.rs:38-39,70-71; setters
+ * pnet_macros/src/decorator.rs:1490-1530). `batch->data` must be writable and
+ * frames must not overlap. `cols` (optional columns) report the frames as they
+ * were BEFORE patching (status OK bits = "was already correct"). */
+int pnetgpu_tx_fill_checksums(pnetgpu_ctx* ctx, const pnetgpu_batch* batch,
+                              const pnetgpu_rx_columns* cols, void* stream);
 
 /* out[i] = util::checksum(data[offsets[i], +lengths[i]), skipwords[i]) */
 int pnetgpu_checksum_slices(pnetgpu_ctx* ctx, const uint8_t* data, uint64_t data_bytes,

@@ -77,8 +77,9 @@ def _load():
     L.pnetgpu_ctx_create.argtypes = [i32, ctypes.POINTER(vp)]
     L.pnetgpu_ctx_destroy.restype = None
     L.pnetgpu_ctx_destroy.argtypes = [vp]
-    L.pnetgpu_rx_process.restype = i32
-    L.pnetgpu_rx_process.argtypes = [vp, ctypes.POINTER(Batch), ctypes.POINTER(RxColumns), vp]
+    for f in (L.pnetgpu_rx_process, L.pnetgpu_tx_fill_checksums):
+        f.restype = i32
+        f.argtypes = [vp, ctypes.POINTER(Batch), ctypes.POINTER(RxColumns), vp]
     L.pnetgpu_checksum_slices.restype = i32
     L.pnetgpu_checksum_slices.argtypes = [vp, vp, u64, u64, vp, vp, vp, vp, vp]
     for f in (L.pnetgpu_ipv4_checksum_slices, L.pnetgpu_ipv6_checksum_slices):

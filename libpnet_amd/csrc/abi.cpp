@@ -84,8 +84,8 @@ int pnetgpu_ctx_create(int device, pnetgpu_ctx** out) {
 
 void pnetgpu_ctx_destroy(pnetgpu_ctx* ctx) { delete ctx; }
 
-int pnetgpu_rx_process(pnetgpu_ctx* ctx, const pnetgpu_batch* b, const pnetgpu_rx_columns* cols,
-                       void* stream) {
+static int rx_common(pnetgpu_ctx* ctx, const pnetgpu_batch* b, const pnetgpu_rx_columns* cols, void* stream,
+                     bool tx) {
     if (!ctx || !b || !cols) return PNETGPU_EINVAL;
     if (b->n_frames == 0) return PNETGPU_OK;
     if (!b->data) return PNETGPU_EINVAL;
@@ -139,8 +139,17 @@ int pnetgpu_rx_process(pnetgpu_ctx* ctx, const pnetgpu_batch* b, const pnetgpu_r
     const uint64_t want = (a.nruns + kWavesPerBlock - 1) / kWavesPerBlock;
     const uint64_t cap = (uint64_t)ctx->cus * (uint64_t)per_cu;
     const int blocks = (int)std::max<uint64_t>(1, std::min(want, cap));
-    if (pnetgpu::launch_rx(a, kind, g, blocks, static_cast<hipStream_t>(stream)) != 0) return PNETGPU_EHIP;
+    if (pnetgpu::launch_rx(a, kind, g, blocks, tx, static_cast<hipStream_t>(stream)) != 0) return PNETGPU_EHIP;
     return PNETGPU_OK;
+}
+
+int pnetgpu_rx_process(pnetgpu_ctx* ctx, const pnetgpu_batch* b, const pnetgpu_rx_columns* cols, void* stream) {
+    return rx_common(ctx, b, cols, stream, false);
+}
+
+int pnetgpu_tx_fill_checksums(pnetgpu_ctx* ctx, const pnetgpu_batch* b, const pnetgpu_rx_columns* cols,
+                              void* stream) {
+    return rx_common(ctx, b, cols, stream, true);
 }
 
 static int slices_common(pnetgpu_ctx* ctx, const uint8_t* data, uint64_t data_bytes, uint64_t n,

@@ -42,7 +42,7 @@ constexpr int kKindSmall = 1;
 constexpr int kKindGeneric = 0;
 
 int rx_blocks_per_cu(int kind, int g, int* numregs, int* lds);
-int launch_rx(const RxArgs& args, int kind, int g, int blocks, hipStream_t stream);
+int launch_rx(const RxArgs& args, int kind, int g, int blocks, bool tx, hipStream_t stream);
 int launch_slices(const SliceArgs& args, int pseudo, int blocks, hipStream_t stream);
 
 }  // namespace pnetgpu

@@ -103,6 +103,7 @@ __device__ __forceinline__ uint4 lds_read16_unaligned(const uint8_t* slot, int p
 struct Parsed {
     uint32_t st, et, proto, ttl, l4off, l4len, sp, dp, s4, d4, ipstored, l4stored, pseudo;
     int r0, m, e;
+    int l4csum_at;            // frame offset of the L4 checksum field (valid when l4do)
     bool is_v4, l4do, v6pseudo;
 };
 
@@ -186,6 +187,7 @@ __device__ __forceinline__ Parsed parse_lds(const uint8_t* W, uint32_t len) {
                 if (P.proto == 17 || P.proto == 6) P.dp = ld16be(W, p + 2);
                 else P.dp = P.l4len >= 8 ? ld16be(W, p + 4) : 0u;
                 P.l4stored = ld16be(W, p + soff);
+                P.l4csum_at = p + soff;
                 if (P.proto == 1) {                            // icmp::checksum: no pseudo-header
                     P.l4do = true;
                     if (v6) { P.r0 = 54; P.m = 54; }
@@ -249,6 +251,21 @@ __device__ __forceinline__ void finalize(Parsed& P, uint32_t tA, uint32_t tB, bo
         l4c = (~fold16(pB + P.pseudo + (P.v6pseudo ? pA : 0u))) & 0xFFFFu;
         P.st |= PNET_ST_L4_CSUM_DONE;
         if (l4c == P.l4stored) P.st |= PNET_ST_L4_CSUM_OK;
+    }
+}
+
+// TX: write the computed checksums into the frame's stored fields (big-endian),
+// i.e. MutableIpv4Packet::set_checksum(ipv4::checksum(..)) and the L4
+// set_checksum(udp|tcp::ipv4_checksum(..) / icmp::checksum(..)) of
+// benches/rs_sender.rs:38-39,70-71. Byte stores: the fields may sit at odd addresses.
+__device__ __forceinline__ void tx_write(uint8_t* frame, const Parsed& P, uint32_t ipc, uint32_t l4c) {
+    if (P.is_v4) {
+        frame[24] = (uint8_t)(ipc >> 8);
+        frame[25] = (uint8_t)ipc;
+    }
+    if (P.st & PNET_ST_L4_CSUM_DONE) {
+        frame[P.l4csum_at] = (uint8_t)(l4c >> 8);
+        frame[P.l4csum_at + 1] = (uint8_t)l4c;
     }
 }
 
@@ -361,6 +378,7 @@ __device__ __forceinline__ SmallRun small_load(const RxArgs& a, uint64_t run, in
     return r;
 }
 
+template <bool TX>
 __global__ __launch_bounds__(kBlock, 5) void rx_small_kernel(RxArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t lds_slots[kWavesPerBlock][kWave * kSmallSlot];
     __shared__ uint64_t blk_ctr[kWavesPerBlock][PNETGPU_NCOUNTERS];
@@ -462,6 +480,7 @@ __global__ __launch_bounds__(kBlock, 5) void rx_small_kernel(RxArgs a) {
                                     stored_le = w9 & 0xFFFFu;                        // bytes 36,37
                                 }
                                 P.l4stored = bswap16(stored_le);
+                                P.l4csum_at = P.proto == 17 ? 40 : (P.proto == 6 ? 50 : 36);
                                 if (P.proto != 58) {       // ICMPv6 over IPv4: no checksum defined
                                     const int e = 34 + (int)P.l4len;
                                     uint32_t tB = sad(w8 & 0xFFFF0000u, 0u);
@@ -501,6 +520,8 @@ __global__ __launch_bounds__(kBlock, 5) void rx_small_kernel(RxArgs a) {
                 finalize(P, tA, tB, false, ipc, l4c);
             }
         }
+        if (TX && in_batch)
+            tx_write(const_cast<uint8_t*>(a.data) + (a.first + a.delta) + (f0 + lane) * a.stride, P, ipc, l4c);
         store_columns(a.cols, f0, lane, in_batch, P, ipc, l4c, slot, 0);
         if (a.cols.counters) K.add(in_batch, len, P.st);
         wave_sync();
@@ -522,7 +543,7 @@ struct WaveLds {
     uint8_t list[kWave];      // frames with a tail, in lane order
 };
 
-template <int NW, int G, int U, bool NT>
+template <int NW, int G, int U, bool NT, bool TX>
 __global__ __launch_bounds__(kBlock, 4) void rx_kernel(RxArgs a) {
     static_assert(NW == 8, "window granules");
     static_assert(G == 4 || G == 8 || G == 16 || G == 32 || G == 64, "tail group");
@@ -667,6 +688,7 @@ __global__ __launch_bounds__(kBlock, 4) void rx_kernel(RxArgs a) {
         // ---- 5. finalize + stores ------------------------------------------
         uint32_t ipc = 0, l4c = 0;
         finalize(P, tA, tB, (off & 1) != 0, ipc, l4c);
+        if (TX && in_batch && !desc_bad) tx_write(const_cast<uint8_t*>(a.data) + off, P, ipc, l4c);
         store_columns(a.cols, f0, lane, in_batch, P, ipc, l4c, slot, sh);
         if (a.cols.counters) K.add(in_batch && !desc_bad, len, P.st);
         wave_sync();   // slots and lists are rewritten by the next run
@@ -756,18 +778,36 @@ static int resident_blocks(const void* fn) {
     return nb > 0 ? nb : 1;
 }
 
-template <int G>
+template <int G, bool TX>
 const void* rx_fn() {
-    return reinterpret_cast<const void*>(rx_kernel<8, G, 4, (G >= 64)>);
+    return reinterpret_cast<const void*>(rx_kernel<8, G, 4, (G >= 64), TX>);
+}
+
+template <bool TX>
+const void* pick_fn(int kind, int g) {
+    return kind == kKindSmall ? reinterpret_cast<const void*>(rx_small_kernel<TX>)
+           : g == 64          ? rx_fn<64, TX>()
+           : g == 16          ? rx_fn<16, TX>()
+                              : rx_fn<8, TX>();
+}
+
+template <bool TX>
+void launch_t(const RxArgs& args, int kind, int g, int blocks, hipStream_t stream) {
+    if (kind == kKindSmall) {
+        hipLaunchKernelGGL(rx_small_kernel<TX>, dim3(blocks), dim3(kBlock), 0, stream, args);
+    } else if (g == 64) {
+        hipLaunchKernelGGL((rx_kernel<8, 64, 4, true, TX>), dim3(blocks), dim3(kBlock), 0, stream, args);
+    } else if (g == 16) {
+        hipLaunchKernelGGL((rx_kernel<8, 16, 4, false, TX>), dim3(blocks), dim3(kBlock), 0, stream, args);
+    } else {
+        hipLaunchKernelGGL((rx_kernel<8, 8, 4, false, TX>), dim3(blocks), dim3(kBlock), 0, stream, args);
+    }
 }
 
 }  // namespace
 
 int rx_blocks_per_cu(int kind, int g, int* numregs, int* lds) {
-    const void* fn = kind == kKindSmall ? reinterpret_cast<const void*>(rx_small_kernel)
-                     : g == 64          ? rx_fn<64>()
-                     : g == 16          ? rx_fn<16>()
-                                        : rx_fn<8>();
+    const void* fn = pick_fn<false>(kind, g);
     hipFuncAttributes fa;
     if (hipFuncGetAttributes(&fa, fn) == hipSuccess) {
         if (numregs) *numregs = fa.numRegs;
@@ -776,16 +816,9 @@ int rx_blocks_per_cu(int kind, int g, int* numregs, int* lds) {
     return resident_blocks(fn);
 }
 
-int launch_rx(const RxArgs& args, int kind, int g, int blocks, hipStream_t stream) {
-    if (kind == kKindSmall) {
-        hipLaunchKernelGGL(rx_small_kernel, dim3(blocks), dim3(kBlock), 0, stream, args);
-    } else if (g == 64) {
-        hipLaunchKernelGGL((rx_kernel<8, 64, 4, true>), dim3(blocks), dim3(kBlock), 0, stream, args);
-    } else if (g == 16) {
-        hipLaunchKernelGGL((rx_kernel<8, 16, 4, false>), dim3(blocks), dim3(kBlock), 0, stream, args);
-    } else {
-        hipLaunchKernelGGL((rx_kernel<8, 8, 4, false>), dim3(blocks), dim3(kBlock), 0, stream, args);
-    }
+int launch_rx(const RxArgs& args, int kind, int g, int blocks, bool tx, hipStream_t stream) {
+    if (tx) launch_t<true>(args, kind, g, blocks, stream);
+    else launch_t<false>(args, kind, g, blocks, stream);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -142,6 +142,22 @@ def rx_process(data, *, n_frames=None, stride=0, frame_len=None, first_offset=0,
     Fixed-stride mode: stride > 0, frame i = data[first_offset + i*stride, +frame_len).
     Descriptor mode:   offsets (int64) / lengths (int32) CUDA tensors, frame i = data[off_i, +len_i).
     Returns an RxResult (device columns, accumulated counters)."""
+    return _rx_or_tx("pnetgpu_rx_process", data, n_frames, stride, frame_len, first_offset, offsets, lengths,
+                     columns, counters, out, stream, data_bytes)
+
+
+def tx_fill_checksums(data, *, n_frames=None, stride=0, frame_len=None, first_offset=0, offsets=None,
+                      lengths=None, columns=("status",), counters=False, out=None, stream=None, data_bytes=None):
+    """Sender side: write every checksum the receive path computes into its field, in place
+    (set_checksum(ipv4::checksum(..)), set_checksum(udp::ipv4_checksum(..)), ... as
+    benches/rs_sender.rs:38-39,70-71). Frames must not overlap. The returned columns
+    describe the frames before patching."""
+    return _rx_or_tx("pnetgpu_tx_fill_checksums", data, n_frames, stride, frame_len, first_offset, offsets,
+                     lengths, columns, counters, out, stream, data_bytes)
+
+
+def _rx_or_tx(fn_name, data, n_frames, stride, frame_len, first_offset, offsets, lengths, columns, counters, out,
+              stream, data_bytes):
     _check_u8_cuda(data, "data")
     if stride:
         if n_frames is None:
@@ -163,8 +179,8 @@ def rx_process(data, *, n_frames=None, stride=0, frame_len=None, first_offset=0,
               lengths.data_ptr() if lengths is not None else 0)
     cols = out.c_struct()
     ctx = context(data.device.index)
-    check(lib.pnetgpu_rx_process(ctx.handle, ctypes.byref(b), ctypes.byref(cols),
-                                 _stream_handle(stream, data.device)), "pnetgpu_rx_process")
+    check(getattr(lib, fn_name)(ctx.handle, ctypes.byref(b), ctypes.byref(cols),
+                                _stream_handle(stream, data.device)), fn_name)
     return out
 
 

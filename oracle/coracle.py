@@ -49,6 +49,10 @@ def lib():
                                       ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
                                       ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                       ctypes.c_int]
+        L.oracle_tx_fill.restype = None
+        L.oracle_tx_fill.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
+                                     ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
+                                     ctypes.c_void_p]
         L.oracle_checksum_slices.restype = None
         L.oracle_checksum_slices.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
                                              ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
@@ -110,3 +114,17 @@ def checksum_slices(buf, offsets, lengths, skipwords):
     lib().oracle_checksum_slices(buf.ctypes.data, len(offsets), offsets.ctypes.data,
                                  lengths.ctypes.data, skipwords.ctypes.data, out.ctypes.data)
     return out
+
+
+def tx_fill(buf, n, *, stride=0, frame_len=0, first=0, offsets=None, lengths=None):
+    """Patch a COPY of buf the way the sender side does; returns (patched, records)."""
+    out_buf = np.array(buf, dtype=np.uint8, copy=True)
+    recs = np.zeros(n, dtype=REC_DTYPE)
+    offp = lenp = None
+    if stride == 0:
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        lengths = np.ascontiguousarray(lengths, dtype=np.uint32)
+        offp, lenp = offsets.ctypes.data, lengths.ctypes.data
+    lib().oracle_tx_fill(out_buf.ctypes.data, out_buf.size, n, first, stride, frame_len, offp, lenp,
+                         recs.ctypes.data)
+    return out_buf, recs

@@ -275,3 +275,33 @@ void oracle_checksum_slices(const uint8_t* buf, uint64_t n, const uint64_t* offs
 }
 
 size_t oracle_rec_size(void) { return sizeof(oracle_rec); }
+
+/* Sender side: the set_checksum(checksum(..)) calls of the reference's packet
+ * builders (benches/rs_sender.rs:38-39,70-71): every checksum the receive
+ * dispatch computes is written big-endian into its field, in place. The record
+ * describes the frame as it was before patching. */
+void oracle_tx_fill(uint8_t* buf, uint64_t buf_len, uint64_t n, uint64_t first, uint32_t stride,
+                    uint32_t frame_len, const uint64_t* offsets, const uint32_t* lengths, oracle_rec* out) {
+    for (uint64_t i = 0; i < n; ++i) {
+        uint64_t off = stride ? first + i * (uint64_t)stride : offsets[i];
+        uint64_t len = stride ? frame_len : lengths[i];
+        oracle_rec* r = &out[i];
+        if (off > buf_len || len > buf_len - off) {
+            memset(r, 0, sizeof(*r));
+            r->status = ORACLE_ST_DESC_INVALID;
+            continue;
+        }
+        uint8_t* f = buf + off;
+        oracle_rx_frame(f, (size_t)len, r);
+        if ((r->status & (ORACLE_ST_L3_IPV4 | ORACLE_ST_L3_IPV6 | ORACLE_ST_L3_MALFORMED)) == ORACLE_ST_L3_IPV4) {
+            f[24] = (uint8_t)(r->ip_csum >> 8);          /* Ipv4 checksum field, bytes 10-11 of the header */
+            f[25] = (uint8_t)r->ip_csum;
+        }
+        if (r->status & ORACLE_ST_L4_CSUM_DONE) {
+            unsigned kind = r->status & (7u << ORACLE_ST_L4_SHIFT);
+            unsigned at = kind == ORACLE_ST_L4_UDP ? 6u : kind == ORACLE_ST_L4_TCP ? 16u : 2u;
+            f[r->l4_offset + at] = (uint8_t)(r->l4_csum >> 8);
+            f[r->l4_offset + at + 1] = (uint8_t)r->l4_csum;
+        }
+    }
+}

@@ -104,6 +104,11 @@ void oracle_rx_batch(const uint8_t* buf, uint64_t buf_len, uint64_t n,
 
 size_t oracle_rec_size(void);
 
+/* Sender side (benches/rs_sender.rs:38-39,70-71): write every computed checksum
+ * into its stored field in place; records describe the frames before patching. */
+void oracle_tx_fill(uint8_t* buf, uint64_t buf_len, uint64_t n, uint64_t first, uint32_t stride,
+                    uint32_t frame_len, const uint64_t* offsets, const uint32_t* lengths, oracle_rec* out);
+
 /* Batched util::checksum over (offset, length, skipword) slices. */
 void oracle_checksum_slices(const uint8_t* buf, uint64_t n, const uint64_t* offsets,
                             const uint32_t* lengths, const uint32_t* skipwords,
