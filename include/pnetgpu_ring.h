@@ -1,0 +1,73 @@
+/*
+ * pnetgpu_ring.h — host-side batch producer for the receive engine.
+ *
+ * The reference hands the application one frame per DataLinkReceiver::next()
+ * call (pnet_datalink/src/lib.rs:227-230; Linux AF_PACKET linux.rs:362-403,
+ * pcap file replay pcap.rs:92,168-179), and the &[u8] is invalidated by the next
+ * call. A pnetgpu_ring is the consumer that turns that stream into GPU batches:
+ * pnetgpu_ring_push() copies each frame into a pinned host batch (descriptor
+ * mode: offsets + lengths), pnetgpu_ring_submit() ships a full batch
+ * asynchronously (hipMemcpyAsync H2D -> pnetgpu_rx_process -> D2H of every
+ * result column) on the slot's own stream, and pnetgpu_ring_wait() hands back the
+ * oldest finished batch's records in pinned host memory. Three slots rotate
+ * (one filling, one in flight, one held by the application), so copies, kernel
+ * and host work overlap.
+ *
+ * Validity: a waited batch (its frames and records) stays valid until the next
+ * pnetgpu_ring_wait() on the same ring. Single-threaded use per ring.
+ */
+#ifndef PNETGPU_RING_H
+#define PNETGPU_RING_H
+
+#include <stdint.h>
+
+#include "pnetgpu.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PNETGPU_EFULL   (-5)   /* push: frame does not fit the filling batch -> submit first   */
+#define PNETGPU_EBUSY   (-6)   /* push/submit: every slot is in flight or held -> wait first     */
+#define PNETGPU_EEMPTY  (-7)   /* wait: nothing in flight; pcap_next: end of file               */
+#define PNETGPU_EFORMAT (-8)   /* pcap: not a classic pcap file with Ethernet link type         */
+
+typedef struct pnetgpu_ring pnetgpu_ring;
+
+/* Host view of one finished batch. Column pointers follow pnetgpu_rx_columns
+ * (every column present, pinned host memory, n_frames elements each). */
+typedef struct pnetgpu_ring_batch {
+    uint64_t            id;         /* submission sequence number, from 0            */
+    uint64_t            n_frames;
+    const uint8_t*      frames;     /* the batch's frame bytes (pinned host)          */
+    const uint64_t*     offsets;    /* frame i = frames[offsets[i], +lengths[i])      */
+    const uint32_t*     lengths;
+    pnetgpu_rx_columns  cols;       /* host pointers; counters has PNETGPU_NCOUNTERS  */
+} pnetgpu_ring_batch;
+
+int  pnetgpu_ring_create(pnetgpu_ctx* ctx, uint64_t batch_bytes, uint32_t batch_frames, pnetgpu_ring** out);
+void pnetgpu_ring_destroy(pnetgpu_ring* ring);
+
+/* Copy one frame into the filling batch: 0, PNETGPU_EFULL or PNETGPU_EBUSY. */
+int pnetgpu_ring_push(pnetgpu_ring* ring, const uint8_t* frame, uint32_t len);
+/* Copy n frames (frame i = buf[offsets[i], +lengths[i]) on the host) until the
+ * batch is full; *pushed = how many were taken (may be < n: then submit). */
+int pnetgpu_ring_push_many(pnetgpu_ring* ring, const uint8_t* buf, const uint64_t* offsets,
+                           const uint32_t* lengths, uint64_t n, uint64_t* pushed);
+/* Ship the filling batch (no-op returning 0 with *id = UINT64_MAX if empty). */
+int pnetgpu_ring_submit(pnetgpu_ring* ring, uint64_t* id);
+/* Block for the oldest submitted batch: 0 (fills *out) or PNETGPU_EEMPTY. */
+int pnetgpu_ring_wait(pnetgpu_ring* ring, pnetgpu_ring_batch* out);
+
+/* Classic pcap reader (the pcap.rs:92 from_file receiver): LINKTYPE_ETHERNET,
+ * microsecond or nanosecond magic, either byte order. next() returns the
+ * captured bytes of each record (incl_len), valid until the following call. */
+typedef struct pnetgpu_pcap pnetgpu_pcap;
+int  pnetgpu_pcap_open(const char* path, pnetgpu_pcap** out);
+int  pnetgpu_pcap_next(pnetgpu_pcap* p, const uint8_t** frame, uint32_t* len);
+void pnetgpu_pcap_close(pnetgpu_pcap* p);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

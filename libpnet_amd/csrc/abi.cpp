@@ -19,6 +19,10 @@ struct pnetgpu_ctx {
     int cus;
 };
 
+namespace pnetgpu {
+int ctx_device(const pnetgpu_ctx* ctx) { return ctx->device; }
+}  // namespace pnetgpu
+
 namespace {
 
 constexpr int kBlock = 256;

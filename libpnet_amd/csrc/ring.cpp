@@ -1,0 +1,312 @@
+// ring.cpp — host batch producer (include/pnetgpu_ring.h): pinned host batches
+// filled frame by frame, shipped and verified asynchronously on the GPU, plus a
+// dependency-free classic pcap reader (the pnet_datalink pcap.rs:92 receiver).
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <deque>
+#include <new>
+#include <vector>
+
+#include "pnetgpu.h"
+#include "pnetgpu_ring.h"
+#include "rx_internal.h"
+
+namespace {
+
+constexpr int kSlots = 3;          // filling, in flight, held by the application
+constexpr int kNumCols = 14;
+// element bytes of each pnetgpu_rx_columns column, in struct order
+constexpr uint32_t kColBytes[kNumCols] = {2, 2, 2, 2, 1, 1, 2, 2, 2, 2, 4, 4, 16, 16};
+
+enum SlotState { kFree = 0, kFilling, kInFlight, kHeld };
+
+struct Slot {
+    uint8_t* h_frames = nullptr;
+    uint64_t* h_off = nullptr;
+    uint32_t* h_len = nullptr;
+    uint8_t* d_frames = nullptr;
+    uint64_t* d_off = nullptr;
+    uint32_t* d_len = nullptr;
+    void* d_cols[kNumCols] = {};
+    void* h_cols[kNumCols] = {};
+    uint64_t* d_ctr = nullptr;
+    uint64_t* h_ctr = nullptr;
+    hipStream_t stream = nullptr;
+    hipEvent_t done = nullptr;
+    uint32_t n = 0;
+    uint64_t bytes = 0;
+    uint64_t id = 0;
+    SlotState state = kFree;
+};
+
+void** col_slot(pnetgpu_rx_columns& c, int k) {
+    void** p[kNumCols] = {(void**)&c.status,    (void**)&c.ip_csum,   (void**)&c.l4_csum,   (void**)&c.ethertype,
+                          (void**)&c.ip_proto,  (void**)&c.ttl,       (void**)&c.l4_offset, (void**)&c.l4_length,
+                          (void**)&c.src_port,  (void**)&c.dst_port,  (void**)&c.src_ipv4,  (void**)&c.dst_ipv4,
+                          (void**)&c.src_ipv6,  (void**)&c.dst_ipv6};
+    return p[k];
+}
+
+}  // namespace
+
+struct pnetgpu_ring {
+    pnetgpu_ctx* ctx = nullptr;
+    int device = 0;
+    uint64_t cap_bytes = 0;
+    uint32_t cap_frames = 0;
+    Slot slots[kSlots];
+    int filling = -1;
+    int held = -1;
+    std::deque<int> inflight;
+    uint64_t next_id = 0;
+};
+
+struct pnetgpu_pcap {
+    FILE* f = nullptr;
+    bool swap = false;
+    std::vector<uint8_t> buf;
+};
+
+static void free_slot(Slot& s) {
+    if (s.h_frames) (void)hipHostFree(s.h_frames);
+    if (s.h_off) (void)hipHostFree(s.h_off);
+    if (s.h_len) (void)hipHostFree(s.h_len);
+    if (s.h_ctr) (void)hipHostFree(s.h_ctr);
+    if (s.d_frames) (void)hipFree(s.d_frames);
+    if (s.d_off) (void)hipFree(s.d_off);
+    if (s.d_len) (void)hipFree(s.d_len);
+    if (s.d_ctr) (void)hipFree(s.d_ctr);
+    for (int k = 0; k < kNumCols; ++k) {
+        if (s.d_cols[k]) (void)hipFree(s.d_cols[k]);
+        if (s.h_cols[k]) (void)hipHostFree(s.h_cols[k]);
+    }
+    if (s.done) (void)hipEventDestroy(s.done);
+    if (s.stream) (void)hipStreamDestroy(s.stream);
+    s = Slot{};
+}
+
+static int take_free_slot(pnetgpu_ring* r) {
+    for (int i = 0; i < kSlots; ++i) {
+        if (r->slots[i].state == kFree) {
+            r->slots[i].state = kFilling;
+            r->slots[i].n = 0;
+            r->slots[i].bytes = 0;
+            return i;
+        }
+    }
+    return -1;
+}
+
+extern "C" {
+
+int pnetgpu_ring_create(pnetgpu_ctx* ctx, uint64_t batch_bytes, uint32_t batch_frames, pnetgpu_ring** out) {
+    if (!ctx || !out || batch_bytes == 0 || batch_frames == 0) return PNETGPU_EINVAL;
+    *out = nullptr;
+    auto* r = new (std::nothrow) pnetgpu_ring;
+    if (!r) return PNETGPU_ENOMEM;
+    r->ctx = ctx;
+    r->device = pnetgpu::ctx_device(ctx);
+    r->cap_bytes = batch_bytes;
+    r->cap_frames = batch_frames;
+    if (hipSetDevice(r->device) != hipSuccess) {
+        delete r;
+        return PNETGPU_EHIP;
+    }
+    bool ok = true;
+    for (int i = 0; i < kSlots && ok; ++i) {
+        Slot& s = r->slots[i];
+        const size_t fb = batch_bytes + 32;    // granule tail
+        ok = hipHostMalloc((void**)&s.h_frames, fb, hipHostMallocDefault) == hipSuccess &&
+             hipHostMalloc((void**)&s.h_off, 8ull * batch_frames, hipHostMallocDefault) == hipSuccess &&
+             hipHostMalloc((void**)&s.h_len, 4ull * batch_frames, hipHostMallocDefault) == hipSuccess &&
+             hipHostMalloc((void**)&s.h_ctr, 8ull * PNETGPU_NCOUNTERS, hipHostMallocDefault) == hipSuccess &&
+             hipMalloc((void**)&s.d_frames, fb) == hipSuccess &&
+             hipMalloc((void**)&s.d_off, 8ull * batch_frames) == hipSuccess &&
+             hipMalloc((void**)&s.d_len, 4ull * batch_frames) == hipSuccess &&
+             hipMalloc((void**)&s.d_ctr, 8ull * PNETGPU_NCOUNTERS) == hipSuccess &&
+             hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking) == hipSuccess &&
+             hipEventCreateWithFlags(&s.done, hipEventDisableTiming) == hipSuccess;
+        for (int k = 0; k < kNumCols && ok; ++k) {
+            const size_t cb = (size_t)kColBytes[k] * batch_frames;
+            ok = hipMalloc(&s.d_cols[k], cb) == hipSuccess &&
+                 hipHostMalloc(&s.h_cols[k], cb, hipHostMallocDefault) == hipSuccess;
+        }
+        if (ok) std::memset(s.h_frames + batch_bytes, 0, 32);
+    }
+    if (!ok) {
+        for (auto& s : r->slots) free_slot(s);
+        delete r;
+        return PNETGPU_ENOMEM;
+    }
+    r->filling = take_free_slot(r);
+    *out = r;
+    return PNETGPU_OK;
+}
+
+void pnetgpu_ring_destroy(pnetgpu_ring* r) {
+    if (!r) return;
+    (void)hipSetDevice(r->device);
+    for (auto& s : r->slots) {
+        if (s.stream) (void)hipStreamSynchronize(s.stream);
+        free_slot(s);
+    }
+    delete r;
+}
+
+int pnetgpu_ring_push(pnetgpu_ring* r, const uint8_t* frame, uint32_t len) {
+    if (!r || (!frame && len)) return PNETGPU_EINVAL;
+    if (r->filling < 0 && (r->filling = take_free_slot(r)) < 0) return PNETGPU_EBUSY;
+    Slot& s = r->slots[r->filling];
+    if (s.n >= r->cap_frames || len > r->cap_bytes - s.bytes) return PNETGPU_EFULL;
+    std::memcpy(s.h_frames + s.bytes, frame, len);
+    s.h_off[s.n] = s.bytes;
+    s.h_len[s.n] = len;
+    s.bytes += len;
+    s.n += 1;
+    return PNETGPU_OK;
+}
+
+int pnetgpu_ring_push_many(pnetgpu_ring* r, const uint8_t* buf, const uint64_t* offsets, const uint32_t* lengths,
+                           uint64_t n, uint64_t* pushed) {
+    if (!r || !pushed || (n && (!buf || !offsets || !lengths))) return PNETGPU_EINVAL;
+    *pushed = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        const int rc = pnetgpu_ring_push(r, buf + offsets[i], lengths[i]);
+        if (rc == PNETGPU_EFULL || rc == PNETGPU_EBUSY) return *pushed ? PNETGPU_OK : rc;
+        if (rc) return rc;
+        *pushed += 1;
+    }
+    return PNETGPU_OK;
+}
+
+int pnetgpu_ring_submit(pnetgpu_ring* r, uint64_t* id) {
+    if (!r) return PNETGPU_EINVAL;
+    if (id) *id = UINT64_MAX;
+    if (r->filling < 0) return PNETGPU_OK;
+    Slot& s = r->slots[r->filling];
+    if (s.n == 0) return PNETGPU_OK;
+    if (hipSetDevice(r->device) != hipSuccess) return PNETGPU_EHIP;
+    const hipStream_t st = s.stream;
+    // granule rule: the tail past the last frame is readable (zeroed once at create)
+    if (hipMemcpyAsync(s.d_frames, s.h_frames, s.bytes, hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipMemcpyAsync(s.d_off, s.h_off, 8ull * s.n, hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipMemcpyAsync(s.d_len, s.h_len, 4ull * s.n, hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipMemsetAsync(s.d_ctr, 0, 8ull * PNETGPU_NCOUNTERS, st) != hipSuccess)
+        return PNETGPU_EHIP;
+    pnetgpu_batch b{};
+    b.data = s.d_frames;
+    b.data_bytes = s.bytes;
+    b.n_frames = s.n;
+    b.offsets = s.d_off;
+    b.lengths = s.d_len;
+    pnetgpu_rx_columns c{};
+    for (int k = 0; k < kNumCols; ++k) *col_slot(c, k) = s.d_cols[k];
+    c.counters = s.d_ctr;
+    int rc = pnetgpu_rx_process(r->ctx, &b, &c, st);
+    if (rc) return rc;
+    for (int k = 0; k < kNumCols; ++k)
+        if (hipMemcpyAsync(s.h_cols[k], s.d_cols[k], (size_t)kColBytes[k] * s.n, hipMemcpyDeviceToHost, st) !=
+            hipSuccess)
+            return PNETGPU_EHIP;
+    if (hipMemcpyAsync(s.h_ctr, s.d_ctr, 8ull * PNETGPU_NCOUNTERS, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipEventRecord(s.done, st) != hipSuccess)
+        return PNETGPU_EHIP;
+    s.state = kInFlight;
+    s.id = r->next_id++;
+    if (id) *id = s.id;
+    r->inflight.push_back(r->filling);
+    r->filling = take_free_slot(r);
+    return PNETGPU_OK;
+}
+
+int pnetgpu_ring_wait(pnetgpu_ring* r, pnetgpu_ring_batch* out) {
+    if (!r || !out) return PNETGPU_EINVAL;
+    if (r->held >= 0) {                          // the previous batch is released now
+        r->slots[r->held].state = kFree;
+        r->held = -1;
+        if (r->filling < 0) r->filling = take_free_slot(r);
+    }
+    if (r->inflight.empty()) return PNETGPU_EEMPTY;
+    const int i = r->inflight.front();
+    r->inflight.pop_front();
+    Slot& s = r->slots[i];
+    if (hipEventSynchronize(s.done) != hipSuccess) return PNETGPU_EHIP;
+    s.state = kHeld;
+    r->held = i;
+    out->id = s.id;
+    out->n_frames = s.n;
+    out->frames = s.h_frames;
+    out->offsets = s.h_off;
+    out->lengths = s.h_len;
+    std::memset(&out->cols, 0, sizeof(out->cols));
+    for (int k = 0; k < kNumCols; ++k) *col_slot(out->cols, k) = s.h_cols[k];
+    out->cols.counters = s.h_ctr;
+    return PNETGPU_OK;
+}
+
+// ---- classic pcap reader -----------------------------------------------------
+
+static uint32_t rd32(const uint8_t* p, bool swap) {
+    uint32_t v;
+    std::memcpy(&v, p, 4);
+    return swap ? __builtin_bswap32(v) : v;
+}
+
+int pnetgpu_pcap_open(const char* path, pnetgpu_pcap** out) {
+    if (!path || !out) return PNETGPU_EINVAL;
+    *out = nullptr;
+    FILE* f = std::fopen(path, "rb");
+    if (!f) return PNETGPU_EINVAL;
+    uint8_t gh[24];
+    if (std::fread(gh, 1, 24, f) != 24) {
+        std::fclose(f);
+        return PNETGPU_EFORMAT;
+    }
+    uint32_t magic;
+    std::memcpy(&magic, gh, 4);
+    bool swap;
+    if (magic == 0xa1b2c3d4u || magic == 0xa1b23c4du) swap = false;
+    else if (magic == 0xd4c3b2a1u || magic == 0x4d3cb2a1u) swap = true;
+    else {
+        std::fclose(f);
+        return PNETGPU_EFORMAT;
+    }
+    if (rd32(gh + 20, swap) != 1u) {             // LINKTYPE_ETHERNET
+        std::fclose(f);
+        return PNETGPU_EFORMAT;
+    }
+    auto* p = new (std::nothrow) pnetgpu_pcap;
+    if (!p) {
+        std::fclose(f);
+        return PNETGPU_ENOMEM;
+    }
+    p->f = f;
+    p->swap = swap;
+    *out = p;
+    return PNETGPU_OK;
+}
+
+int pnetgpu_pcap_next(pnetgpu_pcap* p, const uint8_t** frame, uint32_t* len) {
+    if (!p || !frame || !len) return PNETGPU_EINVAL;
+    uint8_t rh[16];
+    const size_t got = std::fread(rh, 1, 16, p->f);
+    if (got == 0) return PNETGPU_EEMPTY;
+    if (got != 16) return PNETGPU_EFORMAT;
+    const uint32_t incl = rd32(rh + 8, p->swap);
+    if (incl > (1u << 26)) return PNETGPU_EFORMAT;
+    p->buf.resize(incl ? incl : 1);
+    if (incl && std::fread(p->buf.data(), 1, incl, p->f) != incl) return PNETGPU_EFORMAT;
+    *frame = p->buf.data();
+    *len = incl;
+    return PNETGPU_OK;
+}
+
+void pnetgpu_pcap_close(pnetgpu_pcap* p) {
+    if (!p) return;
+    if (p->f) std::fclose(p->f);
+    delete p;
+}
+
+}  // extern "C"

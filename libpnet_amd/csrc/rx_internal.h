@@ -41,6 +41,9 @@ struct SliceArgs {
 constexpr int kKindSmall = 1;
 constexpr int kKindGeneric = 0;
 
+// device index a context is bound to (abi.cpp)
+int ctx_device(const pnetgpu_ctx* ctx);
+
 int rx_blocks_per_cu(int kind, int g, int* numregs, int* lds);
 int launch_rx(const RxArgs& args, int kind, int g, int blocks, bool tx, hipStream_t stream);
 int launch_slices(const SliceArgs& args, int pseudo, int blocks, hipStream_t stream);

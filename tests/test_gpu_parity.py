@@ -22,7 +22,10 @@ DEV = "cuda:0"
 
 
 def to_dev(a, dtype=None):
-    t = torch.from_numpy(np.ascontiguousarray(a))
+    a = np.ascontiguousarray(a)
+    if not a.flags.writeable:
+        a = a.copy()
+    t = torch.from_numpy(a)
     if dtype is not None:
         t = t.view(dtype)
     return t.to(DEV)

@@ -1,0 +1,31 @@
+"""CPU tests of the native pcap reader (pnetgpu_pcap_*): every byte order and
+timestamp resolution, empty records, and rejection of non-Ethernet captures."""
+import struct
+
+import numpy as np
+import pytest
+
+import libpnet_amd as lp
+from libpnet_amd._lib import PnetGpuError
+from tests import framegen
+from tests.pcaputil import write_pcap
+
+
+@pytest.mark.parametrize("nanos", [False, True])
+@pytest.mark.parametrize("big", [False, True])
+def test_pcap_roundtrip(tmp_path, nanos, big):
+    frames = framegen.random_frames(np.random.default_rng(4), 300) + [b""]
+    p = tmp_path / "t.pcap"
+    write_pcap(p, frames, nanos=nanos, big_endian=big)
+    assert list(lp.pcap_frames(p)) == frames
+
+
+def test_pcap_rejects_non_ethernet(tmp_path):
+    p = tmp_path / "x.pcap"
+    p.write_bytes(struct.pack("<IHHiIII", 0xA1B2C3D4, 2, 4, 0, 0, 65535, 101))
+    with pytest.raises(PnetGpuError):
+        list(lp.pcap_frames(p))
+    q = tmp_path / "y.pcap"
+    q.write_bytes(b"not a pcap at all" * 4)
+    with pytest.raises(PnetGpuError):
+        list(lp.pcap_frames(q))
