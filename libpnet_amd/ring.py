@@ -47,16 +47,18 @@ _setup()
 
 
 class Batch:
-    """A finished ring batch, copied out of the ring's pinned memory."""
+    """A finished ring batch. With copy=False the arrays are views of the ring's
+    pinned memory, valid until the ring's next wait (the C-ABI contract)."""
 
-    def __init__(self, rb):
+    def __init__(self, rb, copy=True):
         n = int(rb.n_frames)
         self.id, self.n = int(rb.id), n
-        self.offsets = np.ctypeslib.as_array(ctypes.cast(rb.offsets, ctypes.POINTER(ctypes.c_uint64)), (n,)).copy()
-        self.lengths = np.ctypeslib.as_array(ctypes.cast(rb.lengths, ctypes.POINTER(ctypes.c_uint32)), (n,)).copy()
+        cp = (lambda a: a.copy()) if copy else (lambda a: a)
+        self.offsets = cp(np.ctypeslib.as_array(ctypes.cast(rb.offsets, ctypes.POINTER(ctypes.c_uint64)), (n,)))
+        self.lengths = cp(np.ctypeslib.as_array(ctypes.cast(rb.lengths, ctypes.POINTER(ctypes.c_uint32)), (n,)))
         nbytes = int(self.offsets[-1] + self.lengths[-1]) if n else 0
-        self.frames = np.ctypeslib.as_array(ctypes.cast(rb.frames, ctypes.POINTER(ctypes.c_uint8)),
-                                            (max(nbytes, 1),))[:nbytes].copy()
+        self.frames = cp(np.ctypeslib.as_array(ctypes.cast(rb.frames, ctypes.POINTER(ctypes.c_uint8)),
+                                               (max(nbytes, 1),))[:nbytes])
         self.records = {}
         for c, (_, npdt, shape) in COLUMNS.items():
             ptr = getattr(rb.cols, c)
@@ -64,7 +66,7 @@ class Batch:
             ct = {1: ctypes.c_uint8, 2: ctypes.c_uint16, 4: ctypes.c_uint32}[itemsize]
             a = np.ctypeslib.as_array(ctypes.cast(ptr, ctypes.POINTER(ct)), (n,) + shape) if n else np.zeros(
                 (0,) + shape, npdt)
-            self.records[c] = a.copy().view(npdt)
+            self.records[c] = cp(a).view(npdt)
         ctr = np.ctypeslib.as_array(ctypes.cast(rb.cols.counters, ctypes.POINTER(ctypes.c_uint64)),
                                     (len(COUNTER_NAMES),))
         self.counters = dict(zip(COUNTER_NAMES, (int(x) for x in ctr)))
@@ -73,8 +75,9 @@ class Batch:
 class Ring:
     """Pinned host batches -> asynchronous GPU verification (three rotating slots)."""
 
-    def __init__(self, batch_bytes=64 << 20, batch_frames=1 << 18, device=0):
+    def __init__(self, batch_bytes=64 << 20, batch_frames=1 << 18, device=0, copy=True):
         self.ctx = context(device)
+        self.copy = copy
         h = ctypes.c_void_p()
         check(lib.pnetgpu_ring_create(self.ctx.handle, batch_bytes, batch_frames, ctypes.byref(h)),
               "pnetgpu_ring_create")
@@ -99,7 +102,7 @@ class Ring:
             return None
         check(rc, "pnetgpu_ring_wait")
         self.pending -= 1
-        return Batch(rb)
+        return Batch(rb, self.copy)
 
     def submit(self):
         bid = ctypes.c_uint64()

@@ -54,6 +54,21 @@ __global__ __launch_bounds__(256) void read_cols_kernel(const uint4* __restrict_
     }
 }
 
+// same reads, one packed 32-B record per frame (two dwordx4 stores per lane)
+__global__ __launch_bounds__(256) void read_rec_kernel(const uint4* __restrict__ in, size_t nframes, uint4* rec) {
+    const int lane = threadIdx.x & 63;
+    const size_t wave = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const size_t nwaves = ((size_t)gridDim.x * blockDim.x) >> 6;
+    for (size_t run = wave; run * 64 < nframes; run += nwaves) {
+        const uint4* p = in + run * 256;
+        uint4 v0 = p[lane], v1 = p[64 + lane], v2 = p[128 + lane], v3 = p[192 + lane];
+        uint32_t x = v0.x ^ v1.y ^ v2.z ^ v3.w;
+        const size_t f = run * 64 + lane;
+        rec[2 * f] = make_uint4(x, x + 1, x + 2, x + 3);
+        rec[2 * f + 1] = make_uint4(x + 4, x + 5, x + 6, x + 7);
+    }
+}
+
 __global__ __launch_bounds__(256) void copy_kernel(const uint4* __restrict__ in, uint4* __restrict__ out, size_t n16) {
     const size_t stride = (size_t)gridDim.x * blockDim.x;
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += stride) out[i] = in[i];
@@ -91,6 +106,9 @@ int main() {
         ms = time_it([&] { read_cols_kernel<<<grid, 256>>>(in, nframes, c16, c32, c8); }, 20);
         printf("read+26B cols  grid=%5d: %7.1f us  %6.0f GB/s (alg %zu B)\n", grid, ms * 1e3,
                (bytes + nframes * 26) / ms / 1e6, bytes + nframes * 26);
+        ms = time_it([&] { read_rec_kernel<<<grid, 256>>>(in, nframes, out); }, 20);
+        printf("read+32B rec   grid=%5d: %7.1f us  %6.0f GB/s (alg %zu B)\n", grid, ms * 1e3,
+               (bytes + nframes * 32) / ms / 1e6, bytes + nframes * 32);
         ms = time_it([&] { copy_kernel<<<grid, 256>>>(in, out, n16); }, 20);
         printf("copy           grid=%5d: %7.1f us  %6.0f GB/s (r+w)\n", grid, ms * 1e3, 2.0 * bytes / ms / 1e6);
     }
