@@ -60,7 +60,7 @@
 extern "C" {
 #endif
 
-#define PNETGPU_ABI_VERSION 1
+#define PNETGPU_ABI_VERSION 2
 
 /* ---- return codes ------------------------------------------------------- */
 #define PNETGPU_OK        0
@@ -87,7 +87,25 @@ extern "C" {
 #define PNET_ST_L4_CSUM_OK        0x0400u  /* computed L4 checksum == stored field       */
 #define PNET_ST_UNKNOWN_ETHERTYPE 0x0800u
 #define PNET_ST_UNKNOWN_PROTO     0x1000u
+#define PNET_ST_VLAN              0x2000u  /* PNETGPU_RX_VLAN: one or more VLAN tags were peeled */
+#define PNET_ST_FRAGMENT          0x4000u  /* PNETGPU_RX_IPV6_EXT: non-first IPv6 fragment, no L4 */
 #define PNET_ST_DESC_INVALID      0x8000u  /* descriptor outside [0, data_bytes): not read */
+
+/* ---- opt-in dispatch extensions (pnetgpu_batch.flags) --------------------
+ * The reference's receive chain (packetdump.rs) dispatches Ethernet -> IP
+ * directly. These flags follow the reference's other views first:
+ *   PNETGPU_RX_VLAN      up to two VlanPacket views (vlan.rs:62-72) for
+ *                        ethertypes 0x8100 / 0x88A8 / 0x9100 (ethernet.rs:102-112);
+ *                        a truncated tag (< 4 B) sets VLAN | L3_MALFORMED.
+ *   PNETGPU_RX_IPV6_EXT  up to four IPv6 extension headers (ipv6.rs:39-137):
+ *                        Hop-by-Hop 0 / Destination 60 / Routing 43 (length
+ *                        hdr_ext_len*8+8), Fragment 44 (8 B; a fragment with
+ *                        offset (value & ~3) != 0 sets FRAGMENT and stops); a
+ *                        truncated header sets L4_MALFORMED. ip_proto reports
+ *                        the protocol after the walk; the L4 pseudo-header uses
+ *                        the base header's addresses and the L4 slice length. */
+#define PNETGPU_RX_VLAN           0x1u
+#define PNETGPU_RX_IPV6_EXT       0x2u
 
 /* ---- batch-wide counters (rx columns .counters, uint64 each, accumulated) */
 #define PNETGPU_CTR_FRAMES        0  /* frames with a valid descriptor            */
@@ -116,6 +134,8 @@ typedef struct pnetgpu_batch {
     uint32_t        frame_len;    /* stride mode: length of every frame            */
     const uint64_t* offsets;      /* descriptor mode: device array [n_frames]      */
     const uint32_t* lengths;      /* descriptor mode: device array [n_frames]      */
+    uint32_t        flags;        /* PNETGPU_RX_* dispatch extensions (0 = reference chain) */
+    uint32_t        reserved;     /* must be 0                                     */
 } pnetgpu_batch;
 
 /*
@@ -127,7 +147,7 @@ typedef struct pnetgpu_rx_columns {
     uint16_t* status;     /* PNET_ST_* bits                                        */
     uint16_t* ip_csum;    /* ipv4::checksum(&ip) (IPv4 only)                       */
     uint16_t* l4_csum;    /* udp/tcp ipv4|ipv6_checksum, icmp::checksum, icmpv6::checksum */
-    uint16_t* ethertype;  /* EthernetPacket::get_ethertype                         */
+    uint16_t* ethertype;  /* EthernetPacket::get_ethertype (inner one past VLAN tags) */
     uint8_t*  ip_proto;   /* get_next_level_protocol (v4) / get_next_header (v6)   */
     uint8_t*  ttl;        /* get_ttl (v4) / get_hop_limit (v6)                     */
     uint16_t* l4_offset;  /* frame offset of ip.payload() (0 when it is empty)     */
@@ -138,6 +158,8 @@ typedef struct pnetgpu_rx_columns {
     uint32_t* dst_ipv4;
     uint8_t*  src_ipv6;   /* [n_frames][16] Ipv6 get_source octets (16-B aligned)   */
     uint8_t*  dst_ipv6;   /* [n_frames][16]                                        */
+    uint16_t* vlan_tci;   /* outer VlanPacket TCI (pcp|dei|vid) when PNET_ST_VLAN  */
+    uint8_t*  l3_offset;  /* frame offset of the IP header (14, or 18/22 past tags) */
     uint64_t* counters;   /* [PNETGPU_NCOUNTERS], atomically accumulated           */
 } pnetgpu_rx_columns;
 

@@ -45,7 +45,9 @@ typedef struct pnetgpu_ring_batch {
     pnetgpu_rx_columns  cols;       /* host pointers; counters has PNETGPU_NCOUNTERS  */
 } pnetgpu_ring_batch;
 
-int  pnetgpu_ring_create(pnetgpu_ctx* ctx, uint64_t batch_bytes, uint32_t batch_frames, pnetgpu_ring** out);
+/* flags: PNETGPU_RX_* dispatch extensions applied to every batch */
+int  pnetgpu_ring_create(pnetgpu_ctx* ctx, uint64_t batch_bytes, uint32_t batch_frames, uint32_t flags,
+                         pnetgpu_ring** out);
 void pnetgpu_ring_destroy(pnetgpu_ring* ring);
 
 /* Copy one frame into the filling batch: 0, PNETGPU_EFULL or PNETGPU_EBUSY. */

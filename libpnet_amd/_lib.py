@@ -51,11 +51,12 @@ DEFS = _header_defines()
 class Batch(ctypes.Structure):
     _fields_ = [("data", ctypes.c_void_p), ("data_bytes", ctypes.c_uint64), ("n_frames", ctypes.c_uint64),
                 ("first_offset", ctypes.c_uint64), ("stride", ctypes.c_uint32), ("frame_len", ctypes.c_uint32),
-                ("offsets", ctypes.c_void_p), ("lengths", ctypes.c_void_p)]
+                ("offsets", ctypes.c_void_p), ("lengths", ctypes.c_void_p), ("flags", ctypes.c_uint32),
+                ("reserved", ctypes.c_uint32)]
 
 
 COLUMN_NAMES = ("status", "ip_csum", "l4_csum", "ethertype", "ip_proto", "ttl", "l4_offset", "l4_length",
-                "src_port", "dst_port", "src_ipv4", "dst_ipv4", "src_ipv6", "dst_ipv6")
+                "src_port", "dst_port", "src_ipv4", "dst_ipv4", "src_ipv6", "dst_ipv6", "vlan_tci", "l3_offset")
 
 
 class RxColumns(ctypes.Structure):

@@ -98,6 +98,7 @@ static int rx_common(pnetgpu_ctx* ctx, const pnetgpu_batch* b, const pnetgpu_rx_
         (cols->dst_ipv6 && (reinterpret_cast<uintptr_t>(cols->dst_ipv6) & 15)))
         return PNETGPU_EINVAL;
     if (b->n_frames > (UINT64_MAX - kRunFrames) / 2) return PNETGPU_EINVAL;
+    if ((b->flags & ~(PNETGPU_RX_VLAN | PNETGPU_RX_IPV6_EXT)) || b->reserved) return PNETGPU_EINVAL;
     int rc = set_device(ctx);
     if (rc) return rc;
 
@@ -111,6 +112,7 @@ static int rx_common(pnetgpu_ctx* ctx, const pnetgpu_batch* b, const pnetgpu_rx_
     a.lengths = b->lengths;
     a.cols = *cols;
     a.nruns = (a.n + kRunFrames - 1) / kRunFrames;
+    a.flags = b->flags;
 
     // Kernel choice. Small: fixed stride, every frame 16-B aligned, at most 64 B,
     // inside the buffer (the 64-B configs). Generic otherwise; its tail group
@@ -121,7 +123,8 @@ static int rx_common(pnetgpu_ctx* ctx, const pnetgpu_batch* b, const pnetgpu_rx_
         const uint64_t last_end = a.delta + b->first_offset + (b->n_frames - 1) * (uint64_t)b->stride + b->frame_len;
         const bool fits = b->n_frames <= (UINT64_MAX - a.delta - b->first_offset - b->frame_len) / b->stride &&
                           last_end <= a.limit;
-        if (base_sh == 0 && b->stride % 16 == 0 && b->frame_len <= 64 && fits) kind = pnetgpu::kKindSmall;
+        if (base_sh == 0 && b->stride % 16 == 0 && b->frame_len <= 64 && fits && b->flags == 0)
+            kind = pnetgpu::kKindSmall;
         if (b->frame_len >= 4096) g = 64;
     }
     if (const char* e = std::getenv("PNETGPU_TAIL_GROUP")) {      // tuning override

@@ -16,9 +16,9 @@
 namespace {
 
 constexpr int kSlots = 3;          // filling, in flight, held by the application
-constexpr int kNumCols = 14;
+constexpr int kNumCols = 16;
 // element bytes of each pnetgpu_rx_columns column, in struct order
-constexpr uint32_t kColBytes[kNumCols] = {2, 2, 2, 2, 1, 1, 2, 2, 2, 2, 4, 4, 16, 16};
+constexpr uint32_t kColBytes[kNumCols] = {2, 2, 2, 2, 1, 1, 2, 2, 2, 2, 4, 4, 16, 16, 2, 1};
 
 enum SlotState { kFree = 0, kFilling, kInFlight, kHeld };
 
@@ -45,7 +45,7 @@ void** col_slot(pnetgpu_rx_columns& c, int k) {
     void** p[kNumCols] = {(void**)&c.status,    (void**)&c.ip_csum,   (void**)&c.l4_csum,   (void**)&c.ethertype,
                           (void**)&c.ip_proto,  (void**)&c.ttl,       (void**)&c.l4_offset, (void**)&c.l4_length,
                           (void**)&c.src_port,  (void**)&c.dst_port,  (void**)&c.src_ipv4,  (void**)&c.dst_ipv4,
-                          (void**)&c.src_ipv6,  (void**)&c.dst_ipv6};
+                          (void**)&c.src_ipv6,  (void**)&c.dst_ipv6,  (void**)&c.vlan_tci,  (void**)&c.l3_offset};
     return p[k];
 }
 
@@ -56,6 +56,7 @@ struct pnetgpu_ring {
     int device = 0;
     uint64_t cap_bytes = 0;
     uint32_t cap_frames = 0;
+    uint32_t flags = 0;
     Slot slots[kSlots];
     int filling = -1;
     int held = -1;
@@ -101,8 +102,10 @@ static int take_free_slot(pnetgpu_ring* r) {
 
 extern "C" {
 
-int pnetgpu_ring_create(pnetgpu_ctx* ctx, uint64_t batch_bytes, uint32_t batch_frames, pnetgpu_ring** out) {
+int pnetgpu_ring_create(pnetgpu_ctx* ctx, uint64_t batch_bytes, uint32_t batch_frames, uint32_t flags,
+                        pnetgpu_ring** out) {
     if (!ctx || !out || batch_bytes == 0 || batch_frames == 0) return PNETGPU_EINVAL;
+    if (flags & ~(PNETGPU_RX_VLAN | PNETGPU_RX_IPV6_EXT)) return PNETGPU_EINVAL;
     *out = nullptr;
     auto* r = new (std::nothrow) pnetgpu_ring;
     if (!r) return PNETGPU_ENOMEM;
@@ -110,6 +113,7 @@ int pnetgpu_ring_create(pnetgpu_ctx* ctx, uint64_t batch_bytes, uint32_t batch_f
     r->device = pnetgpu::ctx_device(ctx);
     r->cap_bytes = batch_bytes;
     r->cap_frames = batch_frames;
+    r->flags = flags;
     if (hipSetDevice(r->device) != hipSuccess) {
         delete r;
         return PNETGPU_EHIP;
@@ -201,6 +205,7 @@ int pnetgpu_ring_submit(pnetgpu_ring* r, uint64_t* id) {
     b.n_frames = s.n;
     b.offsets = s.d_off;
     b.lengths = s.d_len;
+    b.flags = r->flags;
     pnetgpu_rx_columns c{};
     for (int k = 0; k < kNumCols; ++k) *col_slot(c, k) = s.d_cols[k];
     c.counters = s.d_ctr;

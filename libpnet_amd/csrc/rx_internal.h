@@ -20,6 +20,7 @@ struct RxArgs {
     const uint64_t* offsets;
     const uint32_t* lengths;
     uint64_t nruns;          // ceil(n / 64): one wave per run of 64 frames
+    uint32_t flags;          // PNETGPU_RX_* (the small kernel requires 0)
     pnetgpu_rx_columns cols;
 };
 

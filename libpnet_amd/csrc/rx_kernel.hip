@@ -81,8 +81,6 @@ __device__ __forceinline__ void wave_sync() {
 
 // ---- LDS byte access ---------------------------------------------------------
 __device__ __forceinline__ uint32_t ld8(const uint8_t* w, int p) { return w[p]; }
-__device__ __forceinline__ uint32_t ld16be(const uint8_t* w, int p) { return (ld8(w, p) << 8) | ld8(w, p + 1); }
-__device__ __forceinline__ uint32_t ld32be(const uint8_t* w, int p) { return (ld16be(w, p) << 16) | ld16be(w, p + 2); }
 
 // 16 bytes of a run [p, p+16) of an LDS slot at any alignment, as 4 LE dwords.
 __device__ __forceinline__ uint4 lds_read16_unaligned(const uint8_t* slot, int p) {
@@ -98,73 +96,151 @@ __device__ __forceinline__ uint4 lds_read16_unaligned(const uint8_t* slot, int p
 }
 
 // ---- the reference's receive dispatch, restated for one lane ---------------
-// Fields of one frame plus the two summed ranges A=[r0,m) (IPv4 header, or the
-// IPv6 pseudo-header addresses) and B=[m,e) (the L4 slice), frame-relative.
+// Fields of one frame plus the two summed ranges, frame-relative:
+//   A = [a_lo, a_hi)  the IPv4 header, or the IPv6 pseudo-header address bytes
+//   B = [b_lo, b_hi)  the L4 slice
+// with a_lo <= a_hi <= b_lo <= b_hi (empty ranges collapse onto their neighbour).
 struct Parsed {
-    uint32_t st, et, proto, ttl, l4off, l4len, sp, dp, s4, d4, ipstored, l4stored, pseudo;
-    int r0, m, e;
+    uint32_t st, et, proto, ttl, l4off, l4len, sp, dp, s4, d4, ipstored, l4stored, pseudo, vlan_tci, l3;
+    int a_lo, a_hi, b_lo, b_hi;
     int l4csum_at;            // frame offset of the L4 checksum field (valid when l4do)
     bool is_v4, l4do, v6pseudo;
 };
 
-// Generic parse of a frame held in LDS at W (frame byte 0), `len` bytes.
-// packetdump.rs:155-217 + ipv4.rs:165-178,226-243 + ipv6.rs:21-37 + udp/tcp/icmp
-// layouts and minimum sizes (decorator.rs:593-600) + payload bounds (decorator.rs:713-769).
-__device__ __forceinline__ Parsed parse_lds(const uint8_t* W, uint32_t len) {
+// Frame bytes for the parse: the LDS window W holds bytes [0, wlim); anything
+// past it (long IPv6 extension chains, L4 headers behind them) is read from the
+// frame in HBM through G. The IPv4 header and VLAN tags always fit the window.
+struct FrameBytes {
+    const uint8_t* W;
+    const uint8_t* G;
+    int wlim;
+    __device__ __forceinline__ uint32_t near8(int p) const { return W[p]; }
+    __device__ __forceinline__ uint32_t near16(int p) const { return (near8(p) << 8) | near8(p + 1); }
+    __device__ __forceinline__ uint32_t near32(int p) const { return (near16(p) << 16) | near16(p + 2); }
+    __device__ __forceinline__ uint32_t far8(int p) const {
+        if (p < wlim) return W[p];
+        return G[p];
+    }
+    __device__ __forceinline__ uint32_t far16(int p) const { return (far8(p) << 8) | far8(p + 1); }
+};
+
+__device__ __forceinline__ bool is_vlan_tpid(uint32_t et) { return et == 0x8100u || et == 0x88A8u || et == 0x9100u; }
+
+// Generic parse of one frame of `len` bytes (FLAGS: PNET_RX_* extensions).
+// packetdump.rs:155-217 + ipv4.rs:165-178,226-243 + ipv6.rs:21-137 + vlan.rs:62-72
+// + udp/tcp/icmp layouts and minimum sizes (decorator.rs:593-600) + payload
+// bounds (decorator.rs:713-769). Mirrors oracle_rx_frame_ex.
+__device__ __forceinline__ Parsed parse_frame(const FrameBytes& F, uint32_t len, uint32_t flags) {
     Parsed P{};
     if (len < 14) {
         P.st = PNET_ST_ETH_MALFORMED;                  // EthernetPacket::new == None
         return P;
     }
-    P.et = ld16be(W, 12);
-    const uint32_t eplen = len - 14;                   // Ethernet payload: unbounded
-    bool l3ok = false, has_l4 = false, v6 = false;
-    uint32_t l4s = 0;
-    if (P.et == 0x0800u) {
+    uint32_t et = F.near16(12);
+    int l3 = 14;
+    if (flags & PNETGPU_RX_VLAN) {
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            if (!is_vlan_tpid(et)) break;
+            P.st |= PNET_ST_VLAN;
+            if (len < (uint32_t)l3 + 4u) {               // VlanPacket::new == None
+                P.et = et;
+                P.st |= PNET_ST_L3_MALFORMED;
+                return P;
+            }
+            if (k == 0) P.vlan_tci = F.near16(l3);
+            et = F.near16(l3 + 2);
+            l3 += 4;
+        }
+    }
+    P.et = et;
+    P.l3 = (uint32_t)l3;
+    const uint32_t eplen = len - (uint32_t)l3;            // Ethernet payload: unbounded
+    bool l3ok = false, v6 = false;
+    uint32_t l4s = 0, l4n = 0;                            // L4 slice [l4s, l4s + l4n)
+    bool has_l4 = false;
+    if (et == 0x0800u) {
         P.st |= PNET_ST_L3_IPV4;
         if (eplen < 20) {
             P.st |= PNET_ST_L3_MALFORMED;
         } else {
             l3ok = true;
             P.is_v4 = true;
-            const uint32_t ihl4 = (ld8(W, 14) & 15u) * 4u;
+            const uint32_t ihl4 = (F.near8(l3) & 15u) * 4u;
             const uint32_t hl = min(max(ihl4, 20u), eplen);   // ipv4.rs:169-175
-            const uint32_t tl = ld16be(W, 16);
-            P.ttl = ld8(W, 22);
-            P.proto = ld8(W, 23);
-            P.ipstored = ld16be(W, 24);
-            P.s4 = ld32be(W, 26);
-            P.d4 = ld32be(W, 30);
-            P.r0 = 14;
-            P.m = 14 + (int)hl;
+            const uint32_t tl = F.near16(l3 + 2);
+            P.ttl = F.near8(l3 + 8);
+            P.proto = F.near8(l3 + 9);
+            P.ipstored = F.near16(l3 + 10);
+            P.s4 = F.near32(l3 + 12);
+            P.d4 = F.near32(l3 + 16);
+            P.a_lo = l3;
+            P.a_hi = l3 + (int)hl;
             const uint32_t start = max(20u, ihl4);             // 20 + ipv4_options_length
             const uint32_t plen = tl > ihl4 ? tl - ihl4 : 0u;  // ipv4_payload_length
             if (eplen > start) {
                 has_l4 = true;
-                l4s = 14 + start;
-                P.l4len = min(start + plen, eplen) - start;
+                l4s = (uint32_t)l3 + start;
+                l4n = min(start + plen, eplen) - start;
             }
         }
-    } else if (P.et == 0x86DDu) {
+    } else if (et == 0x86DDu) {
         P.st |= PNET_ST_L3_IPV6;
         if (eplen < 40) {
             P.st |= PNET_ST_L3_MALFORMED;
         } else {
             l3ok = true;
             v6 = true;
-            P.proto = ld8(W, 20);
-            P.ttl = ld8(W, 21);
-            const uint32_t pl = ld16be(W, 18);
-            if (eplen > 40) {                                  // #[length = "payload_length"]
+            P.proto = F.near8(l3 + 6);
+            P.ttl = F.near8(l3 + 7);
+            const uint32_t pl = F.near16(l3 + 4);
+            uint32_t pln = 0;                                   // #[length = "payload_length"]
+            if (eplen > 40) pln = min(40u + pl, eplen) - 40u;
+            const int pbase = l3 + 40;
+            uint32_t pos = 0;
+            if (flags & PNETGPU_RX_IPV6_EXT) {                  // ipv6.rs:39-137
+                uint32_t nh = P.proto;
+                for (int k = 0; k < 4; ++k) {
+                    if (nh == 0 || nh == 60 || nh == 43) {
+                        const uint32_t minl = nh == 43 ? 4u : 2u;
+                        if (pln - pos < minl) { P.proto = nh; P.st |= PNET_ST_L4_MALFORMED; return P; }
+                        const uint32_t el = F.far8(pbase + (int)pos + 1) * 8u + 8u;
+                        if (el > pln - pos) { P.proto = nh; P.st |= PNET_ST_L4_MALFORMED; return P; }
+                        nh = F.far8(pbase + (int)pos);
+                        pos += el;
+                    } else if (nh == 44) {
+                        if (pln - pos < 8u) { P.proto = nh; P.st |= PNET_ST_L4_MALFORMED; return P; }
+                        const uint32_t fo = F.far16(pbase + (int)pos + 2);
+                        nh = F.far8(pbase + (int)pos);
+                        pos += 8;
+                        if (fo & 0xFFFCu) {                     // not the first fragment
+                            P.proto = nh;
+                            P.st |= PNET_ST_FRAGMENT;
+                            if (pln > pos) {
+                                P.l4off = (uint32_t)pbase + pos;
+                                P.l4len = pln - pos;
+                            }
+                            return P;
+                        }
+                    } else {
+                        break;
+                    }
+                }
+                P.proto = nh;
+            }
+            if (pln > pos) {
                 has_l4 = true;
-                l4s = 54;
-                P.l4len = min(40u + pl, eplen) - 40u;
+                l4s = (uint32_t)pbase + pos;
+                l4n = pln - pos;
             }
         }
     } else {
         P.st |= PNET_ST_UNKNOWN_ETHERTYPE;
     }
-    if (has_l4) P.l4off = l4s;
+    if (has_l4) {
+        P.l4off = l4s;
+        P.l4len = l4n;
+    }
     if (l3ok) {
         uint32_t kind = 0, minlen = 0;
         int soff = 0;
@@ -179,58 +255,65 @@ __device__ __forceinline__ Parsed parse_lds(const uint8_t* W, uint32_t len) {
             P.st |= PNET_ST_UNKNOWN_PROTO;
         } else {
             P.st |= kind;
-            if (P.l4len < minlen) {
+            if (l4n < minlen) {
                 P.st |= PNET_ST_L4_MALFORMED;
             } else {
                 const int p = (int)l4s;
-                P.sp = ld16be(W, p);
-                if (P.proto == 17 || P.proto == 6) P.dp = ld16be(W, p + 2);
-                else P.dp = P.l4len >= 8 ? ld16be(W, p + 4) : 0u;
-                P.l4stored = ld16be(W, p + soff);
+                P.sp = F.far16(p);
+                if (P.proto == 17 || P.proto == 6) P.dp = F.far16(p + 2);
+                else P.dp = l4n >= 8 ? F.far16(p + 4) : 0u;
+                P.l4stored = F.far16(p + soff);
                 P.l4csum_at = p + soff;
                 if (P.proto == 1) {                            // icmp::checksum: no pseudo-header
                     P.l4do = true;
-                    if (v6) { P.r0 = 54; P.m = 54; }
                 } else if (v6) {                               // util::ipv6_checksum
                     P.l4do = true;
                     P.v6pseudo = true;
-                    P.r0 = 22; P.m = 54;                       // pseudo-header address bytes
-                    P.pseudo = P.proto + P.l4len;
+                    P.a_lo = l3 + 8;                           // pseudo-header address bytes
+                    P.a_hi = l3 + 40;
+                    P.pseudo = P.proto + l4n;
                 } else if (P.proto != 58) {                    // util::ipv4_checksum
                     P.l4do = true;
                     P.pseudo = (P.s4 >> 16) + (P.s4 & 0xFFFFu) + (P.d4 >> 16) + (P.d4 & 0xFFFFu) +
-                               P.proto + P.l4len;
+                               P.proto + l4n;
                 }
-                if (P.l4do) P.e = p + (int)P.l4len;            // B = [l4s, l4s+len), l4s == m
+                if (P.l4do) {
+                    P.b_lo = p;
+                    P.b_hi = p + (int)l4n;
+                }
             }
         }
     }
-    if (!P.is_v4 && !P.l4do) { P.r0 = 0; P.m = 0; P.e = 0; }
-    if (P.is_v4 && !P.l4do) P.e = P.m;
+    // canonical empty ranges: a_lo <= a_hi <= b_lo <= b_hi
+    if (!P.l4do) { P.b_lo = P.b_hi = P.a_hi; }
+    if (P.l4do && !P.is_v4 && !P.v6pseudo) { P.a_lo = P.a_hi = P.b_lo; }   // ICMP over IPv6
     return P;
 }
 
-// Window sums of one lane's LDS slot: tA over [rs,ms), tB over [ms,ew) in slot
-// coordinates, rs <= ms <= ew (all zero: nothing to sum). With P(x) = weighted
-// sum of the slot bytes in [4*(rs>>2), x): tA = P(ms) - P(rs), tB = P(ew) - P(ms).
-// One runtime loop over whole dwords (v_sad_u16 each) plus three masked partial
-// dwords; the slot has a readable pad dword so ew>>2 may equal the dword count.
-__device__ __forceinline__ void window_sums(const uint8_t* slot, int rs, int ms, int ew, uint32_t& tA,
+// Window sums of one lane's LDS slot: tA over [p0,p1), tB over [p2,p3), slot
+// coordinates, p0 <= p1 <= p2 <= p3 <= window bytes (the slot has a readable
+// pad dword, so p3>>2 may equal the dword count). With P(x) = weighted sum of
+// the slot bytes in [4*(p0>>2), x): tA = P(p1) - P(p0), tB = P(p3) - P(p2).
+// One runtime loop over whole dwords (v_sad_u16 each) plus four masked partials.
+__device__ __forceinline__ void window_sums(const uint8_t* slot, int p0, int p1, int p2, int p3, uint32_t& tA,
                                             uint32_t& tB) {
     const uint32_t* s32 = reinterpret_cast<const uint32_t*>(slot);
-    const int k0 = rs >> 2, km = ms >> 2, ke = ew >> 2;
-    uint32_t acc = 0, pm = 0;
+    const int k0 = p0 >> 2, k1 = p1 >> 2, k2 = p2 >> 2, k3 = p3 >> 2;
+    uint32_t acc = 0, c1 = 0, c2 = 0;
 #pragma unroll 1
-    for (int k = k0; k < ke; ++k) {
-        if (k == km) pm = acc;
+    for (int k = k0; k < k3; ++k) {
+        if (k == k1) c1 = acc;
+        if (k == k2) c2 = acc;
         acc = sad(s32[k], acc);
     }
-    if (km >= ke) pm = acc;
-    const uint32_t p_rs = sad(s32[k0] & first_bytes(rs & 3), 0u);
-    const uint32_t p_ms = sad(s32[km] & first_bytes(ms & 3), pm);
-    const uint32_t p_ew = sad(s32[ke] & first_bytes(ew & 3), acc);
-    tA += p_ms - p_rs;
-    tB += p_ew - p_ms;
+    if (k1 >= k3) c1 = acc;
+    if (k2 >= k3) c2 = acc;
+    const uint32_t P0 = sad(s32[k0] & first_bytes(p0 & 3), 0u);
+    const uint32_t P1 = sad(s32[k1] & first_bytes(p1 & 3), c1);
+    const uint32_t P2 = sad(s32[k2] & first_bytes(p2 & 3), c2);
+    const uint32_t P3 = sad(s32[k3] & first_bytes(p3 & 3), acc);
+    tA += P1 - P0;
+    tB += P3 - P2;
 }
 
 // Skip-word removal, fold, byte-order fix-up, pseudo-header, compare.
@@ -260,8 +343,8 @@ __device__ __forceinline__ void finalize(Parsed& P, uint32_t tA, uint32_t tB, bo
 // benches/rs_sender.rs:38-39,70-71. Byte stores: the fields may sit at odd addresses.
 __device__ __forceinline__ void tx_write(uint8_t* frame, const Parsed& P, uint32_t ipc, uint32_t l4c) {
     if (P.is_v4) {
-        frame[24] = (uint8_t)(ipc >> 8);
-        frame[25] = (uint8_t)ipc;
+        frame[P.l3 + 10] = (uint8_t)(ipc >> 8);
+        frame[P.l3 + 11] = (uint8_t)ipc;
     }
     if (P.st & PNET_ST_L4_CSUM_DONE) {
         frame[P.l4csum_at] = (uint8_t)(l4c >> 8);
@@ -341,12 +424,14 @@ __device__ __forceinline__ void store_columns(const pnetgpu_rx_columns& C, uint6
     if (C.dst_port) put<uint16_t>(C.dst_port, f0 + lane, (uint16_t)P.dp);
     if (C.src_ipv4) put<uint32_t>(C.src_ipv4, f0 + lane, P.s4);
     if (C.dst_ipv4) put<uint32_t>(C.dst_ipv4, f0 + lane, P.d4);
+    if (C.vlan_tci) put<uint16_t>(C.vlan_tci, f0 + lane, (uint16_t)P.vlan_tci);
+    if (C.l3_offset) put<uint8_t>(C.l3_offset, f0 + lane, (uint8_t)P.l3);
     if (C.src_ipv6 || C.dst_ipv6) {
         const bool v6ok = (P.st & (PNET_ST_L3_MASK | PNET_ST_L3_MALFORMED)) == PNET_ST_L3_IPV6;
         uint4 sv = make_uint4(0, 0, 0, 0), dv = make_uint4(0, 0, 0, 0);
         if (v6ok) {
-            sv = lds_read16_unaligned(slot, sh + 22);
-            dv = lds_read16_unaligned(slot, sh + 38);
+            sv = lds_read16_unaligned(slot, sh + (int)P.l3 + 8);
+            dv = lds_read16_unaligned(slot, sh + (int)P.l3 + 24);
         }
         if (C.src_ipv6) reinterpret_cast<uint4*>(C.src_ipv6)[f0 + lane] = sv;
         if (C.dst_ipv6) reinterpret_cast<uint4*>(C.dst_ipv6)[f0 + lane] = dv;
@@ -378,8 +463,11 @@ __device__ __forceinline__ SmallRun small_load(const RxArgs& a, uint64_t run, in
     return r;
 }
 
+#ifndef PNET_SMALL_WAVES
+#define PNET_SMALL_WAVES 4   // waves/SIMD the small kernel is register-bounded for
+#endif
 template <bool TX>
-__global__ __launch_bounds__(kBlock, 5) void rx_small_kernel(RxArgs a) {
+__global__ __launch_bounds__(kBlock, PNET_SMALL_WAVES) void rx_small_kernel(RxArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t lds_slots[kWavesPerBlock][kWave * kSmallSlot];
     __shared__ uint64_t blk_ctr[kWavesPerBlock][PNETGPU_NCOUNTERS];
     const int lane = threadIdx.x & (kWave - 1);
@@ -422,6 +510,7 @@ __global__ __launch_bounds__(kBlock, 5) void rx_small_kernel(RxArgs a) {
                 P.st = PNET_ST_ETH_MALFORMED;
             } else {
                 P.et = bswap16(w3 & 0xFFFFu);
+                P.l3 = 14;
                 if (P.et == 0x0800u) {
                     if (len < 34) {
                         P.st = PNET_ST_L3_IPV4 | PNET_ST_L3_MALFORMED;
@@ -514,9 +603,10 @@ __global__ __launch_bounds__(kBlock, 5) void rx_small_kernel(RxArgs a) {
         const bool need_v6 = a.cols.src_ipv6 || a.cols.dst_ipv6;
         if (__ballot(slow) || need_v6) {
             if (slow) {
-                P = parse_lds(slot, len);
+                // flags are 0 here and the frame (<= 64 B) is entirely in its slot
+                P = parse_frame(FrameBytes{slot, slot, 64}, len, 0u);
                 uint32_t tA = 0, tB = 0;
-                window_sums(slot, P.r0, P.m, P.e, tA, tB);
+                window_sums(slot, P.a_lo, P.a_hi, P.b_lo, P.b_hi, tA, tB);
                 finalize(P, tA, tB, false, ipc, l4c);
             }
         }
@@ -538,7 +628,8 @@ struct WaveLds {
     static constexpr int kSlot = NW * 16 + 4;   // +4 B pad: conflict-free parse reads
     uint8_t win[kWave * kSlot];
     uint64_t base[kWave];     // aligned byte offset of granule 0 of each frame
-    uint32_t end[kWave];      // slot-relative end of the summed range
+    uint32_t end[kWave];      // slot-relative end of the summed range B
+    uint32_t start[kWave];    // slot-relative start of B's part past the window
     uint32_t tail[kWave];     // tail-phase partial sum per frame
     uint8_t list[kWave];      // frames with a tail, in lane order
 };
@@ -609,35 +700,37 @@ __global__ __launch_bounds__(kBlock, 4) void rx_kernel(RxArgs a) {
         // ---- 3. parse + window sums (lane l <-> frame l) -------------------
         Parsed P{};
         if (desc_bad) P.st = PNET_ST_DESC_INVALID;
-        else if (in_batch) P = parse_lds(slot + sh, len);
-        const int rs = P.r0 ? P.r0 + sh : 0;
-        const int ms = P.m ? P.m + sh : 0;
-        const int es = P.e ? P.e + sh : ms;
+        else if (in_batch)
+            P = parse_frame(FrameBytes{slot + sh, a.data + off, kWin - sh}, len, a.flags);
+        // A (<= 97 B into the frame) always lies in the window; B may run past it
+        const int p0 = P.a_lo + sh, p1 = P.a_hi + sh, p2 = P.b_lo + sh, p3 = P.b_hi + sh;
         uint32_t tA = 0, tB = 0;
-        window_sums(slot, rs, ms, min(es, kWin), tA, tB);
+        window_sums(slot, p0, p1, min(p2, kWin), min(p3, kWin), tA, tB);
 
-        // ---- 4. tail: frames longer than the window, via a per-wave work list --
-        const bool has_tail = es > kWin;
+        // ---- 4. tail: B bytes past the window, via a per-wave work list ------
+        const bool has_tail = p3 > kWin;
         const uint64_t tmask = __ballot(has_tail);
         if (tmask) {
             const int count = __popcll(tmask);
             if (has_tail) {
                 const int pos = __popcll(tmask & ((1ull << lane) - 1ull));
                 L.list[pos] = (uint8_t)lane;
-                L.end[lane] = (uint32_t)es;
+                L.end[lane] = (uint32_t)p3;
+                L.start[lane] = (uint32_t)max(p2, kWin);
             }
             wave_sync();
             const int grp = lane / G, j = lane % G;
             int idx = grp;
             int fl = 0;
-            uint32_t fe = 0, nneed = 0, c0 = 0, acc = 0;
+            uint32_t fs = 0, fe = 0, nneed = 0, c0 = 0, acc = 0;
             const uint8_t* fb = a.data;
             if (idx < count) {
                 fl = L.list[idx];
+                fs = L.start[fl];
                 fe = L.end[fl];
                 fb = a.data + L.base[fl];
                 nneed = (fe + 15u) >> 4;
-                c0 = NW + j;
+                c0 = (fs >> 4) + j;
             }
             while (__ballot(idx < count)) {
                 if (idx < count) {
@@ -652,12 +745,12 @@ __global__ __launch_bounds__(kBlock, 4) void rx_kernel(RxArgs a) {
                     for (int u = 0; u < U; ++u) {
                         const uint32_t c = c0 + u * G;
                         uint32_t x = v[u].x, y = v[u].y, z = v[u].z, w = v[u].w;
-                        if (c + 1 == nneed && (fe & 15u)) {   // last granule: drop bytes past the end
-                            const int r = (int)(fe & 15u);
-                            x &= first_bytes(clamp04(r));
-                            y &= first_bytes(clamp04(r - 4));
-                            z &= first_bytes(clamp04(r - 8));
-                            w &= first_bytes(clamp04(r - 12));
+                        const int hi = (int)fe - (int)(16u * c), lo = (int)fs - (int)(16u * c);
+                        if (hi < 16 || lo > 0) {               // granule straddles an end of B
+                            x &= first_bytes(clamp04(hi)) & ~first_bytes(clamp04(lo));
+                            y &= first_bytes(clamp04(hi - 4)) & ~first_bytes(clamp04(lo - 4));
+                            z &= first_bytes(clamp04(hi - 8)) & ~first_bytes(clamp04(lo - 8));
+                            w &= first_bytes(clamp04(hi - 12)) & ~first_bytes(clamp04(lo - 12));
                         }
                         acc = sad(x, acc);
                         acc = sad(y, acc);
@@ -673,10 +766,11 @@ __global__ __launch_bounds__(kBlock, 4) void rx_kernel(RxArgs a) {
                         idx += kGroups;
                         if (idx < count) {
                             fl = L.list[idx];
+                            fs = L.start[fl];
                             fe = L.end[fl];
                             fb = a.data + L.base[fl];
                             nneed = (fe + 15u) >> 4;
-                            c0 = NW + j;
+                            c0 = (fs >> 4) + j;
                         }
                     }
                 }

@@ -38,11 +38,15 @@ COLUMNS = {
     "dst_ipv4": (torch.int32, np.uint32, ()),
     "src_ipv6": (torch.uint8, np.uint8, (16,)),
     "dst_ipv6": (torch.uint8, np.uint8, (16,)),
+    "vlan_tci": (torch.int16, np.uint16, ()),
+    "l3_offset": (torch.uint8, np.uint8, ()),
 }
 assert tuple(COLUMNS) == COLUMN_NAMES
 
 #: every IPv4-relevant column: the bench's "checksum verify + header extract" record
-IPV4_COLUMNS = tuple(c for c in COLUMN_NAMES if not c.endswith("ipv6"))
+IPV4_COLUMNS = ("status", "ip_csum", "l4_csum", "ethertype", "ip_proto", "ttl", "l4_offset", "l4_length",
+                "src_port", "dst_port", "src_ipv4", "dst_ipv4")
+RX_VLAN, RX_IPV6_EXT = DEFS["PNETGPU_RX_VLAN"], DEFS["PNETGPU_RX_IPV6_EXT"]
 ALL_COLUMNS = COLUMN_NAMES
 NCOUNTERS = DEFS["PNETGPU_NCOUNTERS"]
 COUNTER_NAMES = ("frames", "bytes", "ipv4", "ipv6", "ip_csum_bad", "l4_csum_bad", "malformed", "unknown")
@@ -136,28 +140,29 @@ def _check_u8_cuda(t, what):
 
 
 def rx_process(data, *, n_frames=None, stride=0, frame_len=None, first_offset=0, offsets=None, lengths=None,
-               columns=IPV4_COLUMNS, counters=True, out=None, stream=None, data_bytes=None):
+               columns=IPV4_COLUMNS, counters=True, out=None, stream=None, data_bytes=None, flags=0):
     """Parse + verify every frame of a device-resident batch.
 
     Fixed-stride mode: stride > 0, frame i = data[first_offset + i*stride, +frame_len).
     Descriptor mode:   offsets (int64) / lengths (int32) CUDA tensors, frame i = data[off_i, +len_i).
     Returns an RxResult (device columns, accumulated counters)."""
     return _rx_or_tx("pnetgpu_rx_process", data, n_frames, stride, frame_len, first_offset, offsets, lengths,
-                     columns, counters, out, stream, data_bytes)
+                     columns, counters, out, stream, data_bytes, flags)
 
 
 def tx_fill_checksums(data, *, n_frames=None, stride=0, frame_len=None, first_offset=0, offsets=None,
-                      lengths=None, columns=("status",), counters=False, out=None, stream=None, data_bytes=None):
+                      lengths=None, columns=("status",), counters=False, out=None, stream=None, data_bytes=None,
+                      flags=0):
     """Sender side: write every checksum the receive path computes into its field, in place
     (set_checksum(ipv4::checksum(..)), set_checksum(udp::ipv4_checksum(..)), ... as
     benches/rs_sender.rs:38-39,70-71). Frames must not overlap. The returned columns
     describe the frames before patching."""
     return _rx_or_tx("pnetgpu_tx_fill_checksums", data, n_frames, stride, frame_len, first_offset, offsets,
-                     lengths, columns, counters, out, stream, data_bytes)
+                     lengths, columns, counters, out, stream, data_bytes, flags)
 
 
 def _rx_or_tx(fn_name, data, n_frames, stride, frame_len, first_offset, offsets, lengths, columns, counters, out,
-              stream, data_bytes):
+              stream, data_bytes, flags):
     _check_u8_cuda(data, "data")
     if stride:
         if n_frames is None:
@@ -176,7 +181,7 @@ def _rx_or_tx(fn_name, data, n_frames, stride, frame_len, first_offset, offsets,
         out = RxResult(n_frames, data.device, columns, counters)
     b = Batch(data.data_ptr(), data.numel() if data_bytes is None else data_bytes, n_frames, first_offset,
               stride, frame_len, offsets.data_ptr() if offsets is not None else 0,
-              lengths.data_ptr() if lengths is not None else 0)
+              lengths.data_ptr() if lengths is not None else 0, flags, 0)
     cols = out.c_struct()
     ctx = context(data.device.index)
     check(getattr(lib, fn_name)(ctx.handle, ctypes.byref(b), ctypes.byref(cols),

@@ -24,7 +24,7 @@ class RingBatch(ctypes.Structure):
 def _setup():
     vp, u64, u32, i32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int
     lib.pnetgpu_ring_create.restype = i32
-    lib.pnetgpu_ring_create.argtypes = [vp, u64, u32, ctypes.POINTER(vp)]
+    lib.pnetgpu_ring_create.argtypes = [vp, u64, u32, u32, ctypes.POINTER(vp)]
     lib.pnetgpu_ring_destroy.restype = None
     lib.pnetgpu_ring_destroy.argtypes = [vp]
     lib.pnetgpu_ring_push.restype = i32
@@ -75,11 +75,11 @@ class Batch:
 class Ring:
     """Pinned host batches -> asynchronous GPU verification (three rotating slots)."""
 
-    def __init__(self, batch_bytes=64 << 20, batch_frames=1 << 18, device=0, copy=True):
+    def __init__(self, batch_bytes=64 << 20, batch_frames=1 << 18, device=0, copy=True, flags=0):
         self.ctx = context(device)
         self.copy = copy
         h = ctypes.c_void_p()
-        check(lib.pnetgpu_ring_create(self.ctx.handle, batch_bytes, batch_frames, ctypes.byref(h)),
+        check(lib.pnetgpu_ring_create(self.ctx.handle, batch_bytes, batch_frames, flags, ctypes.byref(h)),
               "pnetgpu_ring_create")
         self.h = h
         self.pending = 0

@@ -18,7 +18,10 @@ REC_DTYPE = np.dtype([
     ("src_port", "<u2"), ("dst_port", "<u2"), ("_pad", "<u2"),
     ("src_ipv4", "<u4"), ("dst_ipv4", "<u4"),
     ("src_ipv6", "u1", (16,)), ("dst_ipv6", "u1", (16,)),
+    ("vlan_tci", "<u2"), ("l3_offset", "u1"), ("_pad2", "u1"),
 ], align=True)
+
+RX_VLAN, RX_IPV6_EXT = 0x1, 0x2
 
 _lib = None
 
@@ -44,6 +47,13 @@ def lib():
                           u8p, u8p, ctypes.c_uint8]
         L.oracle_rx_frame.restype = None
         L.oracle_rx_frame.argtypes = [u8p, ctypes.c_size_t, ctypes.c_void_p]
+        L.oracle_rx_frame_ex.restype = None
+        L.oracle_rx_frame_ex.argtypes = [u8p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_void_p]
+        L.oracle_rx_batch_ex.restype = None
+        L.oracle_rx_batch_ex.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
+                                         ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
+                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                         ctypes.c_void_p, ctypes.c_int]
         L.oracle_rx_batch.restype = None
         L.oracle_rx_batch.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
                                       ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
@@ -52,7 +62,7 @@ def lib():
         L.oracle_tx_fill.restype = None
         L.oracle_tx_fill.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
                                      ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
-                                     ctypes.c_void_p]
+                                     ctypes.c_uint32, ctypes.c_void_p]
         L.oracle_checksum_slices.restype = None
         L.oracle_checksum_slices.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
                                              ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
@@ -84,14 +94,14 @@ def ipv6_checksum(data, skipword, extra, src, dst, proto):
                                       _buf(src), _buf(dst), proto)
 
 
-def rx_frame(frame):
+def rx_frame(frame, flags=0):
     rec = np.zeros(1, dtype=REC_DTYPE)
-    lib().oracle_rx_frame(_buf(frame), len(frame), rec.ctypes.data)
+    lib().oracle_rx_frame_ex(_buf(frame), len(frame), flags, rec.ctypes.data)
     return rec[0]
 
 
 def rx_batch(buf, n, *, stride=0, frame_len=0, first=0, offsets=None, lengths=None,
-             nthreads=1):
+             nthreads=1, flags=0):
     """Oracle records for a frame batch held in a numpy uint8 array."""
     buf = np.ascontiguousarray(buf, dtype=np.uint8)
     out = np.zeros(n, dtype=REC_DTYPE)
@@ -100,8 +110,8 @@ def rx_batch(buf, n, *, stride=0, frame_len=0, first=0, offsets=None, lengths=No
         offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
         lengths = np.ascontiguousarray(lengths, dtype=np.uint32)
         offp, lenp = offsets.ctypes.data, lengths.ctypes.data
-    lib().oracle_rx_batch(buf.ctypes.data, buf.size, n, first, stride, frame_len,
-                          offp, lenp, out.ctypes.data, nthreads)
+    lib().oracle_rx_batch_ex(buf.ctypes.data, buf.size, n, first, stride, frame_len,
+                             offp, lenp, flags, out.ctypes.data, nthreads)
     return out
 
 
@@ -116,7 +126,7 @@ def checksum_slices(buf, offsets, lengths, skipwords):
     return out
 
 
-def tx_fill(buf, n, *, stride=0, frame_len=0, first=0, offsets=None, lengths=None):
+def tx_fill(buf, n, *, stride=0, frame_len=0, first=0, offsets=None, lengths=None, flags=0):
     """Patch a COPY of buf the way the sender side does; returns (patched, records)."""
     out_buf = np.array(buf, dtype=np.uint8, copy=True)
     recs = np.zeros(n, dtype=REC_DTYPE)
@@ -126,5 +136,5 @@ def tx_fill(buf, n, *, stride=0, frame_len=0, first=0, offsets=None, lengths=Non
         lengths = np.ascontiguousarray(lengths, dtype=np.uint32)
         offp, lenp = offsets.ctypes.data, lengths.ctypes.data
     lib().oracle_tx_fill(out_buf.ctypes.data, out_buf.size, n, first, stride, frame_len, offp, lenp,
-                         recs.ctypes.data)
+                         flags, recs.ctypes.data)
     return out_buf, recs

@@ -153,8 +153,8 @@ static void l4_dispatch(oracle_rec* r, int is_v6, uint8_t proto, slice_t l4,
     }
 }
 
-/* packetdump.rs:155-168 handle_ipv4_packet */
-static void handle_ipv4(oracle_rec* r, slice_t ep) {
+/* packetdump.rs:155-168 handle_ipv4_packet; ep = Ipv4 bytes at frame offset l3 */
+static void handle_ipv4(oracle_rec* r, slice_t ep, size_t l3) {
     r->status |= ORACLE_ST_L3_IPV4;
     if (ep.len < 20) { r->status |= ORACLE_ST_L3_MALFORMED; return; }  /* Ipv4Packet::new, min 20 */
     const uint8_t* ip = ep.p;
@@ -184,14 +184,22 @@ static void handle_ipv4(oracle_rec* r, slice_t ep) {
         if (end > ep.len) end = ep.len;
         l4.p = ip + start;
         l4.len = end - start;
-        r->l4_offset = (uint16_t)(14 + start);
+        r->l4_offset = (uint16_t)(l3 + start);
         r->l4_length = (uint16_t)l4.len;
     }
     l4_dispatch(r, 0, ip[9], l4, ip + 12, ip + 16);
 }
 
-/* packetdump.rs:170-183 handle_ipv6_packet */
-static void handle_ipv6(oracle_rec* r, slice_t ep) {
+/* packetdump.rs:170-183 handle_ipv6_packet; with ORACLE_RX_IPV6_EXT the
+ * extension headers of ipv6.rs:39-137 are walked first (at most 4):
+ * Hop-by-Hop (0) / Destination (60): Extension, min 2 bytes, length
+ * hdr_ext_len*8+8 (ipv6_extension_length + the 2 fixed bytes, ipv6.rs:56-58);
+ * Routing (43): min 4, same length (ipv6.rs:75-77); Fragment (44): 8 bytes
+ * (ipv6.rs:80-89), get_fragment_offset = value & !0x3 (ipv6.rs:95-97): a
+ * non-first fragment carries no L4 header (PNET_ST_FRAGMENT, no dispatch).
+ * A truncated extension header (its new() == None, or its length running past
+ * the payload) sets L4_MALFORMED. */
+static void handle_ipv6(oracle_rec* r, slice_t ep, size_t l3, uint32_t flags) {
     r->status |= ORACLE_ST_L3_IPV6;
     if (ep.len < 40) { r->status |= ORACLE_ST_L3_MALFORMED; return; }  /* Ipv6Packet::new, min 40 */
     const uint8_t* ip = ep.p;
@@ -201,29 +209,91 @@ static void handle_ipv6(oracle_rec* r, slice_t ep) {
     memcpy(r->dst_ipv6, ip + 24, 16);
     /* payload bounded by payload_length (ipv6.rs:34-36, #[length = "payload_length"]) */
     size_t payload_length = be16(ip + 4);
-    slice_t l4 = { NULL, 0 };
+    slice_t pl = { NULL, 0 };
     if (ep.len > 40) {
         size_t end = 40 + payload_length;
         if (end > ep.len) end = ep.len;
-        l4.p = ip + 40;
-        l4.len = end - 40;
-        r->l4_offset = 14 + 40;
+        pl.p = ip + 40;
+        pl.len = end - 40;
+    }
+    uint8_t next = ip[6];
+    size_t pos = 0;
+    if (flags & ORACLE_RX_IPV6_EXT) {
+        for (int k = 0; k < 4; ++k) {
+            if (next == 0 || next == 60 || next == 43) {
+                size_t minl = next == 43 ? 4 : 2;
+                if (pl.len - pos < minl) { r->ip_proto = next; r->status |= ORACLE_ST_L4_MALFORMED; return; }
+                size_t el = (size_t)pl.p[pos + 1] * 8 + 8;
+                if (el > pl.len - pos) { r->ip_proto = next; r->status |= ORACLE_ST_L4_MALFORMED; return; }
+                next = pl.p[pos];
+                pos += el;
+            } else if (next == 44) {
+                if (pl.len - pos < 8) { r->ip_proto = next; r->status |= ORACLE_ST_L4_MALFORMED; return; }
+                unsigned fo = be16(pl.p + pos + 2);
+                next = pl.p[pos];
+                pos += 8;
+                if ((fo & 0xFFFCu) != 0) {                /* not the first fragment */
+                    r->ip_proto = next;
+                    r->status |= ORACLE_ST_FRAGMENT;
+                    if (pl.len > pos) {
+                        r->l4_offset = (uint16_t)(l3 + 40 + pos);
+                        r->l4_length = (uint16_t)(pl.len - pos);
+                    }
+                    return;
+                }
+            } else {
+                break;
+            }
+        }
+        r->ip_proto = next;
+    }
+    slice_t l4 = { NULL, 0 };
+    if (pl.len > pos) {
+        l4.p = pl.p + pos;
+        l4.len = pl.len - pos;
+        r->l4_offset = (uint16_t)(l3 + 40 + pos);
         r->l4_length = (uint16_t)l4.len;
     }
-    l4_dispatch(r, 1, ip[6], l4, ip + 8, ip + 24);
+    l4_dispatch(r, 1, next, l4, ip + 8, ip + 24);
 }
 
-/* packetdump.rs:200-217 handle_ethernet_frame */
-void oracle_rx_frame(const uint8_t* frame, size_t len, oracle_rec* r) {
+static int is_vlan_tpid(unsigned et) {       /* EtherTypes::Vlan / PBridge / QinQ, ethernet.rs:102-112 */
+    return et == 0x8100 || et == 0x88A8 || et == 0x9100;
+}
+
+/* packetdump.rs:200-217 handle_ethernet_frame; with ORACLE_RX_VLAN up to two
+ * VlanPacket views (vlan.rs:62-72: 4 bytes, inner ethertype at +2) are peeled
+ * first and the IP header starts after them. */
+void oracle_rx_frame_ex(const uint8_t* frame, size_t len, uint32_t flags, oracle_rec* r) {
     memset(r, 0, sizeof(*r));
     if (len < 14) { r->status = ORACLE_ST_ETH_MALFORMED; return; }  /* EthernetPacket::new, min 14 */
-    r->ethertype = be16(frame + 12);                      /* ethernet.rs:27-28 */
-    slice_t ep = { frame + 14, len - 14 };                /* payload: last field, unbounded */
-    switch (r->ethertype) {
-    case 0x0800: handle_ipv4(r, ep); break;              /* EtherTypes::Ipv4, ethernet.rs:68 */
-    case 0x86DD: handle_ipv6(r, ep); break;              /* EtherTypes::Ipv6, ethernet.rs:88 */
+    unsigned et = be16(frame + 12);                       /* ethernet.rs:27-28 */
+    size_t l3 = 14;
+    if (flags & ORACLE_RX_VLAN) {
+        for (int k = 0; k < 2 && is_vlan_tpid(et); ++k) {
+            r->status |= ORACLE_ST_VLAN;
+            if (len < l3 + 4) {                           /* VlanPacket::new == None */
+                r->ethertype = (uint16_t)et;
+                r->status |= ORACLE_ST_L3_MALFORMED;
+                return;
+            }
+            if (k == 0) r->vlan_tci = be16(frame + l3);
+            et = be16(frame + l3 + 2);
+            l3 += 4;
+        }
+    }
+    r->ethertype = (uint16_t)et;
+    r->l3_offset = (uint8_t)l3;
+    slice_t ep = { frame + l3, len - l3 };                /* payload: last field, unbounded */
+    switch (et) {
+    case 0x0800: handle_ipv4(r, ep, l3); break;          /* EtherTypes::Ipv4, ethernet.rs:68 */
+    case 0x86DD: handle_ipv6(r, ep, l3, flags); break;   /* EtherTypes::Ipv6, ethernet.rs:88 */
     default: r->status |= ORACLE_ST_UNKNOWN_ETHERTYPE; break;
     }
+}
+
+void oracle_rx_frame(const uint8_t* frame, size_t len, oracle_rec* r) {
+    oracle_rx_frame_ex(frame, len, 0, r);
 }
 
 /* ---- batch drivers ------------------------------------------------------ */
@@ -231,7 +301,7 @@ void oracle_rx_frame(const uint8_t* frame, size_t len, oracle_rec* r) {
 typedef struct {
     const uint8_t* buf; uint64_t buf_len; uint64_t lo, hi;
     uint64_t first; uint32_t stride, frame_len;
-    const uint64_t* offsets; const uint32_t* lengths; oracle_rec* out;
+    const uint64_t* offsets; const uint32_t* lengths; oracle_rec* out; uint32_t flags;
 } shard_t;
 
 static void* rx_shard(void* arg) {
@@ -244,7 +314,7 @@ static void* rx_shard(void* arg) {
             s->out[i].status = ORACLE_ST_DESC_INVALID;
             continue;
         }
-        oracle_rx_frame(s->buf + off, (size_t)len, &s->out[i]);
+        oracle_rx_frame_ex(s->buf + off, (size_t)len, s->flags, &s->out[i]);
     }
     return NULL;
 }
@@ -253,13 +323,20 @@ void oracle_rx_batch(const uint8_t* buf, uint64_t buf_len, uint64_t n,
                      uint64_t first, uint32_t stride, uint32_t frame_len,
                      const uint64_t* offsets, const uint32_t* lengths,
                      oracle_rec* out, int nthreads) {
+    oracle_rx_batch_ex(buf, buf_len, n, first, stride, frame_len, offsets, lengths, 0, out, nthreads);
+}
+
+void oracle_rx_batch_ex(const uint8_t* buf, uint64_t buf_len, uint64_t n,
+                        uint64_t first, uint32_t stride, uint32_t frame_len,
+                        const uint64_t* offsets, const uint32_t* lengths, uint32_t flags,
+                        oracle_rec* out, int nthreads) {
     if (nthreads < 1) nthreads = 1;
     if (nthreads > 256) nthreads = 256;
     shard_t sh[256];
     pthread_t th[256];
     for (int t = 0; t < nthreads; ++t) {
         shard_t s = { buf, buf_len, n * (uint64_t)t / nthreads, n * (uint64_t)(t + 1) / nthreads,
-                      first, stride, frame_len, offsets, lengths, out };
+                      first, stride, frame_len, offsets, lengths, out, flags };
         sh[t] = s;
     }
     if (nthreads == 1) { rx_shard(&sh[0]); return; }
@@ -281,7 +358,8 @@ size_t oracle_rec_size(void) { return sizeof(oracle_rec); }
  * dispatch computes is written big-endian into its field, in place. The record
  * describes the frame as it was before patching. */
 void oracle_tx_fill(uint8_t* buf, uint64_t buf_len, uint64_t n, uint64_t first, uint32_t stride,
-                    uint32_t frame_len, const uint64_t* offsets, const uint32_t* lengths, oracle_rec* out) {
+                    uint32_t frame_len, const uint64_t* offsets, const uint32_t* lengths, uint32_t flags,
+                    oracle_rec* out) {
     for (uint64_t i = 0; i < n; ++i) {
         uint64_t off = stride ? first + i * (uint64_t)stride : offsets[i];
         uint64_t len = stride ? frame_len : lengths[i];
@@ -292,10 +370,10 @@ void oracle_tx_fill(uint8_t* buf, uint64_t buf_len, uint64_t n, uint64_t first, 
             continue;
         }
         uint8_t* f = buf + off;
-        oracle_rx_frame(f, (size_t)len, r);
+        oracle_rx_frame_ex(f, (size_t)len, flags, r);
         if ((r->status & (ORACLE_ST_L3_IPV4 | ORACLE_ST_L3_IPV6 | ORACLE_ST_L3_MALFORMED)) == ORACLE_ST_L3_IPV4) {
-            f[24] = (uint8_t)(r->ip_csum >> 8);          /* Ipv4 checksum field, bytes 10-11 of the header */
-            f[25] = (uint8_t)r->ip_csum;
+            f[r->l3_offset + 10] = (uint8_t)(r->ip_csum >> 8);   /* Ipv4 checksum field, header bytes 10-11 */
+            f[r->l3_offset + 11] = (uint8_t)r->ip_csum;
         }
         if (r->status & ORACLE_ST_L4_CSUM_DONE) {
             unsigned kind = r->status & (7u << ORACLE_ST_L4_SHIFT);

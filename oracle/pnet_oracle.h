@@ -53,7 +53,13 @@ extern "C" {
 #define ORACLE_ST_L4_CSUM_OK       0x0400u
 #define ORACLE_ST_UNKNOWN_ETHERTYPE 0x0800u
 #define ORACLE_ST_UNKNOWN_PROTO    0x1000u
+#define ORACLE_ST_VLAN             0x2000u
+#define ORACLE_ST_FRAGMENT         0x4000u
 #define ORACLE_ST_DESC_INVALID     0x8000u
+
+/* opt-in dispatch extensions (beyond packetdump.rs's chain) */
+#define ORACLE_RX_VLAN      0x1u   /* follow 802.1Q/802.1ad/QinQ tags, vlan.rs:62-72 (<= 2)   */
+#define ORACLE_RX_IPV6_EXT  0x2u   /* walk IPv6 extension headers, ipv6.rs:39-137 (<= 4)      */
 
 /* One receive record: the same fields as the GPU result columns. */
 typedef struct oracle_rec {
@@ -71,6 +77,9 @@ typedef struct oracle_rec {
     uint32_t dst_ipv4;
     uint8_t  src_ipv6[16];
     uint8_t  dst_ipv6[16];
+    uint16_t vlan_tci;    /* outer VLAN tag control information (RX_VLAN)   */
+    uint8_t  l3_offset;   /* frame offset of the IP header                 */
+    uint8_t  _pad;
 } oracle_rec;
 
 /* util.rs:158-181 */
@@ -90,6 +99,8 @@ uint16_t oracle_ipv6_checksum(const uint8_t* data, size_t len, size_t skipword,
 
 /* Receive dispatch for one Ethernet frame (packetdump.rs:120-217). */
 void oracle_rx_frame(const uint8_t* frame, size_t len, oracle_rec* out);
+/* Same with opt-in extensions (ORACLE_RX_*). */
+void oracle_rx_frame_ex(const uint8_t* frame, size_t len, uint32_t flags, oracle_rec* out);
 
 /*
  * Batch form over a frame buffer. stride > 0: frame i = buf[first + i*stride,
@@ -101,13 +112,18 @@ void oracle_rx_batch(const uint8_t* buf, uint64_t buf_len, uint64_t n,
                      uint64_t first, uint32_t stride, uint32_t frame_len,
                      const uint64_t* offsets, const uint32_t* lengths,
                      oracle_rec* out, int nthreads);
+void oracle_rx_batch_ex(const uint8_t* buf, uint64_t buf_len, uint64_t n,
+                        uint64_t first, uint32_t stride, uint32_t frame_len,
+                        const uint64_t* offsets, const uint32_t* lengths, uint32_t flags,
+                        oracle_rec* out, int nthreads);
 
 size_t oracle_rec_size(void);
 
 /* Sender side (benches/rs_sender.rs:38-39,70-71): write every computed checksum
  * into its stored field in place; records describe the frames before patching. */
 void oracle_tx_fill(uint8_t* buf, uint64_t buf_len, uint64_t n, uint64_t first, uint32_t stride,
-                    uint32_t frame_len, const uint64_t* offsets, const uint32_t* lengths, oracle_rec* out);
+                    uint32_t frame_len, const uint64_t* offsets, const uint32_t* lengths, uint32_t flags,
+                    oracle_rec* out);
 
 /* Batched util::checksum over (offset, length, skipword) slices. */
 void oracle_checksum_slices(const uint8_t* buf, uint64_t n, const uint64_t* offsets,

@@ -25,10 +25,14 @@ ST_L4_CSUM_DONE = 0x0200
 ST_L4_CSUM_OK = 0x0400
 ST_UNKNOWN_ETHERTYPE = 0x0800
 ST_UNKNOWN_PROTO = 0x1000
+ST_VLAN = 0x2000
+ST_FRAGMENT = 0x4000
 ST_DESC_INVALID = 0x8000
+RX_VLAN, RX_IPV6_EXT = 0x1, 0x2
 
 FIELDS = ("status", "ip_csum", "l4_csum", "ethertype", "ip_proto", "ttl", "l4_offset",
-          "l4_length", "src_port", "dst_port", "src_ipv4", "dst_ipv4", "src_ipv6", "dst_ipv6")
+          "l4_length", "src_port", "dst_port", "src_ipv4", "dst_ipv4", "src_ipv6", "dst_ipv6",
+          "vlan_tci", "l3_offset")
 
 
 def sum_be_words(d, skip):
@@ -70,7 +74,7 @@ def _be16(b, i):
     return (b[i] << 8) | b[i + 1]
 
 
-def rx_frame(frame):
+def rx_frame(frame, flags=0):
     f = bytes(frame)
     r = dict.fromkeys(FIELDS, 0)
     r["src_ipv6"] = bytes(16)
@@ -78,10 +82,24 @@ def rx_frame(frame):
     if len(f) < 14:
         r["status"] = ST_ETH_MALFORMED
         return r
-    et = _be16(f, 12)
-    r["ethertype"] = et
-    ep = f[14:]
     st = 0
+    et = _be16(f, 12)
+    l3 = 14
+    if flags & RX_VLAN:                      # vlan.rs:62-72; TPIDs ethernet.rs:102,104,112
+        for k in range(2):
+            if et not in (0x8100, 0x88A8, 0x9100):
+                break
+            st |= ST_VLAN
+            if len(f) < l3 + 4:
+                r["ethertype"], r["status"] = et, st | ST_L3_MALFORMED
+                return r
+            if k == 0:
+                r["vlan_tci"] = _be16(f, l3)
+            et = _be16(f, l3 + 2)
+            l3 += 4
+    r["ethertype"] = et
+    r["l3_offset"] = l3
+    ep = f[l3:]
     if et == 0x0800:
         st |= ST_L3_IPV4
         if len(ep) < 20:
@@ -100,7 +118,7 @@ def rx_frame(frame):
         l4 = b""
         if len(ep) > start:
             l4 = ep[start:min(start + plen, len(ep))]
-            r["l4_offset"], r["l4_length"] = 14 + start, len(l4)
+            r["l4_offset"], r["l4_length"] = l3 + start, len(l4)
         src, dst, proto, v6 = ep[12:16], ep[16:20], ep[9], False
     elif et == 0x86DD:
         st |= ST_L3_IPV6
@@ -109,13 +127,36 @@ def rx_frame(frame):
             return r
         r["ip_proto"], r["ttl"] = ep[6], ep[7]
         r["src_ipv6"], r["dst_ipv6"] = ep[8:24], ep[24:40]
-        l4 = b""
-        if len(ep) > 40:
-            l4 = ep[40:min(40 + _be16(ep, 4), len(ep))]
-            r["l4_offset"], r["l4_length"] = 54, len(l4)
-        src, dst, proto, v6 = ep[8:24], ep[24:40], ep[6], True
+        pl = ep[40:min(40 + _be16(ep, 4), len(ep))] if len(ep) > 40 else b""
+        proto, pos = ep[6], 0
+        if flags & RX_IPV6_EXT:              # ipv6.rs:39-137
+            for _ in range(4):
+                if proto in (0, 60, 43):
+                    if len(pl) - pos < (4 if proto == 43 else 2) or pl[pos + 1] * 8 + 8 > len(pl) - pos:
+                        r["ip_proto"], r["status"] = proto, st | ST_L4_MALFORMED
+                        return r
+                    proto, pos = pl[pos], pos + pl[pos + 1] * 8 + 8
+                elif proto == 44:
+                    if len(pl) - pos < 8:
+                        r["ip_proto"], r["status"] = proto, st | ST_L4_MALFORMED
+                        return r
+                    fo = _be16(pl, pos + 2)
+                    proto, pos = pl[pos], pos + 8
+                    if fo & 0xFFFC:
+                        r["ip_proto"] = proto
+                        if len(pl) > pos:
+                            r["l4_offset"], r["l4_length"] = l3 + 40 + pos, len(pl) - pos
+                        r["status"] = st | ST_FRAGMENT
+                        return r
+                else:
+                    break
+            r["ip_proto"] = proto
+        l4 = pl[pos:]
+        if l4:
+            r["l4_offset"], r["l4_length"] = l3 + 40 + pos, len(l4)
+        src, dst, v6 = ep[8:24], ep[24:40], True
     else:
-        r["status"] = ST_UNKNOWN_ETHERTYPE
+        r["status"] = st | ST_UNKNOWN_ETHERTYPE
         return r
 
     table = {17: (ST_L4_UDP, 8, 3, 6), 6: (ST_L4_TCP, 20, 8, 16),

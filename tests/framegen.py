@@ -165,3 +165,100 @@ def pack(frames, align=1, gap=0, rng=None):
     parts.append(bytes((-pos) % 16 + 16))  # readable tail up to a 16-B multiple
     buf = np.frombuffer(b"".join(parts), dtype=np.uint8).copy()
     return buf, np.array(offs, dtype=np.uint64), np.array(lens, dtype=np.uint32)
+
+
+# ---- opt-in extensions: VLAN tags and IPv6 extension headers ----------------
+
+def add_vlan(frame, tags):
+    """Insert VLAN tags (list of (tpid, tci)) after the MAC addresses."""
+    f = bytes(frame)
+    if len(f) < 14:
+        return f
+    out = bytearray(f[:12])
+    for tpid, tci in tags:
+        out += tpid.to_bytes(2, "big") + tci.to_bytes(2, "big")
+    out += f[12:]
+    # the tags' inner ethertypes chain: tag k's "ethertype" field is the next TPID / the real one
+    pos = 12
+    tpids = [t for t, _ in tags] + [int.from_bytes(f[12:14], "big")]
+    for k in range(len(tags)):
+        out[pos:pos + 2] = tpids[k].to_bytes(2, "big")
+        out[pos + 4:pos + 6] = tpids[k + 1].to_bytes(2, "big")
+        pos += 4
+    return bytes(out)
+
+
+def ipv6_with_ext(rng, exts, l4_kind, l4_len, frag_offset=0):
+    """An Eth/IPv6 frame whose payload is a chain of extension headers then L4.
+    exts: list of header type ids (0, 43, 44, 60); checksums are valid for the
+    final L4 (pseudo-header = base addresses + L4 slice length)."""
+    proto = {"udp": 17, "tcp": 6, "icmp6": 58, "icmp": 1, "none": 59}[l4_kind]
+    chain = bytearray()
+    types = list(exts) + [proto]
+    for k, t in enumerate(exts):
+        nxt = types[k + 1]
+        if t == 44:
+            fo = (frag_offset << 3) & 0xFFF8
+            chain += bytes([nxt, 0]) + fo.to_bytes(2, "big") + rng.integers(0, 256, 4, dtype=np.uint8).tobytes()
+        else:
+            hel = int(rng.integers(0, 4))
+            body = rng.integers(0, 256, hel * 8 + 6, dtype=np.uint8).tobytes()
+            if t == 43:
+                body = bytes([int(rng.integers(0, 4)), int(rng.integers(0, 3))]) + body[2:]
+            chain += bytes([nxt, hel]) + body
+    base = bytearray(build_frame(rng, "udp6", 8))[:54]
+    base[20] = types[0] if exts else proto
+    l4 = bytearray(rng.integers(0, 256, l4_len, dtype=np.uint8).tobytes())
+    src, dst = bytes(base[22:38]), bytes(base[38:54])
+    if proto == 17 and l4_len >= 8:
+        _set16(l4, 4, l4_len)
+        _set16(l4, 6, 0)
+        _set16(l4, 6, po.ipv6_checksum(bytes(l4), 3, b"", src, dst, 17))
+    elif proto == 6 and l4_len >= 20:
+        l4[12] = 5 << 4
+        _set16(l4, 16, 0)
+        _set16(l4, 16, po.ipv6_checksum(bytes(l4), 8, b"", src, dst, 6))
+    elif proto == 58 and l4_len >= 4:
+        _set16(l4, 2, 0)
+        _set16(l4, 2, po.ipv6_checksum(bytes(l4), 1, b"", src, dst, 58))
+    elif proto == 1 and l4_len >= 4:
+        _set16(l4, 2, 0)
+        _set16(l4, 2, po.checksum(bytes(l4), 1))
+    payload = bytes(chain) + bytes(l4)
+    _set16(base, 18, len(payload))
+    return bytes(base) + payload
+
+
+def extension_frames(rng):
+    """VLAN / QinQ / IPv6-extension frames incl. truncations and long chains."""
+    out = []
+    kinds = ("udp", "tcp", "icmp", "udp6", "tcp6", "icmp6")
+    tag_sets = ([], [(0x8100, 0x0064)], [(0x88A8, 0x2001), (0x8100, 0xE00A)], [(0x9100, 5), (0x9100, 6)],
+                [(0x8100, 1), (0x8100, 2), (0x8100, 3)])
+    for tags in tag_sets:
+        for k in kinds:
+            for l4 in (0, 4, 8, 13, 20, 33, 200):
+                out.append(add_vlan(build_frame(rng, k, l4, ihl=int(rng.integers(5, 16))), tags))
+    # truncated tags
+    f = add_vlan(build_frame(rng, "udp", 20), [(0x8100, 7), (0x8100, 8)])
+    for n in range(12, 26):
+        out.append(f[:n])
+    # IPv6 extension chains
+    chains = ([], [0], [60], [43], [44], [0, 60], [0, 43, 44], [0, 60, 43, 44], [0, 60, 43, 60, 44], [44, 44])
+    for exts in chains:
+        for l4k in ("udp", "tcp", "icmp6", "icmp", "none"):
+            for l4 in (0, 3, 8, 21, 64, 700):
+                out.append(ipv6_with_ext(rng, exts, l4k, l4))
+    for off in (1, 100, 8191):
+        out.append(ipv6_with_ext(rng, [0, 44], "udp", 40, frag_offset=off))
+    # long chains: the L4 header lands past the 128-B window
+    for _ in range(20):
+        exts = [int(x) for x in rng.choice([0, 43, 60], size=4)]
+        out.append(add_vlan(ipv6_with_ext(rng, exts, "tcp", int(rng.integers(20, 400))),
+                            [(0x8100, 9)] if rng.random() < 0.5 else []))
+    # truncated extension headers
+    g = ipv6_with_ext(rng, [0, 43, 60], "udp", 30)
+    for n in range(54, len(g) + 1, 3):
+        h = bytearray(g[:n])
+        out.append(bytes(h))
+    return out

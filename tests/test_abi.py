@@ -37,7 +37,7 @@ def test_exports_every_declared_symbol():
 
 
 def test_abi_version_and_strerror():
-    assert lp.lib.pnetgpu_abi_version() == lp.DEFS["PNETGPU_ABI_VERSION"] == 1
+    assert lp.lib.pnetgpu_abi_version() == lp.DEFS["PNETGPU_ABI_VERSION"] == 2
     for code in (0, -1, -2, -3, -4, -99):
         assert lp.lib.pnetgpu_strerror(code)
 
