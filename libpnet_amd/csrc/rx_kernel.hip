@@ -79,8 +79,7 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// ---- LDS byte access ---------------------------------------------------------
-__device__ __forceinline__ uint32_t ld8(const uint8_t* w, int p) { return w[p]; }
+// ---- LDS access --------------------------------------------------------------
 
 // 16 bytes of a run [p, p+16) of an LDS slot at any alignment, as 4 LE dwords.
 __device__ __forceinline__ uint4 lds_read16_unaligned(const uint8_t* slot, int p) {
