@@ -29,6 +29,9 @@
  *                             extra_data (util.rs:92-117), batched.
  *   pnetgpu_ipv6_checksum_slices  pnet_packet::util::ipv6_checksum with empty
  *                             extra_data (util.rs:125-150), batched.
+ *   pnetgpu_ipv4|ipv6_checksum_adv_slices  the same with extra_data: the
+ *                             udp|tcp::*_checksum_adv wrappers (udp.rs:45-56,115-126,
+ *                             tcp.rs:250-261,275-286).
  *
  * Semantics are bit-exact with the reference: every
  * checksum word and extracted field equals what the Rust code returns for the
@@ -203,6 +206,23 @@ int pnetgpu_ipv6_checksum_slices(pnetgpu_ctx* ctx, const uint8_t* data, uint64_t
                                  uint64_t n, const uint64_t* offsets, const uint32_t* lengths,
                                  const uint32_t* skipwords, const uint8_t* addrs,
                                  const uint8_t* protos, uint16_t* out, void* stream);
+
+/* The *_adv forms: util::ipv4_checksum / ipv6_checksum with a non-empty
+ * extra_data slice per item (udp|tcp::ipv4_checksum_adv / ipv6_checksum_adv,
+ * udp.rs:45-56,115-126, tcp.rs:250-261,275-286): extra slice i =
+ * data[extra_offsets[i], +extra_lengths[i]), summed from its own start; an
+ * odd-length extra drops its trailing byte (util.rs:114, udp.rs:42-44) while
+ * the pseudo-header length counts it. */
+int pnetgpu_ipv4_checksum_adv_slices(pnetgpu_ctx* ctx, const uint8_t* data, uint64_t data_bytes,
+                                     uint64_t n, const uint64_t* offsets, const uint32_t* lengths,
+                                     const uint32_t* skipwords, const uint64_t* extra_offsets,
+                                     const uint32_t* extra_lengths, const uint8_t* addrs,
+                                     const uint8_t* protos, uint16_t* out, void* stream);
+int pnetgpu_ipv6_checksum_adv_slices(pnetgpu_ctx* ctx, const uint8_t* data, uint64_t data_bytes,
+                                     uint64_t n, const uint64_t* offsets, const uint32_t* lengths,
+                                     const uint32_t* skipwords, const uint64_t* extra_offsets,
+                                     const uint32_t* extra_lengths, const uint8_t* addrs,
+                                     const uint8_t* protos, uint16_t* out, void* stream);
 
 #ifdef __cplusplus
 }

@@ -9,7 +9,7 @@ from ._lib import DEFS, LIB_PATH, PnetGpuError, lib  # noqa: F401  (fails loudly
 from . import synth  # noqa: F401
 from .ring import Ring, pcap_frames  # noqa: F401
 from .engine import (ALL_COLUMNS, COUNTER_NAMES, IPV4_COLUMNS, Context, RxResult,  # noqa: F401
-                     checksum_slices, column_bytes, context, ipv4_checksum_slices,
+                     checksum_adv_slices, checksum_slices, column_bytes, context, ipv4_checksum_slices,
                      ipv6_checksum_slices, rx_process, tx_fill_checksums)
 
 __version__ = "0.1.0"

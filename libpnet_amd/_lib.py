@@ -86,6 +86,9 @@ def _load():
     for f in (L.pnetgpu_ipv4_checksum_slices, L.pnetgpu_ipv6_checksum_slices):
         f.restype = i32
         f.argtypes = [vp, vp, u64, u64, vp, vp, vp, vp, vp, vp, vp]
+    for f in (L.pnetgpu_ipv4_checksum_adv_slices, L.pnetgpu_ipv6_checksum_adv_slices):
+        f.restype = i32
+        f.argtypes = [vp, vp, u64, u64, vp, vp, vp, vp, vp, vp, vp, vp, vp]
     L.pnetgpu_synth_layout.restype = i32
     L.pnetgpu_synth_layout.argtypes = [i32, u64, u64, ctypes.POINTER(u64), ctypes.POINTER(u32),
                                        ctypes.POINTER(u32)]

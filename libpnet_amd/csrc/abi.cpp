@@ -162,7 +162,8 @@ int pnetgpu_tx_fill_checksums(pnetgpu_ctx* ctx, const pnetgpu_batch* b, const pn
 static int slices_common(pnetgpu_ctx* ctx, const uint8_t* data, uint64_t data_bytes, uint64_t n,
                          const uint64_t* offsets, const uint32_t* lengths, const uint32_t* skipwords,
                          const uint8_t* addrs, const uint8_t* protos, uint16_t* out, int pseudo,
-                         void* stream) {
+                         void* stream, const uint64_t* extra_offsets = nullptr,
+                         const uint32_t* extra_lengths = nullptr) {
     if (!ctx) return PNETGPU_EINVAL;
     if (n == 0) return PNETGPU_OK;
     if (!data || !offsets || !lengths || !skipwords || !out) return PNETGPU_EINVAL;
@@ -177,6 +178,8 @@ static int slices_common(pnetgpu_ctx* ctx, const uint8_t* data, uint64_t data_by
     a.skipwords = skipwords;
     a.addrs = addrs;
     a.protos = protos;
+    a.extra_offsets = extra_offsets;
+    a.extra_lengths = extra_lengths;
     a.out = out;
     const uint64_t groups_per_block = kBlock / 16;
     const uint64_t want = (n + groups_per_block - 1) / groups_per_block;
@@ -206,6 +209,24 @@ int pnetgpu_ipv6_checksum_slices(pnetgpu_ctx* ctx, const uint8_t* data, uint64_t
                                  uint16_t* out, void* stream) {
     return slices_common(ctx, data, data_bytes, n, offsets, lengths, skipwords, addrs, protos, out, 16,
                          stream);
+}
+
+int pnetgpu_ipv4_checksum_adv_slices(pnetgpu_ctx* ctx, const uint8_t* data, uint64_t data_bytes, uint64_t n,
+                                     const uint64_t* offsets, const uint32_t* lengths, const uint32_t* skipwords,
+                                     const uint64_t* extra_offsets, const uint32_t* extra_lengths,
+                                     const uint8_t* addrs, const uint8_t* protos, uint16_t* out, void* stream) {
+    if (n && (!extra_offsets || !extra_lengths)) return PNETGPU_EINVAL;
+    return slices_common(ctx, data, data_bytes, n, offsets, lengths, skipwords, addrs, protos, out, 4, stream,
+                         extra_offsets, extra_lengths);
+}
+
+int pnetgpu_ipv6_checksum_adv_slices(pnetgpu_ctx* ctx, const uint8_t* data, uint64_t data_bytes, uint64_t n,
+                                     const uint64_t* offsets, const uint32_t* lengths, const uint32_t* skipwords,
+                                     const uint64_t* extra_offsets, const uint32_t* extra_lengths,
+                                     const uint8_t* addrs, const uint8_t* protos, uint16_t* out, void* stream) {
+    if (n && (!extra_offsets || !extra_lengths)) return PNETGPU_EINVAL;
+    return slices_common(ctx, data, data_bytes, n, offsets, lengths, skipwords, addrs, protos, out, 16, stream,
+                         extra_offsets, extra_lengths);
 }
 
 }  // extern "C"

@@ -34,6 +34,8 @@ struct SliceArgs {
     const uint32_t* skipwords;
     const uint8_t* addrs;
     const uint8_t* protos;
+    const uint64_t* extra_offsets;   // *_adv: extra_data slices (nullptr otherwise)
+    const uint32_t* extra_lengths;
     uint16_t* out;
 };
 

@@ -794,39 +794,61 @@ __global__ __launch_bounds__(kBlock, 4) void rx_kernel(RxArgs a) {
 // One group of 16 lanes per slice (4 slices per wave per step): coalesced
 // 16-B granules, masked sums, shuffle reduce, lane 0 of the group finalizes.
 // PSEUDO: 0 = util::checksum, 4 = ipv4_checksum, 16 = ipv6_checksum.
-template <int PSEUDO>
+// Weighted byte sum of [off, off+len) (absolute offsets into a.data) by one
+// 16-lane group: coalesced aligned granules, masked at both ends, shuffle-reduced
+// so every lane of the group returns the total.
+__device__ __forceinline__ uint32_t group_range_sum(const uint8_t* data, uint64_t off, uint32_t len, int j) {
+    constexpr int G = 16;
+    const int sh = (int)(off & 15);
+    const uint8_t* fb = data + (off - (uint64_t)sh);
+    const int e = sh + (int)len;
+    const uint32_t nneed = len ? (uint32_t)((e + 15) >> 4) : 0u;
+    uint32_t acc = 0;
+#pragma unroll 1
+    for (uint32_t c = j; c < nneed; c += G) {
+        const uint4 v = *reinterpret_cast<const uint4*>(fb + 16u * c);
+        const uint32_t dw[4] = {v.x, v.y, v.z, v.w};
+        const int p = (int)(16u * c);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const uint32_t mk = first_bytes(clamp04(e - p - 4 * t)) & ~first_bytes(clamp04(sh - p - 4 * t));
+            acc = sad(dw[t] & mk, acc);
+        }
+    }
+#pragma unroll
+    for (int o = G / 2; o >= 1; o >>= 1) acc += __shfl_xor(acc, o);
+    return acc;
+}
+
+// PSEUDO: 0 = util::checksum, 4 = util::ipv4_checksum, 16 = util::ipv6_checksum.
+// EXTRA: the *_checksum_adv form with an extra_data slice (util.rs:109-114).
+template <int PSEUDO, bool EXTRA>
 __global__ __launch_bounds__(kBlock) void slice_kernel(SliceArgs a) {
     constexpr int G = 16;
     const int lane = threadIdx.x & (kWave - 1);
     const int j = lane % G;
     const uint64_t gid = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) / G;
     const uint64_t ngroups = (uint64_t)gridDim.x * kBlock / G;
-    // groups are 16-lane aligned, so every shuffle below stays inside one group,
-    // whose lanes share i (and therefore control flow)
+    // groups are 16-lane aligned, so every shuffle stays inside one group, whose
+    // lanes share i (and therefore control flow)
     for (uint64_t i = gid; i < a.n; i += ngroups) {
-        uint64_t off = a.offsets[i] + a.delta;
+        const uint64_t off = a.offsets[i] + a.delta;
         uint32_t len = a.lengths[i];
         const uint32_t skip = a.skipwords[i];
-        const bool bad = off > a.limit || (uint64_t)len > a.limit - off;
-        if (bad) len = 0;
-        const int sh = (int)(off & 15);
-        const uint8_t* fb = a.data + (off - (uint64_t)sh);
-        const int e = sh + (int)len;
-        const uint32_t nneed = len ? (uint32_t)((e + 15) >> 4) : 0u;
-        uint32_t acc = 0;
-#pragma unroll 1
-        for (uint32_t c = j; c < nneed; c += G) {
-            const uint4 v = *reinterpret_cast<const uint4*>(fb + 16u * c);
-            const uint32_t dw[4] = {v.x, v.y, v.z, v.w};
-            const int p = (int)(16u * c);
-#pragma unroll
-            for (int t = 0; t < 4; ++t) {
-                const uint32_t mk = first_bytes(clamp04(e - p - 4 * t)) & ~first_bytes(clamp04(sh - p - 4 * t));
-                acc = sad(dw[t] & mk, acc);
-            }
+        if (off > a.limit || (uint64_t)len > a.limit - off) len = 0;
+        uint32_t acc = group_range_sum(a.data, off, len, j);
+        uint32_t pe = 0, elen = 0;
+        if (EXTRA) {
+            // sum_be_words(extra, extra.len() / 2): every whole word, never the odd
+            // trailing byte (util.rs:114; the quirk documented at udp.rs:42-44); the
+            // extra slice starts its own word alignment
+            const uint64_t eoff = a.extra_offsets[i] + a.delta;
+            elen = a.extra_lengths[i];
+            if (eoff > a.limit || (uint64_t)elen > a.limit - eoff) elen = 0;
+            const uint32_t te = group_range_sum(a.data, eoff, elen & ~1u, j);
+            pe = fold16(te);
+            if (!(eoff & 1)) pe = bswap16(pe);
         }
-#pragma unroll
-        for (int o = G / 2; o >= 1; o >>= 1) acc += __shfl_xor(acc, o);
         if (j == 0) {
             // skipped word: bytes [2*skip, 2*skip+2) of the slice that exist (util.rs:166-178)
             const uint8_t* sb = a.data + off;
@@ -849,7 +871,7 @@ __global__ __launch_bounds__(kBlock) void slice_kernel(SliceArgs a) {
                 uint32_t s = 0;
 #pragma unroll
                 for (int k = 0; k < 2 * PSEUDO; k += 2) s += ((uint32_t)ad[k] << 8) | ad[k + 1];
-                s += a.protos[i] + len + p;
+                s += a.protos[i] + len + elen + p + pe;     // util.rs:103-114
                 r = (~fold16(s)) & 0xFFFFu;
             }
             a.out[i] = (uint16_t)r;
@@ -916,9 +938,12 @@ int launch_rx(const RxArgs& args, int kind, int g, int blocks, bool tx, hipStrea
 }
 
 int launch_slices(const SliceArgs& args, int pseudo, int blocks, hipStream_t stream) {
-    if (pseudo == 0) hipLaunchKernelGGL(slice_kernel<0>, dim3(blocks), dim3(kBlock), 0, stream, args);
-    else if (pseudo == 4) hipLaunchKernelGGL(slice_kernel<4>, dim3(blocks), dim3(kBlock), 0, stream, args);
-    else hipLaunchKernelGGL(slice_kernel<16>, dim3(blocks), dim3(kBlock), 0, stream, args);
+    const bool extra = args.extra_offsets != nullptr;
+    if (pseudo == 0) hipLaunchKernelGGL((slice_kernel<0, false>), dim3(blocks), dim3(kBlock), 0, stream, args);
+    else if (pseudo == 4 && !extra) hipLaunchKernelGGL((slice_kernel<4, false>), dim3(blocks), dim3(kBlock), 0, stream, args);
+    else if (pseudo == 4) hipLaunchKernelGGL((slice_kernel<4, true>), dim3(blocks), dim3(kBlock), 0, stream, args);
+    else if (!extra) hipLaunchKernelGGL((slice_kernel<16, false>), dim3(blocks), dim3(kBlock), 0, stream, args);
+    else hipLaunchKernelGGL((slice_kernel<16, true>), dim3(blocks), dim3(kBlock), 0, stream, args);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -212,6 +212,21 @@ def ipv4_checksum_slices(data, offsets, lengths, skipwords, addrs, protos, strea
     return _slices("pnetgpu_ipv4_checksum_slices", data, offsets, lengths, skipwords, addrs, protos, stream)
 
 
+def checksum_adv_slices(version, data, offsets, lengths, skipwords, extra_offsets, extra_lengths, addrs, protos,
+                        stream=None):
+    """util::ipv4_checksum / ipv6_checksum with extra_data (the *_checksum_adv wrappers):
+    version 4 (addrs [n, 8]) or 6 (addrs [n, 32])."""
+    _check_u8_cuda(data, "data")
+    n = offsets.numel()
+    out = torch.empty(n, dtype=torch.int16, device=data.device)
+    ctx = context(data.device.index)
+    fn = "pnetgpu_ipv4_checksum_adv_slices" if version == 4 else "pnetgpu_ipv6_checksum_adv_slices"
+    check(getattr(lib, fn)(ctx.handle, _ptr(data), data.numel(), n, _ptr(offsets), _ptr(lengths), _ptr(skipwords),
+                           _ptr(extra_offsets), _ptr(extra_lengths), _ptr(addrs), _ptr(protos), _ptr(out),
+                           _stream_handle(stream, data.device)), fn)
+    return out
+
+
 def ipv6_checksum_slices(data, offsets, lengths, skipwords, addrs, protos, stream=None):
     """util::ipv6_checksum per slice; addrs uint8 [n, 32] (src||dst), protos uint8 [n]."""
     return _slices("pnetgpu_ipv6_checksum_slices", data, offsets, lengths, skipwords, addrs, protos, stream)

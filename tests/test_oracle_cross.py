@@ -38,3 +38,23 @@ def test_batch_threads_and_invalid_desc():
     offs2[5] = buf.size + 1
     c = coracle.rx_batch(buf, len(frames), offsets=offs2, lengths=lens)
     assert c["status"][5] == pyoracle.ST_DESC_INVALID
+
+
+def test_checksum_adv_extra_data():
+    """util::ipv4/ipv6_checksum with non-empty extra_data (the udp|tcp
+    *_checksum_adv wrappers, udp.rs:45-56, tcp.rs:250-261): C vs Python, and the
+    odd-length quirk of util.rs:114 — the extra's trailing byte never enters the
+    sum, but it does count in the pseudo-header length."""
+    rng = np.random.default_rng(11)
+    for alen, cfn in ((4, coracle.ipv4_checksum), (16, coracle.ipv6_checksum)):
+        for _ in range(300):
+            d = rng.integers(0, 256, int(rng.integers(0, 90)), dtype=np.uint8).tobytes()
+            e = rng.integers(0, 256, int(rng.integers(0, 40)), dtype=np.uint8).tobytes()
+            src = rng.integers(0, 256, alen, dtype=np.uint8).tobytes()
+            dst = rng.integers(0, 256, alen, dtype=np.uint8).tobytes()
+            skip, proto = int(rng.integers(0, 50)), int(rng.integers(0, 256))
+            want = pyoracle.ipv4_checksum(d, skip, e, src, dst, proto)
+            assert cfn(d, skip, e, src, dst, proto) == want
+            if len(e) % 2:
+                flipped = e[:-1] + bytes([e[-1] ^ 0xFF])
+                assert cfn(d, skip, flipped, src, dst, proto) == want
