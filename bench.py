@@ -126,7 +126,19 @@ def cpu_baseline(sh, budget_cpu_s=12.0):
         if el * nthreads >= budget_cpu_s or el > 30:
             break
     mpps = frames / el / 1e6
+    # the same restatement on one core, short sample
+    n1, f1, t1 = min(n, 1 << 17), 0, time.perf_counter()
+    while True:
+        if w.stride:
+            coracle.rx_batch(w.buf, n1, stride=w.stride, frame_len=w.frame_len, nthreads=1)
+        else:
+            coracle.rx_batch(w.buf, n1, offsets=w.offsets[:n1], lengths=w.lengths[:n1], nthreads=1)
+        f1 += n1
+        e1 = time.perf_counter() - t1
+        if e1 >= 3.0:
+            break
     return {"value": round(mpps, 2), "unit": "Mpkts/s", "cores": nthreads, "kind": "port",
+            "value_1core": round(f1 / e1 / 1e6, 2),
             "gbps": round(frames * (w.expect["bytes"] / sh.n) / el / 1e9, 2),
             "sample": f"first {n} frames of the same {sh.name} batch x{reps} passes ({el:.1f} s wall, "
                       f"{nthreads} threads, oracle/pnet_oracle.c scalar per-frame restatement)"}

@@ -115,9 +115,10 @@ static int rx_common(pnetgpu_ctx* ctx, const pnetgpu_batch* b, const pnetgpu_rx_
     a.flags = b->flags;
 
     // Kernel choice. Small: fixed stride, every frame 16-B aligned, at most 64 B,
-    // inside the buffer (the 64-B configs). Generic otherwise; its tail group
-    // width G follows the typical frame size.
-    int kind = pnetgpu::kKindGeneric, g = 8;
+    // inside the buffer (the 64-B configs). Otherwise rx_kernel with the tail
+    // shape of the batch's frame sizes: MTU or jumbo for fixed stride, mixed for
+    // descriptor batches (their lengths are device-resident).
+    int kind = pnetgpu::kKindMixed;
     if (b->stride) {
         const uint64_t base_sh = (a.delta + b->first_offset) & 15u;
         const uint64_t last_end = a.delta + b->first_offset + (b->n_frames - 1) * (uint64_t)b->stride + b->frame_len;
@@ -125,14 +126,17 @@ static int rx_common(pnetgpu_ctx* ctx, const pnetgpu_batch* b, const pnetgpu_rx_
                           last_end <= a.limit;
         if (base_sh == 0 && b->stride % 16 == 0 && b->frame_len <= 64 && fits && b->flags == 0)
             kind = pnetgpu::kKindSmall;
-        if (b->frame_len >= 4096) g = 64;
+        else
+            kind = b->frame_len >= 4096 ? pnetgpu::kKindJumbo : pnetgpu::kKindMtu;
     }
-    if (const char* e = std::getenv("PNETGPU_TAIL_GROUP")) {      // tuning override
+    if (const char* e = std::getenv("PNETGPU_RX_KIND")) {          // tuning override (not the small kernel)
         const int v = std::atoi(e);
-        if (v == 8 || v == 16 || v == 64) g = v;
+        if ((v == pnetgpu::kKindMixed || v == pnetgpu::kKindMtu || v == pnetgpu::kKindJumbo) &&
+            kind != pnetgpu::kKindSmall)
+            kind = v;
     }
     int numregs = 0, lds = 0;
-    int per_cu = pnetgpu::rx_blocks_per_cu(kind, g, &numregs, &lds);
+    int per_cu = pnetgpu::rx_blocks_per_cu(kind, &numregs, &lds);
     if (per_cu <= 0) return PNETGPU_EHIP;
     if (const char* e = std::getenv("PNETGPU_BLOCKS_PER_CU")) {   // tuning override
         const int v = std::atoi(e);
@@ -140,13 +144,13 @@ static int rx_common(pnetgpu_ctx* ctx, const pnetgpu_batch* b, const pnetgpu_rx_
     }
     if (const char* e = std::getenv("PNETGPU_DEBUG")) {
         if (*e == '1')
-            std::fprintf(stderr, "[pnetgpu] rx kind=%d g=%d regs=%d lds=%d blocks/cu=%d cus=%d\n", kind, g, numregs,
-                         lds, per_cu, ctx->cus);
+            std::fprintf(stderr, "[pnetgpu] rx kind=%d regs=%d lds=%d blocks/cu=%d cus=%d\n", kind, numregs, lds,
+                         per_cu, ctx->cus);
     }
     const uint64_t want = (a.nruns + kWavesPerBlock - 1) / kWavesPerBlock;
     const uint64_t cap = (uint64_t)ctx->cus * (uint64_t)per_cu;
     const int blocks = (int)std::max<uint64_t>(1, std::min(want, cap));
-    if (pnetgpu::launch_rx(a, kind, g, blocks, tx, static_cast<hipStream_t>(stream)) != 0) return PNETGPU_EHIP;
+    if (pnetgpu::launch_rx(a, kind, blocks, tx, static_cast<hipStream_t>(stream)) != 0) return PNETGPU_EHIP;
     return PNETGPU_OK;
 }
 

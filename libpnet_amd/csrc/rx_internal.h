@@ -41,14 +41,18 @@ struct SliceArgs {
 
 // Kernel kinds: the register-resident small-frame kernel (fixed stride, frames
 // 16-B aligned, span <= 64 B, every descriptor valid) or the generic one.
+// kernel kinds: rx_small_kernel, or rx_kernel with the tail shape for
+// descriptor batches (mixed sizes), MTU-size and jumbo fixed-stride frames
+constexpr int kKindMixed = 0;
 constexpr int kKindSmall = 1;
-constexpr int kKindGeneric = 0;
+constexpr int kKindMtu = 2;
+constexpr int kKindJumbo = 3;
 
 // device index a context is bound to (abi.cpp)
 int ctx_device(const pnetgpu_ctx* ctx);
 
-int rx_blocks_per_cu(int kind, int g, int* numregs, int* lds);
-int launch_rx(const RxArgs& args, int kind, int g, int blocks, bool tx, hipStream_t stream);
+int rx_blocks_per_cu(int kind, int* numregs, int* lds);
+int launch_rx(const RxArgs& args, int kind, int blocks, bool tx, hipStream_t stream);
 int launch_slices(const SliceArgs& args, int pseudo, int blocks, hipStream_t stream);
 
 }  // namespace pnetgpu

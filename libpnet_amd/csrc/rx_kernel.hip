@@ -627,19 +627,111 @@ struct WaveLds {
     static constexpr int kSlot = NW * 16 + 4;   // +4 B pad: conflict-free parse reads
     uint8_t win[kWave * kSlot];
     uint64_t base[kWave];     // aligned byte offset of granule 0 of each frame
-    uint32_t end[kWave];      // slot-relative end of the summed range B
-    uint32_t start[kWave];    // slot-relative start of B's part past the window
-    uint32_t tail[kWave];     // tail-phase partial sum per frame
-    uint8_t list[kWave];      // frames with a tail, in lane order
+    uint32_t end[kWave];      // window granules to load; then slot-relative frame end
+    uint32_t tail[kWave];     // weighted sum of the frame's bytes past the window
+    uint8_t list[kWave];      // frames with bytes past the window, in lane order
 };
 
-template <int NW, int G, int U, bool NT, bool TX>
+// Weighted sum of slot bytes [lo, hi) of a frame whose granule 0 is at fb, read
+// from memory by one lane (the rare correction when the L4 range does not run
+// from the window to the end of the frame).
+__device__ __forceinline__ uint32_t lane_range_sum(const uint8_t* fb, int lo, int hi) {
+    uint32_t acc = 0;
+#pragma unroll 1
+    for (int c = lo >> 4; 16 * c < hi; ++c) {
+        const uint4 v = load16(fb + 16 * c);
+        const uint32_t dw[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int p = 16 * c + 4 * t;
+            acc = sad(dw[t] & first_bytes(clamp04(hi - p)) & ~first_bytes(clamp04(lo - p)), acc);
+        }
+    }
+    return acc;
+}
+
+// The speculative tail: every byte of every frame past its window,
+// [kWin, end), summed before the parse by groups of G lanes that stream
+// coalesced granules (U loads in flight per lane); a group takes the next frame
+// of the wave's list as soon as it finishes one. Sums land in L.tail.
+// UNI (unified): the group streams the whole frame from granule 0 and writes
+// granules 0..NW-1 into the frame's LDS slot itself (zeros past the frame's
+// span) instead of a separate window phase: one pass per frame, so the line
+// holding the window/tail boundary and the line shared with the next frame are
+// fetched once, while they are still in L2 (the windows-first order read ~15 %
+// more than the frame bytes on MTU frames: TCC_EA0_RDREQ, profiles/).
+template <int NW, int G, int U, bool NT, bool UNI>
+__device__ __forceinline__ void tail_sums(const uint8_t* data, WaveLds<NW>& L, int lane, int count) {
+    constexpr int kGroups = kWave / G;
+    constexpr int kSlot = WaveLds<NW>::kSlot;
+    constexpr uint32_t c_first = UNI ? 0u : (uint32_t)NW;
+    static_assert(!UNI || G * U >= NW, "the first round must cover the window");
+    const int j = lane % G;
+    int idx = lane / G;
+    int fl = 0;
+    uint32_t fe = 0, nneed = 0, c0 = 0, acc = 0;
+    const uint8_t* fb = data;
+    if (idx < count) {
+        fl = L.list[idx];
+        fe = L.end[fl];
+        fb = data + L.base[fl];
+        nneed = (fe + 15u) >> 4;
+        c0 = c_first + j;
+    }
+    while (__ballot(idx < count)) {
+        if (idx < count) {
+            uint4 v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t c = c0 + u * G;
+                v[u] = c < nneed ? (NT ? load16_nt(fb + 16u * c) : load16(fb + 16u * c)) : make_uint4(0, 0, 0, 0);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t c = c0 + u * G;
+                uint32_t x = v[u].x, y = v[u].y, z = v[u].z, w = v[u].w;
+                if (UNI && c < (uint32_t)NW) {                   // window granule -> the frame's slot
+                    uint32_t* dst = reinterpret_cast<uint32_t*>(L.win + fl * kSlot + 16 * c);
+                    dst[0] = x; dst[1] = y; dst[2] = z; dst[3] = w;
+                    continue;
+                }
+                const int hi = (int)fe - (int)(16u * c);
+                if (hi < 16) {                                   // the frame's last granule
+                    x &= first_bytes(clamp04(hi));
+                    y &= first_bytes(clamp04(hi - 4));
+                    z &= first_bytes(clamp04(hi - 8));
+                    w &= first_bytes(clamp04(hi - 12));
+                }
+                acc = sad(x, acc);
+                acc = sad(y, acc);
+                acc = sad(z, acc);
+                acc = sad(w, acc);
+            }
+            c0 += U * G;
+            if (c0 - j >= (nneed > c_first ? nneed : c_first + 1u)) {   // group-uniform: frame done
+#pragma unroll
+                for (int o = G / 2; o >= 1; o >>= 1) acc += __shfl_xor(acc, o);
+                if (j == 0) L.tail[fl] = acc;
+                acc = 0;
+                idx += kGroups;
+                if (idx < count) {
+                    fl = L.list[idx];
+                    fe = L.end[fl];
+                    fb = data + L.base[fl];
+                    nneed = (fe + 15u) >> 4;
+                    c0 = c_first + j;
+                }
+            }
+        }
+    }
+}
+
+template <int NW, int G, int U, bool NT, bool UNI, bool TX>
 __global__ __launch_bounds__(kBlock, 4) void rx_kernel(RxArgs a) {
     static_assert(NW == 8, "window granules");
     static_assert(G == 4 || G == 8 || G == 16 || G == 32 || G == 64, "tail group");
     constexpr int kSlot = WaveLds<NW>::kSlot;
     constexpr int kWin = NW * 16;
-    constexpr int kGroups = kWave / G;
 
     __shared__ WaveLds<NW> lds_all[kWavesPerBlock];
     __shared__ uint64_t blk_ctr[kWavesPerBlock][PNETGPU_NCOUNTERS];
@@ -651,6 +743,18 @@ __global__ __launch_bounds__(kBlock, 4) void rx_kernel(RxArgs a) {
     Counters K;
 
     const uint64_t wave_stride = (uint64_t)gridDim.x * kWavesPerBlock;
+    // descriptor-mode offset/length of this lane's frame, loaded one run ahead
+    // so the descriptor round trip overlaps the previous run
+    uint64_t d_off = 0;
+    uint32_t d_len = 0;
+    auto fetch_desc = [&](uint64_t r) {
+        const uint64_t fr = r * kWave + lane;
+        if (!a.stride && r < a.nruns && fr < a.n) {
+            d_off = a.offsets[fr];
+            d_len = a.lengths[fr];
+        }
+    };
+    fetch_desc((uint64_t)blockIdx.x * kWavesPerBlock + wv);
     for (uint64_t run = (uint64_t)blockIdx.x * kWavesPerBlock + wv; run < a.nruns; run += wave_stride) {
         // ---- 1. descriptor -------------------------------------------------
         const uint64_t f0 = run * kWave;
@@ -663,8 +767,8 @@ __global__ __launch_bounds__(kBlock, 4) void rx_kernel(RxArgs a) {
                 off = a.first + f * a.stride;
                 len = a.frame_len;
             } else {
-                off = a.offsets[f];
-                len = a.lengths[f];
+                off = d_off;
+                len = d_len;
             }
             off += a.delta;
         }
@@ -672,31 +776,53 @@ __global__ __launch_bounds__(kBlock, 4) void rx_kernel(RxArgs a) {
         if (!in_batch || desc_bad) len = 0;
         const int sh = (int)(off & 15);
         const uint64_t base = off - (uint64_t)sh;
-        const uint32_t span = len ? (uint32_t)((sh + (uint64_t)len + 15) >> 4) : 0u;
+        const uint32_t fend = (uint32_t)sh + len;            // slot-relative end of the frame
+        const uint32_t span = (fend + 15u) >> 4;
         L.base[lane] = base;
         L.end[lane] = span < (uint32_t)NW ? span : (uint32_t)NW;   // granules to load into the window
         wave_sync();
 
         // ---- 2. window: NW*64 granule loads, all in flight before any store --
-        uint4 g[NW];
+        if (!UNI) {
+            uint4 g[NW];
 #pragma unroll
-        for (int i = 0; i < NW; ++i) {
-            const int q = i * kWave + lane;
-            const int fl = q / NW, c = q % NW;
-            g[i] = make_uint4(0, 0, 0, 0);
-            if ((uint32_t)c < L.end[fl])
-                g[i] = load16(a.data + L.base[fl] + 16u * c);
+            for (int i = 0; i < NW; ++i) {
+                const int q = i * kWave + lane;
+                const int fl = q / NW, c = q % NW;
+                g[i] = make_uint4(0, 0, 0, 0);
+                if ((uint32_t)c < L.end[fl])
+                    g[i] = load16(a.data + L.base[fl] + 16u * c);
+            }
+            fetch_desc(run + wave_stride);
+#pragma unroll
+            for (int i = 0; i < NW; ++i) {
+                const int q = i * kWave + lane;
+                const int fl = q / NW, c = q % NW;
+                uint32_t* dst = reinterpret_cast<uint32_t*>(L.win + fl * kSlot + 16 * c);
+                dst[0] = g[i].x; dst[1] = g[i].y; dst[2] = g[i].z; dst[3] = g[i].w;
+            }
+        } else {
+            fetch_desc(run + wave_stride);
         }
-#pragma unroll
-        for (int i = 0; i < NW; ++i) {
-            const int q = i * kWave + lane;
-            const int fl = q / NW, c = q % NW;
-            uint32_t* dst = reinterpret_cast<uint32_t*>(L.win + fl * kSlot + 16 * c);
-            dst[0] = g[i].x; dst[1] = g[i].y; dst[2] = g[i].z; dst[3] = g[i].w;
+
+        // ---- 3. speculative tail: all frame bytes past the window ----------
+        // Summed before the parse (no parse state is live, so more loads fit in
+        // flight); the parse then trims it to the L4 range B, which in every
+        // well-formed frame already runs to the end of the frame. UNI: every
+        // frame goes through the group loop, which also fills its window.
+        const bool has_tail = UNI ? in_batch : fend > (uint32_t)kWin;
+        const uint64_t tmask = __ballot(has_tail);
+        if (tmask) {
+            if (has_tail) {
+                L.list[__popcll(tmask & ((1ull << lane) - 1ull))] = (uint8_t)lane;
+                L.end[lane] = fend;
+            }
+            wave_sync();
+            tail_sums<NW, G, U, NT, UNI>(a.data, L, lane, __popcll(tmask));
         }
         wave_sync();
 
-        // ---- 3. parse + window sums (lane l <-> frame l) -------------------
+        // ---- 4. parse + window sums (lane l <-> frame l) -------------------
         Parsed P{};
         if (desc_bad) P.st = PNET_ST_DESC_INVALID;
         else if (in_batch)
@@ -705,77 +831,12 @@ __global__ __launch_bounds__(kBlock, 4) void rx_kernel(RxArgs a) {
         const int p0 = P.a_lo + sh, p1 = P.a_hi + sh, p2 = P.b_lo + sh, p3 = P.b_hi + sh;
         uint32_t tA = 0, tB = 0;
         window_sums(slot, p0, p1, min(p2, kWin), min(p3, kWin), tA, tB);
-
-        // ---- 4. tail: B bytes past the window, via a per-wave work list ------
-        const bool has_tail = p3 > kWin;
-        const uint64_t tmask = __ballot(has_tail);
-        if (tmask) {
-            const int count = __popcll(tmask);
-            if (has_tail) {
-                const int pos = __popcll(tmask & ((1ull << lane) - 1ull));
-                L.list[pos] = (uint8_t)lane;
-                L.end[lane] = (uint32_t)p3;
-                L.start[lane] = (uint32_t)max(p2, kWin);
-            }
-            wave_sync();
-            const int grp = lane / G, j = lane % G;
-            int idx = grp;
-            int fl = 0;
-            uint32_t fs = 0, fe = 0, nneed = 0, c0 = 0, acc = 0;
-            const uint8_t* fb = a.data;
-            if (idx < count) {
-                fl = L.list[idx];
-                fs = L.start[fl];
-                fe = L.end[fl];
-                fb = a.data + L.base[fl];
-                nneed = (fe + 15u) >> 4;
-                c0 = (fs >> 4) + j;
-            }
-            while (__ballot(idx < count)) {
-                if (idx < count) {
-                    uint4 v[U];
-#pragma unroll
-                    for (int u = 0; u < U; ++u) {
-                        const uint32_t c = c0 + u * G;
-                        v[u] = c < nneed ? (NT ? load16_nt(fb + 16u * c) : load16(fb + 16u * c))
-                                         : make_uint4(0, 0, 0, 0);
-                    }
-#pragma unroll
-                    for (int u = 0; u < U; ++u) {
-                        const uint32_t c = c0 + u * G;
-                        uint32_t x = v[u].x, y = v[u].y, z = v[u].z, w = v[u].w;
-                        const int hi = (int)fe - (int)(16u * c), lo = (int)fs - (int)(16u * c);
-                        if (hi < 16 || lo > 0) {               // granule straddles an end of B
-                            x &= first_bytes(clamp04(hi)) & ~first_bytes(clamp04(lo));
-                            y &= first_bytes(clamp04(hi - 4)) & ~first_bytes(clamp04(lo - 4));
-                            z &= first_bytes(clamp04(hi - 8)) & ~first_bytes(clamp04(lo - 8));
-                            w &= first_bytes(clamp04(hi - 12)) & ~first_bytes(clamp04(lo - 12));
-                        }
-                        acc = sad(x, acc);
-                        acc = sad(y, acc);
-                        acc = sad(z, acc);
-                        acc = sad(w, acc);
-                    }
-                    c0 += U * G;
-                    if (c0 - j >= nneed) {                      // group-uniform: frame done
-#pragma unroll
-                        for (int o = G / 2; o >= 1; o >>= 1) acc += __shfl_xor(acc, o);
-                        if (j == 0) L.tail[fl] = acc;
-                        acc = 0;
-                        idx += kGroups;
-                        if (idx < count) {
-                            fl = L.list[idx];
-                            fs = L.start[fl];
-                            fe = L.end[fl];
-                            fb = a.data + L.base[fl];
-                            nneed = (fe + 15u) >> 4;
-                            c0 = (fs >> 4) + j;
-                        }
-                    }
-                }
-            }
-            wave_sync();
-            if (has_tail) tB += L.tail[lane];
+        if (P.l4do && p3 > kWin) {
+            // B past the window = the speculative tail minus [kWin, p2) and [p3, fend)
+            tB += L.tail[lane];
+            const uint8_t* fb = a.data + base;
+            if (p2 > kWin) tB -= lane_range_sum(fb, kWin, p2);
+            if ((uint32_t)p3 < fend) tB -= lane_range_sum(fb, p3, (int)fend);
         }
 
         // ---- 5. finalize + stores ------------------------------------------
@@ -793,7 +854,7 @@ __global__ __launch_bounds__(kBlock, 4) void rx_kernel(RxArgs a) {
 // Batched util::checksum / ipv4_checksum / ipv6_checksum over slices.
 // One group of 16 lanes per slice (4 slices per wave per step): coalesced
 // 16-B granules, masked sums, shuffle reduce, lane 0 of the group finalizes.
-// PSEUDO: 0 = util::checksum, 4 = ipv4_checksum, 16 = ipv6_checksum.
+
 // Weighted byte sum of [off, off+len) (absolute offsets into a.data) by one
 // 16-lane group: coalesced aligned granules, masked at both ends, shuffle-reduced
 // so every lane of the group returns the total.
@@ -893,36 +954,53 @@ static int resident_blocks(const void* fn) {
     return nb > 0 ? nb : 1;
 }
 
-template <int G, bool TX>
-const void* rx_fn() {
-    return reinterpret_cast<const void*>(rx_kernel<8, G, 4, (G >= 64), TX>);
+// Tail shapes per kernel kind: <G lanes per frame, U loads in flight per lane,
+// non-temporal loads, unified window+tail pass>, from same-box A/B runs on
+// MI355X (tools/abvar.sh): descriptor batches of mixed sizes want narrow groups
+// and deep loads; MTU frames 8-lane groups streaming each whole frame once
+// (unified: -6 % time); jumbo frames the whole wave on one frame, 9 KiB in
+// flight per round (one round per 9000-B frame), non-temporal.
+#ifndef PNET_MIXED_CFG
+#define PNET_MIXED_CFG 4, 8, false, false
+#endif
+#ifndef PNET_MTU_CFG
+#define PNET_MTU_CFG 8, 4, false, true
+#endif
+#ifndef PNET_JUMBO_CFG
+#define PNET_JUMBO_CFG 64, 9, true, false
+#endif
+
+template <bool TX>
+const void* pick_fn(int kind) {
+    switch (kind) {
+    case kKindSmall: return reinterpret_cast<const void*>(rx_small_kernel<TX>);
+    case kKindMtu: return reinterpret_cast<const void*>(rx_kernel<8, PNET_MTU_CFG, TX>);
+    case kKindJumbo: return reinterpret_cast<const void*>(rx_kernel<8, PNET_JUMBO_CFG, TX>);
+    default: return reinterpret_cast<const void*>(rx_kernel<8, PNET_MIXED_CFG, TX>);
+    }
 }
 
 template <bool TX>
-const void* pick_fn(int kind, int g) {
-    return kind == kKindSmall ? reinterpret_cast<const void*>(rx_small_kernel<TX>)
-           : g == 64          ? rx_fn<64, TX>()
-           : g == 16          ? rx_fn<16, TX>()
-                              : rx_fn<8, TX>();
-}
-
-template <bool TX>
-void launch_t(const RxArgs& args, int kind, int g, int blocks, hipStream_t stream) {
-    if (kind == kKindSmall) {
+void launch_t(const RxArgs& args, int kind, int blocks, hipStream_t stream) {
+    switch (kind) {
+    case kKindSmall:
         hipLaunchKernelGGL(rx_small_kernel<TX>, dim3(blocks), dim3(kBlock), 0, stream, args);
-    } else if (g == 64) {
-        hipLaunchKernelGGL((rx_kernel<8, 64, 4, true, TX>), dim3(blocks), dim3(kBlock), 0, stream, args);
-    } else if (g == 16) {
-        hipLaunchKernelGGL((rx_kernel<8, 16, 4, false, TX>), dim3(blocks), dim3(kBlock), 0, stream, args);
-    } else {
-        hipLaunchKernelGGL((rx_kernel<8, 8, 4, false, TX>), dim3(blocks), dim3(kBlock), 0, stream, args);
+        break;
+    case kKindMtu:
+        hipLaunchKernelGGL((rx_kernel<8, PNET_MTU_CFG, TX>), dim3(blocks), dim3(kBlock), 0, stream, args);
+        break;
+    case kKindJumbo:
+        hipLaunchKernelGGL((rx_kernel<8, PNET_JUMBO_CFG, TX>), dim3(blocks), dim3(kBlock), 0, stream, args);
+        break;
+    default:
+        hipLaunchKernelGGL((rx_kernel<8, PNET_MIXED_CFG, TX>), dim3(blocks), dim3(kBlock), 0, stream, args);
     }
 }
 
 }  // namespace
 
-int rx_blocks_per_cu(int kind, int g, int* numregs, int* lds) {
-    const void* fn = pick_fn<false>(kind, g);
+int rx_blocks_per_cu(int kind, int* numregs, int* lds) {
+    const void* fn = pick_fn<false>(kind);
     hipFuncAttributes fa;
     if (hipFuncGetAttributes(&fa, fn) == hipSuccess) {
         if (numregs) *numregs = fa.numRegs;
@@ -931,9 +1009,9 @@ int rx_blocks_per_cu(int kind, int g, int* numregs, int* lds) {
     return resident_blocks(fn);
 }
 
-int launch_rx(const RxArgs& args, int kind, int g, int blocks, bool tx, hipStream_t stream) {
-    if (tx) launch_t<true>(args, kind, g, blocks, stream);
-    else launch_t<false>(args, kind, g, blocks, stream);
+int launch_rx(const RxArgs& args, int kind, int blocks, bool tx, hipStream_t stream) {
+    if (tx) launch_t<true>(args, kind, blocks, stream);
+    else launch_t<false>(args, kind, blocks, stream);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

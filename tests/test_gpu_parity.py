@@ -194,6 +194,36 @@ def test_stride_mode_odd_stride_and_offset():
         compare(res, rec)
 
 
+@pytest.mark.parametrize("stride,flen", [(144, 144), (150, 97), (333, 333), (1500, 1500), (1514, 1400),
+                                         (4000, 3999), (9018, 9018)])
+def test_stride_mode_random_frames_every_kernel(stride, flen, monkeypatch):
+    """Fixed-stride batches of random/malformed frames (garbage between frames,
+    L4 ranges shorter than the frame, IPv4 options, IPv6) at every first-offset
+    alignment: the streaming kernel (chosen by default for these strides) and
+    the per-frame kernel kinds (forced through PNETGPU_RX_KIND) all bit-exact."""
+    rng = np.random.default_rng(stride + flen)
+    n = 700
+    frames = framegen.random_frames(rng, n, max_len=min(stride + 64, 9100))
+    for first in (0, 5, 12):
+        buf = rng.integers(0, 256, first + stride * n + 64, dtype=np.uint8)
+        for i, f in enumerate(frames):
+            f = np.frombuffer(f, np.uint8)[:stride]
+            buf[first + i * stride:first + i * stride + len(f)] = f
+        rec = coracle.rx_batch(buf, n, first=first, stride=stride, frame_len=flen, nthreads=NTHREADS)
+        d = to_dev(buf)
+        for kind in (None, "0", "2", "3"):
+            if kind is None:
+                monkeypatch.delenv("PNETGPU_RX_KIND", raising=False)
+            else:
+                monkeypatch.setenv("PNETGPU_RX_KIND", kind)
+            res = lp.rx_process(d, stride=stride, frame_len=flen, first_offset=first, n_frames=n,
+                                columns=ALL_COLUMNS)
+            torch.cuda.synchronize()
+            compare(res, rec)
+            lens = np.full(n, flen, np.uint32)
+            assert res.counter_dict() == oracle_counters(rec, lens), (first, kind)
+
+
 # ---- BASELINE workloads at full per-GPU size -------------------------------
 
 FULL = {"udp64": 1 << 24, "tcp1500": 1 << 20, "imix": 1 << 22, "udp6_jumbo": 1 << 17}

@@ -69,6 +69,29 @@ __global__ __launch_bounds__(256) void read_rec_kernel(const uint4* __restrict__
     }
 }
 
+// each wave streams whole contiguous chunks of U*R KiB: R rounds of U 1-KiB
+// wave loads (U in flight); chunks handed out round-robin over the waves
+template <int U, int R>
+__global__ __launch_bounds__(256) void read_chunk_kernel(const uint4* __restrict__ in, size_t n16, uint32_t* out) {
+    const int lane = threadIdx.x & 63;
+    const size_t wave = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const size_t nwaves = ((size_t)gridDim.x * blockDim.x) >> 6;
+    constexpr size_t kChunk = (size_t)U * R * 64;   // uint4 per chunk
+    uint32_t acc = 0;
+    for (size_t ch = wave; (ch + 1) * kChunk <= n16; ch += nwaves) {
+        const uint4* p = in + ch * kChunk + lane;
+#pragma unroll 1
+        for (int r = 0; r < R; ++r) {
+            uint4 v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) v[u] = p[(r * U + u) * 64];
+#pragma unroll
+            for (int u = 0; u < U; ++u) acc += v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+        }
+    }
+    if (acc == 0x12345678u) out[0] = acc;
+}
+
 __global__ __launch_bounds__(256) void copy_kernel(const uint4* __restrict__ in, uint4* __restrict__ out, size_t n16) {
     const size_t stride = (size_t)gridDim.x * blockDim.x;
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += stride) out[i] = in[i];
@@ -103,6 +126,11 @@ int main() {
         printf("read    nt    U4 grid=%5d: %7.1f us  %6.0f GB/s\n", grid, ms * 1e3, bytes / ms / 1e6);
         ms = time_it([&] { read_kernel<8, false><<<grid, 256>>>(in, n16, o); }, 20);
         printf("read    plain U8 grid=%5d: %7.1f us  %6.0f GB/s\n", grid, ms * 1e3, bytes / ms / 1e6);
+#define CHUNK(U, R)                                                                                   \
+        ms = time_it([&] { read_chunk_kernel<U, R><<<grid, 256>>>(in, n16, o); }, 20);                    \
+        printf("read    chunk U%-2d R%d (%3d KiB) grid=%5d: %7.1f us  %6.0f GB/s\n", U, R, U * R, grid, ms * 1e3, \
+               bytes / ms / 1e6);
+        CHUNK(4, 1) CHUNK(8, 1) CHUNK(12, 1) CHUNK(16, 1) CHUNK(4, 4) CHUNK(8, 4) CHUNK(12, 4) CHUNK(16, 4) CHUNK(8, 16)
         ms = time_it([&] { read_cols_kernel<<<grid, 256>>>(in, nframes, c16, c32, c8); }, 20);
         printf("read+26B cols  grid=%5d: %7.1f us  %6.0f GB/s (alg %zu B)\n", grid, ms * 1e3,
                (bytes + nframes * 26) / ms / 1e6, bytes + nframes * 26);
