@@ -479,6 +479,7 @@ __global__ __launch_bounds__(kBlock, PNET_SMALL_WAVES) void rx_small_kernel(RxAr
     SmallRun cur = run < a.nruns ? small_load(a, run, lane) : SmallRun{};
     for (; run < a.nruns; run += wave_stride) {
         // software pipelining: the next run's loads are in flight while this one is processed
+        // (two runs ahead measured no faster: the wave is not short of loads in flight)
         const uint64_t nrun = run + wave_stride;
         SmallRun nxt = nrun < a.nruns ? small_load(a, nrun, lane) : SmallRun{};
 
