@@ -480,8 +480,10 @@ __global__ __launch_bounds__(kBlock, PNET_SMALL_WAVES) void rx_small_kernel(RxAr
     for (; run < a.nruns; run += wave_stride) {
         // software pipelining: the next run's loads are in flight while this one is processed
         // (two runs ahead measured no faster: the wave is not short of loads in flight)
+#ifndef PNET_SMALL_NOPF
         const uint64_t nrun = run + wave_stride;
         SmallRun nxt = nrun < a.nruns ? small_load(a, nrun, lane) : SmallRun{};
+#endif
 
         const uint64_t f0 = run * kWave;
         const bool in_batch = f0 + lane < a.n;
@@ -601,7 +603,12 @@ __global__ __launch_bounds__(kBlock, PNET_SMALL_WAVES) void rx_small_kernel(RxAr
         }
         // ---- generic path through LDS for the lanes the fast path did not take ----
         const bool need_v6 = a.cols.src_ipv6 || a.cols.dst_ipv6;
+#ifdef PNET_SMALL_NOSLOW
+        if (slow) P.st = 0xFFFFu;
+        if (false) {
+#else
         if (__ballot(slow) || need_v6) {
+#endif
             if (slow) {
                 // flags are 0 here and the frame (<= 64 B) is entirely in its slot
                 P = parse_frame(FrameBytes{slot, slot, 64}, len, 0u);
@@ -615,7 +622,11 @@ __global__ __launch_bounds__(kBlock, PNET_SMALL_WAVES) void rx_small_kernel(RxAr
         store_columns(a.cols, f0, lane, in_batch, P, ipc, l4c, slot, 0);
         if (a.cols.counters) K.add(in_batch, len, P.st);
         wave_sync();
+#ifndef PNET_SMALL_NOPF
         cur = nxt;
+#else
+        if (run + wave_stride < a.nruns) cur = small_load(a, run + wave_stride, lane);
+#endif
     }
     if (a.cols.counters) K.flush(a.cols.counters, blk_ctr, wv, lane);
 }
@@ -727,7 +738,10 @@ __device__ __forceinline__ void tail_sums(const uint8_t* data, WaveLds<NW>& L, i
     }
 }
 
-template <int NW, int G, int U, bool NT, bool UNI, bool TX>
+// PASS: 0 = window phase for every frame, then the tails of the long ones;
+// 1 = unified: every frame streamed once by the group loop (a hybrid - windows
+// of short frames first, long frames unified - measured 5-15 % slower on IMIX).
+template <int NW, int G, int U, bool NT, int PASS, bool TX>
 __global__ __launch_bounds__(kBlock, 4) void rx_kernel(RxArgs a) {
     static_assert(NW == 8, "window granules");
     static_assert(G == 4 || G == 8 || G == 16 || G == 32 || G == 64, "tail group");
@@ -779,12 +793,13 @@ __global__ __launch_bounds__(kBlock, 4) void rx_kernel(RxArgs a) {
         const uint64_t base = off - (uint64_t)sh;
         const uint32_t fend = (uint32_t)sh + len;            // slot-relative end of the frame
         const uint32_t span = (fend + 15u) >> 4;
+        const bool long_frame = fend > (uint32_t)kWin;
         L.base[lane] = base;
         L.end[lane] = span < (uint32_t)NW ? span : (uint32_t)NW;   // granules to load into the window
         wave_sync();
 
         // ---- 2. window: NW*64 granule loads, all in flight before any store --
-        if (!UNI) {
+        if (PASS != 1) {
             uint4 g[NW];
 #pragma unroll
             for (int i = 0; i < NW; ++i) {
@@ -809,9 +824,9 @@ __global__ __launch_bounds__(kBlock, 4) void rx_kernel(RxArgs a) {
         // ---- 3. speculative tail: all frame bytes past the window ----------
         // Summed before the parse (no parse state is live, so more loads fit in
         // flight); the parse then trims it to the L4 range B, which in every
-        // well-formed frame already runs to the end of the frame. UNI: every
-        // frame goes through the group loop, which also fills its window.
-        const bool has_tail = UNI ? in_batch : fend > (uint32_t)kWin;
+        // well-formed frame already runs to the end of the frame. Unified pass:
+        // the group loop also fills the window of every frame.
+        const bool has_tail = PASS == 1 ? in_batch : long_frame;
         const uint64_t tmask = __ballot(has_tail);
         if (tmask) {
             if (has_tail) {
@@ -819,7 +834,7 @@ __global__ __launch_bounds__(kBlock, 4) void rx_kernel(RxArgs a) {
                 L.end[lane] = fend;
             }
             wave_sync();
-            tail_sums<NW, G, U, NT, UNI>(a.data, L, lane, __popcll(tmask));
+            tail_sums<NW, G, U, NT, (PASS != 0)>(a.data, L, lane, __popcll(tmask));
         }
         wave_sync();
 
@@ -956,19 +971,19 @@ static int resident_blocks(const void* fn) {
 }
 
 // Tail shapes per kernel kind: <G lanes per frame, U loads in flight per lane,
-// non-temporal loads, unified window+tail pass>, from same-box A/B runs on
+// non-temporal loads, PASS (0 window/tail split, 1 unified)>, from same-box A/B runs on
 // MI355X (tools/abvar.sh): descriptor batches of mixed sizes want narrow groups
 // and deep loads; MTU frames 8-lane groups streaming each whole frame once
 // (unified: -6 % time); jumbo frames the whole wave on one frame, 9 KiB in
 // flight per round (one round per 9000-B frame), non-temporal.
 #ifndef PNET_MIXED_CFG
-#define PNET_MIXED_CFG 4, 8, false, false
+#define PNET_MIXED_CFG 4, 8, false, 0
 #endif
 #ifndef PNET_MTU_CFG
-#define PNET_MTU_CFG 8, 4, false, true
+#define PNET_MTU_CFG 8, 4, false, 1
 #endif
 #ifndef PNET_JUMBO_CFG
-#define PNET_JUMBO_CFG 64, 9, true, false
+#define PNET_JUMBO_CFG 64, 9, true, 0
 #endif
 
 template <bool TX>
