@@ -232,11 +232,15 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist_on = world > 1
+    # one rank per GPU; the modulo only matters for a rehearsal with more ranks
+    # than GPUs (PNETGPU_BENCH_BACKEND=gloo, e.g. 2 ranks on a 1-GPU box)
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
     if dist_on:
         import datetime
-        torch.distributed.init_process_group("nccl", timeout=datetime.timedelta(minutes=10))
+        backend = os.environ.get("PNETGPU_BENCH_BACKEND", "nccl")   # nccl = RCCL over xGMI
+        torch.distributed.init_process_group(backend, timeout=datetime.timedelta(minutes=10))
 
     names = [w for w in args.workloads.split(",") if w]
     results = {}

@@ -194,6 +194,40 @@ def test_stride_mode_odd_stride_and_offset():
         compare(res, rec)
 
 
+@pytest.mark.parametrize("stride", [16, 48, 64, 80, 128])
+def test_small_kernel_strides_and_lengths(stride):
+    """The register-resident small kernel (fixed stride, multiple of 16, frames
+    <= 64 B, 16-B aligned): every frame length from the Ethernet minimum edge to
+    64 B, random kinds (IPv6 and IPv4 options take its generic slow path),
+    corrupted bytes, a batch that is not a whole number of 64-frame runs, and
+    garbage between frames."""
+    rng = np.random.default_rng(stride)
+    n = 1000
+    kinds = ("udp", "tcp", "icmp", "udp6", "tcp6", "icmp6", "icmp_over6")
+    frames = []
+    for i in range(n):
+        k = kinds[i % len(kinds)]
+        ihl = 5 if i % 5 else int(rng.integers(5, 16))
+        f = bytearray(framegen.build_frame(rng, k, int(rng.integers(0, 40)), ihl=ihl))
+        if i % 9 == 0 and len(f) > 20:
+            f[int(rng.integers(14, len(f)))] ^= 0x5A
+        frames.append(bytes(f))
+    for first in (0, 32):
+        for flen in sorted({0, 1, 13, 14, 33, 34, 41, 42, 53, 54, 61, 64, min(stride, 64)}):
+            if flen > stride:
+                continue
+            buf = rng.integers(0, 256, first + stride * n + 64, dtype=np.uint8)
+            for i, f in enumerate(frames):
+                f = np.frombuffer(f, np.uint8)[:stride]
+                buf[first + i * stride:first + i * stride + len(f)] = f
+            rec = coracle.rx_batch(buf, n, first=first, stride=stride, frame_len=flen, nthreads=NTHREADS)
+            res = lp.rx_process(to_dev(buf), stride=stride, frame_len=flen, first_offset=first, n_frames=n,
+                                columns=ALL_COLUMNS)
+            torch.cuda.synchronize()
+            compare(res, rec)
+            assert res.counter_dict() == oracle_counters(rec, np.full(n, flen, np.uint32)), (first, flen)
+
+
 @pytest.mark.parametrize("stride,flen", [(144, 144), (150, 97), (333, 333), (1500, 1500), (1514, 1400),
                                          (4000, 3999), (9018, 9018)])
 def test_stride_mode_random_frames_every_kernel(stride, flen, monkeypatch):

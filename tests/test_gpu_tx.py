@@ -55,3 +55,28 @@ def test_tx_then_rx_all_verify_and_idempotent():
     r = lp.rx_process(d, stride=64, frame_len=64, n_frames=w.n)
     c = r.counter_dict()
     assert c["ip_csum_bad"] == 0 and c["l4_csum_bad"] == 0 and c["frames"] == w.n
+
+
+@pytest.mark.parametrize("stride,flen", [(64, 64), (64, 60), (1514, 1514), (1500, 1400), (9018, 9018)])
+def test_tx_fill_stride_every_kernel(stride, flen, monkeypatch):
+    """Fixed-stride TX fill of random/corrupted frames through the default kernel
+    for the shape and every forced rx_kernel kind (PNETGPU_RX_KIND)."""
+    rng = np.random.default_rng(stride * 7 + flen)
+    n = 300
+    frames = framegen.random_frames(rng, n, max_len=min(stride, 9100))
+    buf = rng.integers(0, 256, stride * n + 64, dtype=np.uint8)
+    for i, f in enumerate(frames):
+        f = np.frombuffer(f, np.uint8)[:stride]
+        buf[i * stride:i * stride + len(f)] = f
+    want_buf, want_rec = coracle.tx_fill(buf, n, stride=stride, frame_len=flen)
+    for kind in (None, "0", "2", "3"):
+        if kind is None:
+            monkeypatch.delenv("PNETGPU_RX_KIND", raising=False)
+        else:
+            monkeypatch.setenv("PNETGPU_RX_KIND", kind)
+        d = to_dev(buf.copy())
+        res = lp.tx_fill_checksums(d, stride=stride, frame_len=flen, n_frames=n, columns=ALL_COLUMNS)
+        torch.cuda.synchronize()
+        got = d.cpu().numpy()
+        assert np.array_equal(got, want_buf), (kind, int((got != want_buf).sum()))
+        compare(res, want_rec)

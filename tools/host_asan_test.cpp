@@ -1,0 +1,152 @@
+// host_asan_test.cpp — AddressSanitizer/UBSan run of the library's HOST code
+// (no GPU needed): the synthetic-frame producer, the classic-pcap reader and
+// the C-ABI's argument validation. Linked from objects built with
+// -fsanitize=address,undefined (libpnet_amd/Makefile target `asan-test`), so
+// the sanitizer runtime comes with the executable itself.
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "pnetgpu.h"
+#include "pnetgpu_ring.h"
+#include "pnetgpu_synth.h"
+
+static int failures = 0;
+#define CHECK(c)                                                              \
+    do {                                                                      \
+        if (!(c)) {                                                           \
+            std::fprintf(stderr, "FAIL %s:%d: %s\n", __FILE__, __LINE__, #c); \
+            ++failures;                                                       \
+        }                                                                     \
+    } while (0)
+
+static void put32(std::vector<uint8_t>& b, uint32_t v, bool be) {
+    for (int i = 0; i < 4; ++i) b.push_back((uint8_t)(be ? v >> (24 - 8 * i) : v >> (8 * i)));
+}
+static void put16(std::vector<uint8_t>& b, uint16_t v, bool be) {
+    b.push_back((uint8_t)(be ? v >> 8 : v));
+    b.push_back((uint8_t)(be ? v : v >> 8));
+}
+
+static std::string write_pcap(const char* name, bool be, bool ns, const std::vector<std::vector<uint8_t>>& frames,
+                              size_t truncate_to = 0) {
+    std::vector<uint8_t> b;
+    put32(b, ns ? 0xA1B23C4Du : 0xA1B2C3D4u, be);
+    put16(b, 2, be);
+    put16(b, 4, be);
+    put32(b, 0, be);
+    put32(b, 0, be);
+    put32(b, 65535, be);
+    put32(b, 1, be);   // LINKTYPE_ETHERNET
+    for (const auto& f : frames) {
+        put32(b, 1, be);
+        put32(b, 2, be);
+        put32(b, (uint32_t)f.size(), be);
+        put32(b, (uint32_t)f.size() + 4, be);
+        b.insert(b.end(), f.begin(), f.end());
+    }
+    if (truncate_to && truncate_to < b.size()) b.resize(truncate_to);
+    std::string path = std::string("/tmp/pnet_asan_") + name + ".pcap";
+    FILE* fp = std::fopen(path.c_str(), "wb");
+    std::fwrite(b.data(), 1, b.size(), fp);
+    std::fclose(fp);
+    return path;
+}
+
+static void test_synth() {
+    for (int w = 0; w <= 4; ++w) {
+        for (uint64_t n : {1ull, 63ull, 1000ull}) {
+            uint64_t total = 0;
+            uint32_t stride = 0, flen = 0;
+            CHECK(pnetgpu_synth_layout(w, n, 7, &total, &stride, &flen) == 0);
+            std::vector<uint8_t> buf(total);
+            std::vector<uint64_t> offs(n);
+            std::vector<uint32_t> lens(n);
+            uint64_t exp[PNETGPU_SYNTH_NEXP] = {};
+            CHECK(pnetgpu_synth_fill(w, n, 7, 300000, buf.data(), buf.size(), offs.data(), lens.data(), exp, 3) == 0);
+            CHECK(exp[PNETGPU_SYNTH_EXP_BYTES] > 0);
+            // a buffer one byte short is refused, not overrun
+            if (total > 0)
+                CHECK(pnetgpu_synth_fill(w, n, 7, 0, buf.data(), total - 1, offs.data(), lens.data(), exp, 1) != 0);
+        }
+    }
+    uint64_t total = 0;
+    uint32_t stride = 0, flen = 0;
+    CHECK(pnetgpu_synth_layout(99, 10, 1, &total, &stride, &flen) != 0);
+}
+
+static void test_pcap() {
+    std::vector<std::vector<uint8_t>> frames;
+    for (int i = 0; i < 50; ++i) frames.emplace_back((size_t)(i * 37 % 1600), (uint8_t)i);
+    for (int be = 0; be < 2; ++be) {
+        for (int ns = 0; ns < 2; ++ns) {
+            const std::string p = write_pcap("ok", be, ns, frames);
+            pnetgpu_pcap* pc = nullptr;
+            CHECK(pnetgpu_pcap_open(p.c_str(), &pc) == 0);
+            const uint8_t* f = nullptr;
+            uint32_t len = 0;
+            size_t k = 0;
+            int rc;
+            while ((rc = pnetgpu_pcap_next(pc, &f, &len)) == 0) {
+                CHECK(k < frames.size() && len == frames[k].size());
+                if (k < frames.size() && len == frames[k].size() && len) CHECK(std::memcmp(f, frames[k].data(), len) == 0);
+                ++k;
+            }
+            CHECK(rc == PNETGPU_EEMPTY && k == frames.size());
+            pnetgpu_pcap_close(pc);
+        }
+    }
+    // truncated inside a record: the reader stops without reading past the file
+    const std::string t = write_pcap("trunc", false, false, frames, 24 + 16 + 10 + 16 + 3);
+    pnetgpu_pcap* pc = nullptr;
+    if (pnetgpu_pcap_open(t.c_str(), &pc) == 0) {
+        const uint8_t* f = nullptr;
+        uint32_t len = 0;
+        int n = 0;
+        while (pnetgpu_pcap_next(pc, &f, &len) == 0 && n < 100) ++n;
+        CHECK(n <= 2);
+        pnetgpu_pcap_close(pc);
+    }
+    // not a pcap file / missing file
+    const std::string g = "/tmp/pnet_asan_garbage.pcap";
+    FILE* fp = std::fopen(g.c_str(), "wb");
+    std::fputs("definitely not a capture file", fp);
+    std::fclose(fp);
+    CHECK(pnetgpu_pcap_open(g.c_str(), &pc) == PNETGPU_EFORMAT);
+    CHECK(pnetgpu_pcap_open("/tmp/pnet_asan_does_not_exist.pcap", &pc) != 0);
+}
+
+static void test_abi_validation() {
+    CHECK(pnetgpu_abi_version() == 2);
+    for (int c = 0; c >= -8; --c) CHECK(pnetgpu_strerror(c) != nullptr && std::strlen(pnetgpu_strerror(c)) > 0);
+    CHECK(pnetgpu_strerror(-1000) != nullptr);
+    pnetgpu_batch b{};
+    pnetgpu_rx_columns cols{};
+    CHECK(pnetgpu_rx_process(nullptr, &b, &cols, nullptr) == PNETGPU_EINVAL);
+    CHECK(pnetgpu_tx_fill_checksums(nullptr, &b, &cols, nullptr) == PNETGPU_EINVAL);
+    uint16_t out[4];
+    uint64_t off[4] = {0, 1, 2, 3};
+    uint32_t len[4] = {1, 1, 1, 1}, skip[4] = {0, 0, 0, 0};
+    uint8_t data[16] = {};
+    CHECK(pnetgpu_checksum_slices(nullptr, data, 16, 4, off, len, skip, out, nullptr) == PNETGPU_EINVAL);
+    CHECK(pnetgpu_ipv4_checksum_adv_slices(nullptr, data, 16, 4, off, len, skip, off, len, data, data, out,
+                                           nullptr) == PNETGPU_EINVAL);
+    pnetgpu_ring* r = nullptr;
+    CHECK(pnetgpu_ring_create(nullptr, 1 << 20, 1024, 0, &r) == PNETGPU_EINVAL);
+    pnetgpu_ctx* ctx = nullptr;
+    CHECK(pnetgpu_ctx_create(-1, &ctx) != 0);
+    pnetgpu_ctx_destroy(nullptr);
+    pnetgpu_ring_destroy(nullptr);
+    pnetgpu_pcap_close(nullptr);
+}
+
+int main() {
+    test_synth();
+    test_pcap();
+    test_abi_validation();
+    std::printf("%s (%d failures)\n", failures ? "FAILED" : "ok", failures);
+    return failures ? 1 : 0;
+}
