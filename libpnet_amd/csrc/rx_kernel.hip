@@ -641,7 +641,8 @@ struct WaveLds {
     uint64_t base[kWave];     // aligned byte offset of granule 0 of each frame
     uint32_t end[kWave];      // window granules to load; then slot-relative frame end
     uint32_t tail[kWave];     // weighted sum of the frame's bytes past the window
-    uint8_t list[kWave];      // frames with bytes past the window, in lane order
+    uint8_t list[kWave];      // frames with bytes past the window (longest class first)
+    uint32_t qhead;           // next list entry for a group that runs out of work
 };
 
 // Weighted sum of slot bytes [lo, hi) of a frame whose granule 0 is at fb, read
@@ -672,7 +673,11 @@ __device__ __forceinline__ uint32_t lane_range_sum(const uint8_t* fb, int lo, in
 // holding the window/tail boundary and the line shared with the next frame are
 // fetched once, while they are still in L2 (the windows-first order read ~15 %
 // more than the frame bytes on MTU frames: TCC_EA0_RDREQ, profiles/).
-template <int NW, int G, int U, bool NT, bool UNI>
+// DYN: a group that finishes a frame takes the next list entry from a shared
+// LDS counter instead of a fixed stride of the list, and the list holds the
+// frames needing more than one round first, so mixed sizes balance across the
+// groups (the caller sets L.qhead = kWave / G).
+template <int NW, int G, int U, bool NT, bool UNI, bool DYN>
 __device__ __forceinline__ void tail_sums(const uint8_t* data, WaveLds<NW>& L, int lane, int count) {
     constexpr int kGroups = kWave / G;
     constexpr int kSlot = WaveLds<NW>::kSlot;
@@ -725,7 +730,13 @@ __device__ __forceinline__ void tail_sums(const uint8_t* data, WaveLds<NW>& L, i
                 for (int o = G / 2; o >= 1; o >>= 1) acc += __shfl_xor(acc, o);
                 if (j == 0) L.tail[fl] = acc;
                 acc = 0;
-                idx += kGroups;
+                if (DYN) {
+                    uint32_t nidx = 0;
+                    if (j == 0) nidx = atomicAdd(&L.qhead, 1u);
+                    idx = __shfl((int)nidx, lane - j);
+                } else {
+                    idx += kGroups;
+                }
                 if (idx < count) {
                     fl = L.list[idx];
                     fe = L.end[fl];
@@ -741,7 +752,7 @@ __device__ __forceinline__ void tail_sums(const uint8_t* data, WaveLds<NW>& L, i
 // PASS: 0 = window phase for every frame, then the tails of the long ones;
 // 1 = unified: every frame streamed once by the group loop (a hybrid - windows
 // of short frames first, long frames unified - measured 5-15 % slower on IMIX).
-template <int NW, int G, int U, bool NT, int PASS, bool TX>
+template <int NW, int G, int U, bool NT, int PASS, bool DYN, bool TX>
 __global__ __launch_bounds__(kBlock, 4) void rx_kernel(RxArgs a) {
     static_assert(NW == 8, "window granules");
     static_assert(G == 4 || G == 8 || G == 16 || G == 32 || G == 64, "tail group");
@@ -829,12 +840,18 @@ __global__ __launch_bounds__(kBlock, 4) void rx_kernel(RxArgs a) {
         const bool has_tail = PASS == 1 ? in_batch : long_frame;
         const uint64_t tmask = __ballot(has_tail);
         if (tmask) {
+            // DYN: frames needing more than one group round go first
+            const bool big = DYN && has_tail && span > (uint32_t)(NW + G * U);
+            const uint64_t bmask = __ballot(big);
+            const uint64_t below = (1ull << lane) - 1ull;
             if (has_tail) {
-                L.list[__popcll(tmask & ((1ull << lane) - 1ull))] = (uint8_t)lane;
+                const int pos = big ? __popcll(bmask & below) : __popcll(bmask) + __popcll(tmask & ~bmask & below);
+                L.list[pos] = (uint8_t)lane;
                 L.end[lane] = fend;
             }
+            if (DYN && lane == 0) L.qhead = kWave / G;
             wave_sync();
-            tail_sums<NW, G, U, NT, (PASS != 0)>(a.data, L, lane, __popcll(tmask));
+            tail_sums<NW, G, U, NT, (PASS != 0), DYN>(a.data, L, lane, __popcll(tmask));
         }
         wave_sync();
 
@@ -971,19 +988,19 @@ static int resident_blocks(const void* fn) {
 }
 
 // Tail shapes per kernel kind: <G lanes per frame, U loads in flight per lane,
-// non-temporal loads, PASS (0 window/tail split, 1 unified)>, from same-box A/B runs on
+// non-temporal loads, PASS (0 window/tail split, 1 unified), DYN queue>, from same-box A/B runs on
 // MI355X (tools/abvar.sh): descriptor batches of mixed sizes want narrow groups
 // and deep loads; MTU frames 8-lane groups streaming each whole frame once
 // (unified: -6 % time); jumbo frames the whole wave on one frame, 9 KiB in
 // flight per round (one round per 9000-B frame), non-temporal.
 #ifndef PNET_MIXED_CFG
-#define PNET_MIXED_CFG 4, 8, false, 0
+#define PNET_MIXED_CFG 4, 8, false, 0, true
 #endif
 #ifndef PNET_MTU_CFG
-#define PNET_MTU_CFG 8, 4, false, 1
+#define PNET_MTU_CFG 8, 4, false, 1, false
 #endif
 #ifndef PNET_JUMBO_CFG
-#define PNET_JUMBO_CFG 64, 9, true, 0
+#define PNET_JUMBO_CFG 64, 9, true, 0, false
 #endif
 
 template <bool TX>
