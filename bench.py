@@ -175,7 +175,7 @@ def e2e_rate(sh, device, chunks=16, reps=3):
 
 
 def e2e_ring_rate(sh, seconds=3.0):
-    """Producer-inclusive rate: frames copied one by one into the pinned ring
+    """Producer-inclusive rate: frames copied into the pinned ring
     (pnetgpu_ring_push_many: the DataLinkReceiver::next() consumer), shipped,
     verified and every record column copied back (three rotating slots)."""
     w = sh.w
@@ -200,8 +200,9 @@ def e2e_ring_rate(sh, seconds=3.0):
     el = time.perf_counter() - t0
     ring.close()
     return {"mpkts_s": round(frames / el / 1e6, 1), "gb_s": round(nbytes / el / 1e9, 2),
-            "note": "host frames pushed into the pinned ring one memcpy per frame (one host thread), "
-                    "async H2D -> rx kernel -> D2H of all 14 result columns, 3 rotating slots of 1 Mi frames"}
+            "note": "host frames pushed into the pinned ring with pnetgpu_ring_push_many (source-adjacent "
+                    "frames coalesced, up to 8 copy threads), async H2D -> rx kernel -> D2H of all 16 result "
+                    "columns, 3 rotating slots of 1 Mi frames"}
 
 
 def load_traffic(workload):

@@ -3,10 +3,12 @@
 // dependency-free classic pcap reader (the pnet_datalink pcap.rs:92 receiver).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstring>
 #include <deque>
 #include <new>
+#include <thread>
 #include <vector>
 
 #include "pnetgpu.h"
@@ -176,12 +178,46 @@ int pnetgpu_ring_push_many(pnetgpu_ring* r, const uint8_t* buf, const uint64_t* 
                            uint64_t n, uint64_t* pushed) {
     if (!r || !pushed || (n && (!buf || !offsets || !lengths))) return PNETGPU_EINVAL;
     *pushed = 0;
-    for (uint64_t i = 0; i < n; ++i) {
-        const int rc = pnetgpu_ring_push(r, buf + offsets[i], lengths[i]);
-        if (rc == PNETGPU_EFULL || rc == PNETGPU_EBUSY) return *pushed ? PNETGPU_OK : rc;
-        if (rc) return rc;
-        *pushed += 1;
+    if (n == 0) return PNETGPU_OK;
+    if (r->filling < 0 && (r->filling = take_free_slot(r)) < 0) return PNETGPU_EBUSY;
+    Slot& s = r->slots[r->filling];
+    // descriptors of the frames that fit, in order (the same cut as pushing one by one)
+    const uint64_t room_f = r->cap_frames - s.n;
+    uint64_t k = 0, bytes = 0;
+    while (k < n && k < room_f && lengths[k] <= r->cap_bytes - s.bytes - bytes) {
+        s.h_off[s.n + k] = s.bytes + bytes;
+        s.h_len[s.n + k] = lengths[k];
+        bytes += lengths[k];
+        ++k;
     }
+    if (k == 0) return PNETGPU_EFULL;
+    // frame bytes: runs of frames adjacent in the source go in one memcpy; large
+    // pushes are split over host threads (one thread's memcpy into pinned memory
+    // tops out far below the PCIe link the batch is headed for)
+    uint8_t* dst = s.h_frames;
+    const uint64_t* doff = s.h_off + s.n;
+    auto copy_range = [&](uint64_t lo, uint64_t hi) {
+        uint64_t i = lo;
+        while (i < hi) {
+            uint64_t j = i + 1;
+            while (j < hi && offsets[j] == offsets[j - 1] + lengths[j - 1]) ++j;
+            const uint64_t run = doff[j - 1] + lengths[j - 1] - doff[i];
+            if (run) std::memcpy(dst + doff[i], buf + offsets[i], run);
+            i = j;
+        }
+    };
+    unsigned nt = 1;
+    if (bytes >= (8ull << 20)) nt = std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
+    if (nt == 1) {
+        copy_range(0, k);
+    } else {
+        std::vector<std::thread> th;
+        for (unsigned t = 0; t < nt; ++t) th.emplace_back(copy_range, k * t / nt, k * (t + 1) / nt);
+        for (auto& t : th) t.join();
+    }
+    s.n += k;
+    s.bytes += bytes;
+    *pushed = k;
     return PNETGPU_OK;
 }
 
