@@ -370,3 +370,42 @@ def test_adv_slices_match_tcp_with_options_split():
                                      to_dev(np.array([1000 - hl], np.int32)), to_dev(addrs),
                                      to_dev(np.array([6], np.uint8)))
         assert int(got.cpu().numpy().view(np.uint16)[0]) == whole, hl
+
+
+def test_maximum_sizes_all_ones():
+    """The largest sums the path can meet: IPv4 total_length 65535 and IPv6
+    payload_length 65535 frames of 0xFF bytes (every 16-bit word 0xFFFF), plus
+    the same through the fixed-stride jumbo kernel, and util::checksum slices
+    of 0xFF up to 131070 bytes (the longest slice whose u32 word sum cannot wrap,
+    SURVEY.md §8(a) a1)."""
+    rng = np.random.default_rng(77)
+    frames = []
+    for kind in ("udp", "tcp", "udp6", "tcp6"):
+        iphl = 40 if kind.endswith("6") else 20
+        f = bytearray(framegen.build_frame(rng, kind, 65535 - (0 if iphl == 40 else 20)))
+        f[14 + iphl:] = b"\xff" * (len(f) - 14 - iphl)
+        frames.append(bytes(f))
+        g = bytearray(f)
+        g[14 + iphl + 100] = 0          # one zero byte: a different sum
+        frames.append(bytes(g))
+    buf, offs, lens = framegen.pack(frames, gap=15, rng=rng)
+    rec = oracle_desc(buf, offs, lens)
+    compare(run_desc(buf, offs, lens), rec)
+    # the same frames through the fixed-stride kernels (one frame length at a time)
+    for f in frames[:2]:
+        stride = len(f) + 3
+        sbuf = np.zeros(stride * 4 + 64, np.uint8)
+        for i in range(4):
+            sbuf[i * stride:i * stride + len(f)] = np.frombuffer(f, np.uint8)
+        srec = coracle.rx_batch(sbuf, 4, stride=stride, frame_len=len(f))
+        res = lp.rx_process(to_dev(sbuf), stride=stride, frame_len=len(f), n_frames=4, columns=ALL_COLUMNS)
+        torch.cuda.synchronize()
+        compare(res, srec)
+    # util::checksum over long all-ones slices at every alignment
+    big = np.full(131070 + 64, 0xFF, np.uint8)
+    offs_s = np.array([0, 1, 2, 7, 15, 3, 0], np.int64)
+    lens_s = np.array([131070, 131069, 131068, 65535, 100000, 131000, 1], np.int32)
+    skips = np.array([0, 5, 70000, 65534, 3, 1 << 20, 0], np.int32)
+    want = coracle.checksum_slices(big, offs_s.astype(np.uint64), lens_s.astype(np.uint32), skips.astype(np.uint32))
+    got = lp.checksum_slices(to_dev(big), to_dev(offs_s), to_dev(lens_s), to_dev(skips))
+    assert np.array_equal(got.cpu().numpy().view(np.uint16), want)

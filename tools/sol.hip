@@ -98,6 +98,44 @@ __global__ __launch_bounds__(256) void read_cols_nt_kernel(const uint4* __restri
     }
 }
 
+// same reads; the run's 26 B/frame of columns staged in LDS and written as
+// 16-B-per-lane stores (2 wave instructions instead of 12 narrow ones)
+__global__ __launch_bounds__(256) void read_cols_lds_kernel(const uint4* __restrict__ in, size_t nframes,
+                                                            uint16_t* c16, uint32_t* c32, uint8_t* c8) {
+    __shared__ __attribute__((aligned(16))) uint8_t stage[4][1664];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    uint8_t* st = stage[wv];
+    const size_t wave = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const size_t nwaves = ((size_t)gridDim.x * blockDim.x) >> 6;
+    for (size_t run = wave; run * 64 < nframes; run += nwaves) {
+        const uint4* p = in + run * 256;
+        uint4 v0 = p[lane], v1 = p[64 + lane], v2 = p[128 + lane], v3 = p[192 + lane];
+        uint32_t x = v0.x ^ v1.y ^ v2.z ^ v3.w;
+        // staging layout: 8 u16 columns (128 B each), 2 u32 (256 B each), 2 u8 (64 B each)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) reinterpret_cast<uint16_t*>(st + 128 * k)[lane] = (uint16_t)(x + k);
+        reinterpret_cast<uint32_t*>(st + 1024)[lane] = x;
+        reinterpret_cast<uint32_t*>(st + 1280)[lane] = x ^ 1;
+        st[1536 + lane] = (uint8_t)x;
+        st[1600 + lane] = (uint8_t)(x >> 8);
+        __builtin_amdgcn_wave_barrier();
+        const size_t f0 = run * 64;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int q = h * 64 + lane;       // 16-B piece index, 104 pieces
+            if (q < 104) {
+                const uint4 val = *reinterpret_cast<const uint4*>(st + 16 * q);
+                uint8_t* dst;
+                if (q < 64) dst = reinterpret_cast<uint8_t*>(c16 + (size_t)(q >> 3) * nframes + f0) + 16 * (q & 7);
+                else if (q < 96) dst = reinterpret_cast<uint8_t*>(c32 + (size_t)((q - 64) >> 4) * nframes + f0) + 16 * ((q - 64) & 15);
+                else dst = c8 + (size_t)((q - 96) >> 2) * nframes + f0 + 16 * ((q - 96) & 3);
+                __builtin_nontemporal_store(*reinterpret_cast<const u32x4_t*>(&val), reinterpret_cast<u32x4_t*>(dst));
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
 // same reads, one packed 32-B record per frame (two dwordx4 stores per lane)
 __global__ __launch_bounds__(256) void read_rec_kernel(const uint4* __restrict__ in, size_t nframes, uint4* rec) {
     const int lane = threadIdx.x & 63;
@@ -180,6 +218,8 @@ int main() {
                (bytes + nframes * 26) / ms / 1e6, bytes + nframes * 26);
         ms = time_it([&] { read_cols_nt_kernel<<<grid, 256>>>(in, nframes, c16, c32, c8); }, 20);
         printf("read+26B cols nt grid=%5d: %7.1f us  %6.0f GB/s\n", grid, ms * 1e3, (bytes + nframes * 26) / ms / 1e6);
+        ms = time_it([&] { read_cols_lds_kernel<<<grid, 256>>>(in, nframes, c16, c32, c8); }, 20);
+        printf("read+26B cols lds16 grid=%5d: %7.1f us  %6.0f GB/s\n", grid, ms * 1e3, (bytes + nframes * 26) / ms / 1e6);
         ms = time_it([&] { read_cols2_kernel<<<grid, 256>>>(in, nframes, c16, c32, c8); }, 20);
         printf("read+26B cols x2 grid=%5d: %7.1f us  %6.0f GB/s\n", grid, ms * 1e3, (bytes + nframes * 26) / ms / 1e6);
         ms = time_it([&] { read_rec_kernel<<<grid, 256>>>(in, nframes, out); }, 20);
