@@ -6,7 +6,7 @@ pnet_packet. The product is libpnetgpu.so (HIP kernels behind the C-ABI in
 include/pnetgpu.h); this package is its Python host binding.
 """
 from ._lib import DEFS, LIB_PATH, PnetGpuError, lib  # noqa: F401  (fails loudly if the .so is absent)
-from . import synth  # noqa: F401
+from . import packet, synth  # noqa: F401  (packet: pnet_packet's function names)
 from .ring import Ring, pcap_frames  # noqa: F401
 from .engine import (ALL_COLUMNS, COUNTER_NAMES, IPV4_COLUMNS, Context, RxResult,  # noqa: F401
                      checksum_adv_slices, checksum_slices, column_bytes, context, ipv4_checksum_slices,
