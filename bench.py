@@ -32,12 +32,12 @@ METRIC = "device-resident Mpkts/s & GB/s, checksum+parse, 64B & 1500B, 1/2/4/8 G
 WORKLOADS = {
     "udp64": {"n": 1 << 24, "kernel": "rx_small_kernel", "desc": "configs[1]: 64B UDP/IPv4/Ethernet, checksum verify + header extract, "
                                     "device-resident batch"},
-    "tcp1500": {"n": 1 << 20, "kernel": "rx_kernel<8, 8, 4, false, 1, false> (MTU, unified pass)", "desc": "configs[2]: 1500B TCP/IPv4/Ethernet, full-MTU ones-complement sum over "
+    "tcp1500": {"n": 1 << 20, "kernel": "rx_kernel<8, 8, 4, false, 1, false, false> (MTU, unified pass)", "desc": "configs[2]: 1500B TCP/IPv4/Ethernet, full-MTU ones-complement sum over "
                                       "pseudo-header+payload"},
     # not in the default run: the 8-GPU configs, per-GPU shard sizes (weak scaling)
-    "imix": {"n": 1 << 22, "kernel": "rx_kernel<8, 4, 8, false, 0, true> (mixed, dynamic tail queue)",
+    "imix": {"n": 1 << 22, "kernel": "rx_kernel<8, 4, 8, false, 0, true, false> (mixed, dynamic tail queue)",
              "desc": "configs[3]: IMIX 64/576/1500B 7:4:1 Eth/IPv4/{UDP,TCP,ICMP}, descriptor mode, per-GPU shard"},
-    "udp6_jumbo": {"n": 1 << 17, "kernel": "rx_kernel<8, 64, 9, true, 0, false> (jumbo)",
+    "udp6_jumbo": {"n": 1 << 17, "kernel": "rx_kernel<8, 64, 9, true, 0, false, false> (jumbo)",
                    "desc": "configs[4]: 9000B IPv6/UDP jumbo frames, IPv6 pseudo-header checksum, per-GPU shard"},
 }
 

@@ -136,7 +136,7 @@ static int rx_common(pnetgpu_ctx* ctx, const pnetgpu_batch* b, const pnetgpu_rx_
             kind = v;
     }
     int numregs = 0, lds = 0;
-    int per_cu = pnetgpu::rx_blocks_per_cu(kind, &numregs, &lds);
+    int per_cu = pnetgpu::rx_blocks_per_cu(kind, b->flags != 0, &numregs, &lds);
     if (per_cu <= 0) return PNETGPU_EHIP;
     if (const char* e = std::getenv("PNETGPU_BLOCKS_PER_CU")) {   // tuning override
         const int v = std::atoi(e);

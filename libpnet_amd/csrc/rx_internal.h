@@ -51,7 +51,7 @@ constexpr int kKindJumbo = 3;
 // device index a context is bound to (abi.cpp)
 int ctx_device(const pnetgpu_ctx* ctx);
 
-int rx_blocks_per_cu(int kind, int* numregs, int* lds);
+int rx_blocks_per_cu(int kind, bool ext, int* numregs, int* lds);
 int launch_rx(const RxArgs& args, int kind, int blocks, bool tx, hipStream_t stream);
 int launch_slices(const SliceArgs& args, int pseudo, int blocks, hipStream_t stream);
 

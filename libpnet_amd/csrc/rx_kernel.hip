@@ -44,6 +44,7 @@
 #include "pnetgpu.h"
 #include "rx_internal.h"
 
+
 namespace pnetgpu {
 
 namespace {
@@ -752,7 +753,10 @@ __device__ __forceinline__ void tail_sums(const uint8_t* data, WaveLds<NW>& L, i
 // PASS: 0 = window phase for every frame, then the tails of the long ones;
 // 1 = unified: every frame streamed once by the group loop (a hybrid - windows
 // of short frames first, long frames unified - measured 5-15 % slower on IMIX).
-template <int NW, int G, int U, bool NT, int PASS, bool DYN, bool TX>
+// EXT: batch flags may be non-zero (VLAN / IPv6 extension dispatch); the
+// flags-0 instantiation compiles the parse without those branches (half the
+// code, SGPR spills 118 -> 14, IMIX -2 %).
+template <int NW, int G, int U, bool NT, int PASS, bool DYN, bool EXT, bool TX>
 __global__ __launch_bounds__(kBlock, 4) void rx_kernel(RxArgs a) {
     static_assert(NW == 8, "window granules");
     static_assert(G == 4 || G == 8 || G == 16 || G == 32 || G == 64, "tail group");
@@ -859,7 +863,7 @@ __global__ __launch_bounds__(kBlock, 4) void rx_kernel(RxArgs a) {
         Parsed P{};
         if (desc_bad) P.st = PNET_ST_DESC_INVALID;
         else if (in_batch)
-            P = parse_frame(FrameBytes{slot + sh, a.data + off, kWin - sh}, len, a.flags);
+            P = parse_frame(FrameBytes{slot + sh, a.data + off, kWin - sh}, len, EXT ? a.flags : 0u);
         // A (<= 97 B into the frame) always lies in the window; B may run past it
         const int p0 = P.a_lo + sh, p1 = P.a_hi + sh, p2 = P.b_lo + sh, p3 = P.b_hi + sh;
         uint32_t tA = 0, tB = 0;
@@ -1003,37 +1007,37 @@ static int resident_blocks(const void* fn) {
 #define PNET_JUMBO_CFG 64, 9, true, 0, false
 #endif
 
-template <bool TX>
+template <bool EXT, bool TX>
 const void* pick_fn(int kind) {
     switch (kind) {
     case kKindSmall: return reinterpret_cast<const void*>(rx_small_kernel<TX>);
-    case kKindMtu: return reinterpret_cast<const void*>(rx_kernel<8, PNET_MTU_CFG, TX>);
-    case kKindJumbo: return reinterpret_cast<const void*>(rx_kernel<8, PNET_JUMBO_CFG, TX>);
-    default: return reinterpret_cast<const void*>(rx_kernel<8, PNET_MIXED_CFG, TX>);
+    case kKindMtu: return reinterpret_cast<const void*>(rx_kernel<8, PNET_MTU_CFG, EXT, TX>);
+    case kKindJumbo: return reinterpret_cast<const void*>(rx_kernel<8, PNET_JUMBO_CFG, EXT, TX>);
+    default: return reinterpret_cast<const void*>(rx_kernel<8, PNET_MIXED_CFG, EXT, TX>);
     }
 }
 
-template <bool TX>
+template <bool EXT, bool TX>
 void launch_t(const RxArgs& args, int kind, int blocks, hipStream_t stream) {
     switch (kind) {
     case kKindSmall:
         hipLaunchKernelGGL(rx_small_kernel<TX>, dim3(blocks), dim3(kBlock), 0, stream, args);
         break;
     case kKindMtu:
-        hipLaunchKernelGGL((rx_kernel<8, PNET_MTU_CFG, TX>), dim3(blocks), dim3(kBlock), 0, stream, args);
+        hipLaunchKernelGGL((rx_kernel<8, PNET_MTU_CFG, EXT, TX>), dim3(blocks), dim3(kBlock), 0, stream, args);
         break;
     case kKindJumbo:
-        hipLaunchKernelGGL((rx_kernel<8, PNET_JUMBO_CFG, TX>), dim3(blocks), dim3(kBlock), 0, stream, args);
+        hipLaunchKernelGGL((rx_kernel<8, PNET_JUMBO_CFG, EXT, TX>), dim3(blocks), dim3(kBlock), 0, stream, args);
         break;
     default:
-        hipLaunchKernelGGL((rx_kernel<8, PNET_MIXED_CFG, TX>), dim3(blocks), dim3(kBlock), 0, stream, args);
+        hipLaunchKernelGGL((rx_kernel<8, PNET_MIXED_CFG, EXT, TX>), dim3(blocks), dim3(kBlock), 0, stream, args);
     }
 }
 
 }  // namespace
 
-int rx_blocks_per_cu(int kind, int* numregs, int* lds) {
-    const void* fn = pick_fn<false>(kind);
+int rx_blocks_per_cu(int kind, bool ext, int* numregs, int* lds) {
+    const void* fn = ext ? pick_fn<true, false>(kind) : pick_fn<false, false>(kind);
     hipFuncAttributes fa;
     if (hipFuncGetAttributes(&fa, fn) == hipSuccess) {
         if (numregs) *numregs = fa.numRegs;
@@ -1043,8 +1047,9 @@ int rx_blocks_per_cu(int kind, int* numregs, int* lds) {
 }
 
 int launch_rx(const RxArgs& args, int kind, int blocks, bool tx, hipStream_t stream) {
-    if (tx) launch_t<true>(args, kind, blocks, stream);
-    else launch_t<false>(args, kind, blocks, stream);
+    const bool ext = args.flags != 0;
+    if (tx) ext ? launch_t<true, true>(args, kind, blocks, stream) : launch_t<false, true>(args, kind, blocks, stream);
+    else ext ? launch_t<true, false>(args, kind, blocks, stream) : launch_t<false, false>(args, kind, blocks, stream);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -13,7 +13,7 @@ timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d $O/sta
     python3 $R/bench.py --workloads udp64,tcp1500,imix,udp6_jumbo --no-cpu --no-e2e \
     > $O/bench_under_rocprof.json 2> $O/bench_under_rocprof.err
 cp $(find $O/stats -name "*kernel_stats.csv" | head -1) $O/kernel_stats.csv
-declare -A KN=([udp64]=rx_small_kernel [tcp1500]="rx_kernel<8, 8, 4, false, 1, false" [imix]="rx_kernel<8, 4, 8, false, 0, true" [udp6_jumbo]="rx_kernel<8, 64, 9, true, 0, false")
+declare -A KN=([udp64]=rx_small_kernel [tcp1500]="rx_kernel<8, 8, 4, false, 1, false, false, false" [imix]="rx_kernel<8, 4, 8, false, 0, true, false, false" [udp6_jumbo]="rx_kernel<8, 64, 9, true, 0, false, false, false")
 for W in udp64 tcp1500 imix udp6_jumbo; do
   for C in FETCH_SIZE WRITE_SIZE; do
     timeout -k 10 300 rocprofv3 --pmc $C --kernel-trace --output-format csv -d $O/pmc_${W}_$C -o run -- \
