@@ -5,7 +5,7 @@
 // over pnet_packet's views and checksums, pnet_packet/src/util.rs:76-181); see
 // include/pnetgpu.h for the contract and DESIGN.md for layouts and rooflines.
 //
-// Two kernels, one wavefront (64 lanes) per run of 64 consecutive frames:
+// Receive kernels: one wavefront (64 lanes) per run of 64 consecutive frames:
 //
 //  rx_small_kernel  fixed-stride batches whose frames sit 16-B aligned and span
 //                   at most 64 B (the 64-B configs). The run's 4 KiB arrive as
@@ -19,14 +19,19 @@
 //                   options) takes the generic parse on its LDS slot.
 //
 //  rx_kernel        everything else (descriptor mode, any alignment, any size).
-//                   Window phase: the first NW=8 aligned 16-B granules of each
-//                   frame are loaded coalesced (8 loads in flight per lane) into
-//                   a padded LDS slot; lane l parses frame l there and sums the
-//                   window bytes. Tail phase: frames longer than the window go
-//                   on a per-wave work list served by groups of G lanes that
-//                   stream coalesced granules straight from HBM (U loads in
-//                   flight per lane), each group taking the next frame as soon
-//                   as it finishes one; partial sums are reduced with shuffles.
+//                   Per run: descriptors (prefetched a run ahead); the window
+//                   (first NW=8 aligned 16-B granules of each frame) into a
+//                   padded LDS slot; then, before any parsing, the speculative
+//                   tail: every frame byte past the window is summed by groups
+//                   of G lanes streaming coalesced granules (U loads in flight
+//                   per lane) from a per-wave frame list; then lane l parses
+//                   frame l from its slot, sums the window part of its ranges
+//                   and trims the tail sum to the L4 range. Shapes per kind
+//                   (mixed / MTU / jumbo) and the unified pass, where the group
+//                   loop also fills the window, are at the end of this file.
+//
+//  slice_kernel     the batched util::checksum / ipv4_checksum / ipv6_checksum
+//                   (and *_adv) entry points: 16 lanes per slice.
 //
 // Checksum arithmetic (why the sums are bit-exact without byte-swapping loads):
 //   The reference sums big-endian 16-bit words relative to the start of the slice
