@@ -27,7 +27,6 @@ namespace {
 
 constexpr int kBlock = 256;
 constexpr int kRunFrames = 64;      // frames per wave-run
-constexpr int kWavesPerBlock = 4;
 
 int set_device(const pnetgpu_ctx* ctx) {
     return hipSetDevice(ctx->device) == hipSuccess ? PNETGPU_OK : PNETGPU_EHIP;
@@ -119,11 +118,17 @@ static int rx_common(pnetgpu_ctx* ctx, const pnetgpu_batch* b, const pnetgpu_rx_
     // shape of the batch's frame sizes: MTU or jumbo for fixed stride, mixed for
     // descriptor batches (their lengths are device-resident).
     int kind = pnetgpu::kKindMixed;
+    bool stream_ok = false;
     if (b->stride) {
         const uint64_t base_sh = (a.delta + b->first_offset) & 15u;
         const uint64_t last_end = a.delta + b->first_offset + (b->n_frames - 1) * (uint64_t)b->stride + b->frame_len;
         const bool fits = b->n_frames <= (UINT64_MAX - a.delta - b->first_offset - b->frame_len) / b->stride &&
                           last_end <= a.limit;
+        // stream kernel (opt-in through PNETGPU_RX_KIND=4 until it beats the per-frame
+        // kernels): contiguous frames >= 1 KiB apart with at most 1/8 of the span in gaps
+        stream_ok = !tx && fits && b->stride >= 1024 && b->stride <= (1u << 20) && b->frame_len <= b->stride &&
+                    b->frame_len >= 256 &&
+                    (uint64_t)b->frame_len * 8 >= (uint64_t)b->stride * 7;
         if (base_sh == 0 && b->stride % 16 == 0 && b->frame_len <= 64 && fits && b->flags == 0)
             kind = pnetgpu::kKindSmall;
         else
@@ -131,7 +136,8 @@ static int rx_common(pnetgpu_ctx* ctx, const pnetgpu_batch* b, const pnetgpu_rx_
     }
     if (const char* e = std::getenv("PNETGPU_RX_KIND")) {          // tuning override (not the small kernel)
         const int v = std::atoi(e);
-        if ((v == pnetgpu::kKindMixed || v == pnetgpu::kKindMtu || v == pnetgpu::kKindJumbo) &&
+        if ((v == pnetgpu::kKindMixed || v == pnetgpu::kKindMtu || v == pnetgpu::kKindJumbo ||
+             (v == pnetgpu::kKindStream && stream_ok)) &&
             kind != pnetgpu::kKindSmall)
             kind = v;
     }
@@ -147,7 +153,8 @@ static int rx_common(pnetgpu_ctx* ctx, const pnetgpu_batch* b, const pnetgpu_rx_
             std::fprintf(stderr, "[pnetgpu] rx kind=%d regs=%d lds=%d blocks/cu=%d cus=%d\n", kind, numregs, lds,
                          per_cu, ctx->cus);
     }
-    const uint64_t want = (a.nruns + kWavesPerBlock - 1) / kWavesPerBlock;
+    const uint64_t wpb = (uint64_t)pnetgpu::rx_waves_per_block(kind);
+    const uint64_t want = (a.nruns + wpb - 1) / wpb;
     const uint64_t cap = (uint64_t)ctx->cus * (uint64_t)per_cu;
     const int blocks = (int)std::max<uint64_t>(1, std::min(want, cap));
     if (pnetgpu::launch_rx(a, kind, blocks, tx, static_cast<hipStream_t>(stream)) != 0) return PNETGPU_EHIP;

@@ -47,11 +47,13 @@ constexpr int kKindMixed = 0;
 constexpr int kKindSmall = 1;
 constexpr int kKindMtu = 2;
 constexpr int kKindJumbo = 3;
+constexpr int kKindStream = 4;   // rx_stream_kernel: fixed stride >= 1 KiB, LDS-DMA byte stream (receive only)
 
 // device index a context is bound to (abi.cpp)
 int ctx_device(const pnetgpu_ctx* ctx);
 
 int rx_blocks_per_cu(int kind, bool ext, int* numregs, int* lds);
+int rx_waves_per_block(int kind);
 int launch_rx(const RxArgs& args, int kind, int blocks, bool tx, hipStream_t stream);
 int launch_slices(const SliceArgs& args, int pseudo, int blocks, hipStream_t stream);
 
