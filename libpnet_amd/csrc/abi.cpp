@@ -127,14 +127,13 @@ static int rx_common(pnetgpu_ctx* ctx, const pnetgpu_batch* b, const pnetgpu_rx_
         // stream kernel (opt-in through PNETGPU_RX_KIND=4 until it beats the per-frame
         // kernels): contiguous frames >= 1 KiB apart with at most 1/8 of the span in gaps
         stream_ok = !tx && fits && b->stride >= 1024 && b->stride <= (1u << 20) && b->frame_len <= b->stride &&
-                    b->frame_len >= 256 &&
-                    (uint64_t)b->frame_len * 8 >= (uint64_t)b->stride * 7;
+                    b->frame_len >= 256 && (uint64_t)b->frame_len * 8 >= (uint64_t)b->stride * 7;
         if (base_sh == 0 && b->stride % 16 == 0 && b->frame_len <= 64 && fits && b->flags == 0)
             kind = pnetgpu::kKindSmall;
         else
             kind = b->frame_len >= 4096 ? pnetgpu::kKindJumbo : pnetgpu::kKindMtu;
     }
-    if (const char* e = std::getenv("PNETGPU_RX_KIND")) {          // tuning override (not the small kernel)
+    if (const char* e = std::getenv("PNETGPU_RX_KIND")) {          // tuning override
         const int v = std::atoi(e);
         if ((v == pnetgpu::kKindMixed || v == pnetgpu::kKindMtu || v == pnetgpu::kKindJumbo ||
              (v == pnetgpu::kKindStream && stream_ok)) &&

@@ -484,6 +484,115 @@ __device__ __forceinline__ SmallRun small_load(const RxArgs& a, uint64_t run, in
     return r;
 }
 
+// The small kernel's register fast path (frame bytes [0, 64) of a 16-B-aligned
+// frame in w[0..15]): IPv4 with IHL 5, and every frame the dispatch classifies
+// without reading past the Ethernet header, with every field at a compile-time
+// position. Returns true for the frames that need parse_frame (IPv6, IPv4
+// options or an IHL below 5); P, ipc and l4c are complete otherwise.
+// packetdump.rs:155-217, ipv4.rs:165-178, udp/tcp/icmp layouts and sizes.
+__device__ __forceinline__ bool small_fast(const uint32_t (&w)[16], uint32_t len, Parsed& P, uint32_t& ipc,
+                                           uint32_t& l4c) {
+    [[maybe_unused]] const uint32_t w0 = w[0], w1 = w[1], w2 = w[2];
+    const uint32_t w3 = w[3];
+    const uint32_t w4 = w[4], w5 = w[5], w6 = w[6], w7 = w[7];
+    const uint32_t w8 = w[8], w9 = w[9], w10 = w[10], w11 = w[11];
+    const uint32_t w12 = w[12], w13 = w[13], w14 = w[14], w15 = w[15];
+    bool slow = false;
+    if (len < 14) {
+        P.st = PNET_ST_ETH_MALFORMED;
+    } else {
+        P.et = bswap16(w3 & 0xFFFFu);
+        P.l3 = 14;
+        if (P.et == 0x0800u) {
+            if (len < 34) {
+                P.st = PNET_ST_L3_IPV4 | PNET_ST_L3_MALFORMED;
+            } else if (((w3 >> 16) & 0xFu) != 5u) {
+                slow = true;                       // IPv4 options / IHL clamp: generic path
+            } else {
+                // ---- fast path: IPv4, IHL 5; every position below is static ----
+                P.st = PNET_ST_L3_IPV4;
+                P.is_v4 = true;
+                const uint32_t eplen = len - 14;
+                const uint32_t tl = bswap16(w4 & 0xFFFFu);
+                P.ttl = (w5 >> 16) & 0xFFu;
+                P.proto = w5 >> 24;
+                P.ipstored = bswap16(w6 & 0xFFFFu);
+                P.s4 = (bswap16(w6 >> 16) << 16) | bswap16(w7 & 0xFFFFu);   // bytes 26..29
+                P.d4 = (bswap16(w7 >> 16) << 16) | bswap16(w8 & 0xFFFFu);   // bytes 30..33
+                // header sum [14,34) without the checksum word (bytes 24,25)
+                uint32_t tA = sad(w3 & 0xFFFF0000u, 0u);
+                tA = sad(w4, tA);
+                tA = sad(w5, tA);
+                tA = sad(w6 & 0xFFFF0000u, tA);
+                tA = sad(w7, tA);
+                tA = sad(w8 & 0x0000FFFFu, tA);
+                ipc = (~bswap16(fold16(tA))) & 0xFFFFu;
+                if (ipc == P.ipstored) P.st |= PNET_ST_IP_CSUM_OK;
+                const uint32_t plen = tl > 20u ? tl - 20u : 0u;
+                if (eplen > 20u) {
+                    P.l4off = 34;
+                    P.l4len = min(20u + plen, eplen) - 20u;
+                }
+                uint32_t kind = 0, minlen = 0;
+                switch (P.proto) {
+                    case 17: kind = PNET_ST_L4_UDP; minlen = 8; break;
+                    case 6: kind = PNET_ST_L4_TCP; minlen = 20; break;
+                    case 1: kind = PNET_ST_L4_ICMP; minlen = 4; break;
+                    case 58: kind = PNET_ST_L4_ICMPV6; minlen = 4; break;
+                    default: break;
+                }
+                if (!kind) {
+                    P.st |= PNET_ST_UNKNOWN_PROTO;
+                } else {
+                    P.st |= kind;
+                    if (P.l4len < minlen) {
+                        P.st |= PNET_ST_L4_MALFORMED;
+                    } else {
+                        P.sp = bswap16(w8 >> 16);                            // bytes 34,35
+                        uint32_t stored_le;
+                        if (P.proto == 17) {
+                            P.dp = bswap16(w9 & 0xFFFFu);
+                            stored_le = w10 & 0xFFFFu;                       // bytes 40,41
+                        } else if (P.proto == 6) {
+                            P.dp = bswap16(w9 & 0xFFFFu);
+                            stored_le = w12 >> 16;                           // bytes 50,51
+                        } else {
+                            P.dp = P.l4len >= 8 ? bswap16(w9 >> 16) : 0u;    // bytes 38,39
+                            stored_le = w9 & 0xFFFFu;                        // bytes 36,37
+                        }
+                        P.l4stored = bswap16(stored_le);
+                        P.l4csum_at = P.proto == 17 ? 40 : (P.proto == 6 ? 50 : 36);
+                        if (P.proto != 58) {       // ICMPv6 over IPv4: no checksum defined
+                            const int e = 34 + (int)P.l4len;
+                            uint32_t tB = sad(w8 & 0xFFFF0000u, 0u);
+                            tB = sad(w9 & first_bytes(clamp04(e - 36)), tB);
+                            tB = sad(w10 & first_bytes(clamp04(e - 40)), tB);
+                            tB = sad(w11 & first_bytes(clamp04(e - 44)), tB);
+                            tB = sad(w12 & first_bytes(clamp04(e - 48)), tB);
+                            tB = sad(w13 & first_bytes(clamp04(e - 52)), tB);
+                            tB = sad(w14 & first_bytes(clamp04(e - 56)), tB);
+                            tB = sad(w15 & first_bytes(clamp04(e - 60)), tB);
+                            tB -= stored_le;
+                            uint32_t pseudo = 0;
+                            if (P.proto != 1)
+                                pseudo = (P.s4 >> 16) + (P.s4 & 0xFFFFu) + (P.d4 >> 16) + (P.d4 & 0xFFFFu) +
+                                         P.proto + P.l4len;
+                            l4c = (~fold16(bswap16(fold16(tB)) + pseudo)) & 0xFFFFu;
+                            P.st |= PNET_ST_L4_CSUM_DONE;
+                            if (l4c == P.l4stored) P.st |= PNET_ST_L4_CSUM_OK;
+                        }
+                    }
+                }
+            }
+        } else if (P.et == 0x86DDu) {
+            slow = true;
+        } else {
+            P.st = PNET_ST_UNKNOWN_ETHERTYPE;
+        }
+    }
+    return slow;
+}
+
 #ifndef PNET_SMALL_WAVES
 #define PNET_SMALL_WAVES 4   // waves/SIMD the small kernel is register-bounded for
 #endif
@@ -520,109 +629,13 @@ __global__ __launch_bounds__(kBlock, PNET_SMALL_WAVES) void rx_small_kernel(RxAr
 #pragma unroll
             for (int c = 0; c < 4; ++c) cur.g[c] = *reinterpret_cast<const uint4*>(slot + 16 * c);
         }
-        [[maybe_unused]] const uint32_t w0 = cur.g[0].x, w1 = cur.g[0].y, w2 = cur.g[0].z;
-        const uint32_t w3 = cur.g[0].w;
-        const uint32_t w4 = cur.g[1].x, w5 = cur.g[1].y, w6 = cur.g[1].z, w7 = cur.g[1].w;
-        const uint32_t w8 = cur.g[2].x, w9 = cur.g[2].y, w10 = cur.g[2].z, w11 = cur.g[2].w;
-        const uint32_t w12 = cur.g[3].x, w13 = cur.g[3].y, w14 = cur.g[3].z, w15 = cur.g[3].w;
 
         Parsed P{};
         uint32_t ipc = 0, l4c = 0;
-        bool slow = false;
-        if (in_batch) {
-            if (len < 14) {
-                P.st = PNET_ST_ETH_MALFORMED;
-            } else {
-                P.et = bswap16(w3 & 0xFFFFu);
-                P.l3 = 14;
-                if (P.et == 0x0800u) {
-                    if (len < 34) {
-                        P.st = PNET_ST_L3_IPV4 | PNET_ST_L3_MALFORMED;
-                    } else if (((w3 >> 16) & 0xFu) != 5u) {
-                        slow = true;                       // IPv4 options / IHL clamp: generic path
-                    } else {
-                        // ---- fast path: IPv4, IHL 5; every position below is static ----
-                        P.st = PNET_ST_L3_IPV4;
-                        P.is_v4 = true;
-                        const uint32_t eplen = len - 14;
-                        const uint32_t tl = bswap16(w4 & 0xFFFFu);
-                        P.ttl = (w5 >> 16) & 0xFFu;
-                        P.proto = w5 >> 24;
-                        P.ipstored = bswap16(w6 & 0xFFFFu);
-                        P.s4 = (bswap16(w6 >> 16) << 16) | bswap16(w7 & 0xFFFFu);   // bytes 26..29
-                        P.d4 = (bswap16(w7 >> 16) << 16) | bswap16(w8 & 0xFFFFu);   // bytes 30..33
-                        // header sum [14,34) without the checksum word (bytes 24,25)
-                        uint32_t tA = sad(w3 & 0xFFFF0000u, 0u);
-                        tA = sad(w4, tA);
-                        tA = sad(w5, tA);
-                        tA = sad(w6 & 0xFFFF0000u, tA);
-                        tA = sad(w7, tA);
-                        tA = sad(w8 & 0x0000FFFFu, tA);
-                        ipc = (~bswap16(fold16(tA))) & 0xFFFFu;
-                        if (ipc == P.ipstored) P.st |= PNET_ST_IP_CSUM_OK;
-                        const uint32_t plen = tl > 20u ? tl - 20u : 0u;
-                        if (eplen > 20u) {
-                            P.l4off = 34;
-                            P.l4len = min(20u + plen, eplen) - 20u;
-                        }
-                        uint32_t kind = 0, minlen = 0;
-                        switch (P.proto) {
-                            case 17: kind = PNET_ST_L4_UDP; minlen = 8; break;
-                            case 6: kind = PNET_ST_L4_TCP; minlen = 20; break;
-                            case 1: kind = PNET_ST_L4_ICMP; minlen = 4; break;
-                            case 58: kind = PNET_ST_L4_ICMPV6; minlen = 4; break;
-                            default: break;
-                        }
-                        if (!kind) {
-                            P.st |= PNET_ST_UNKNOWN_PROTO;
-                        } else {
-                            P.st |= kind;
-                            if (P.l4len < minlen) {
-                                P.st |= PNET_ST_L4_MALFORMED;
-                            } else {
-                                P.sp = bswap16(w8 >> 16);                            // bytes 34,35
-                                uint32_t stored_le;
-                                if (P.proto == 17) {
-                                    P.dp = bswap16(w9 & 0xFFFFu);
-                                    stored_le = w10 & 0xFFFFu;                       // bytes 40,41
-                                } else if (P.proto == 6) {
-                                    P.dp = bswap16(w9 & 0xFFFFu);
-                                    stored_le = w12 >> 16;                           // bytes 50,51
-                                } else {
-                                    P.dp = P.l4len >= 8 ? bswap16(w9 >> 16) : 0u;    // bytes 38,39
-                                    stored_le = w9 & 0xFFFFu;                        // bytes 36,37
-                                }
-                                P.l4stored = bswap16(stored_le);
-                                P.l4csum_at = P.proto == 17 ? 40 : (P.proto == 6 ? 50 : 36);
-                                if (P.proto != 58) {       // ICMPv6 over IPv4: no checksum defined
-                                    const int e = 34 + (int)P.l4len;
-                                    uint32_t tB = sad(w8 & 0xFFFF0000u, 0u);
-                                    tB = sad(w9 & first_bytes(clamp04(e - 36)), tB);
-                                    tB = sad(w10 & first_bytes(clamp04(e - 40)), tB);
-                                    tB = sad(w11 & first_bytes(clamp04(e - 44)), tB);
-                                    tB = sad(w12 & first_bytes(clamp04(e - 48)), tB);
-                                    tB = sad(w13 & first_bytes(clamp04(e - 52)), tB);
-                                    tB = sad(w14 & first_bytes(clamp04(e - 56)), tB);
-                                    tB = sad(w15 & first_bytes(clamp04(e - 60)), tB);
-                                    tB -= stored_le;
-                                    uint32_t pseudo = 0;
-                                    if (P.proto != 1)
-                                        pseudo = (P.s4 >> 16) + (P.s4 & 0xFFFFu) + (P.d4 >> 16) + (P.d4 & 0xFFFFu) +
-                                                 P.proto + P.l4len;
-                                    l4c = (~fold16(bswap16(fold16(tB)) + pseudo)) & 0xFFFFu;
-                                    P.st |= PNET_ST_L4_CSUM_DONE;
-                                    if (l4c == P.l4stored) P.st |= PNET_ST_L4_CSUM_OK;
-                                }
-                            }
-                        }
-                    }
-                } else if (P.et == 0x86DDu) {
-                    slow = true;
-                } else {
-                    P.st = PNET_ST_UNKNOWN_ETHERTYPE;
-                }
-            }
-        }
+        const uint32_t wv16[16] = {cur.g[0].x, cur.g[0].y, cur.g[0].z, cur.g[0].w, cur.g[1].x, cur.g[1].y,
+                                   cur.g[1].z, cur.g[1].w, cur.g[2].x, cur.g[2].y, cur.g[2].z, cur.g[2].w,
+                                   cur.g[3].x, cur.g[3].y, cur.g[3].z, cur.g[3].w};
+        const bool slow = in_batch && small_fast(wv16, len, P, ipc, l4c);
         // ---- generic path through LDS for the lanes the fast path did not take ----
         const bool need_v6 = a.cols.src_ipv6 || a.cols.dst_ipv6;
 #ifdef PNET_SMALL_NOSLOW
@@ -1149,7 +1162,6 @@ __global__ __launch_bounds__(kWave) void rx_stream_kernel(RxArgs a) {
             const int wo0 = (int)x - (int)(wn ? bg : bf);
             uint8_t* wslot = L.win + (f + (wn ? 1u : 0u)) * kSlot + wo0;
             const uint32_t ce = dte < 64u ? (dte >> 4) : 4u;
-#ifndef PNET_STREAM_NOWIN   // tuning experiment only: results are wrong
 #pragma unroll
             for (int c = 0; c < 4; ++c) {
                 if ((uint32_t)(wo0 + 16 * c) < (uint32_t)kWin) {
@@ -1158,16 +1170,10 @@ __global__ __launch_bounds__(kWave) void rx_stream_kernel(RxArgs a) {
                 }
                 if (ce == (uint32_t)c) L.endg[f] = g[c];
             }
-#endif
         }
         wave_sync();
 
         // ---- parse + window sums + stores (as rx_kernel steps 4-5) ---------
-#ifdef PNET_STREAM_NOPARSE   // tuning experiment only: results are wrong
-        if (lane < nf) reinterpret_cast<uint16_t*>(a.cols.status)[f0 + lane] = (uint16_t)(L.pte[lane] - L.pts[lane]);
-        wave_sync();
-        continue;
-#endif
         const bool in_batch = (uint32_t)lane < nf;
         const uint64_t off = rs.off0 + (uint64_t)lane * stride;
         const uint32_t len = in_batch ? flen : 0u;
@@ -1175,16 +1181,10 @@ __global__ __launch_bounds__(kWave) void rx_stream_kernel(RxArgs a) {
         const uint64_t base_g = off - (uint64_t)sh;
         const uint32_t fend = (uint32_t)sh + len;
         Parsed P{};
-#ifndef PNET_XP_NOPF
         if (in_batch) P = parse_frame(FrameBytes{slot + sh, a.data + off, kWin - sh}, len, EXT ? a.flags : 0u);
-#else
-        P.st = PNET_ST_L3_IPV4; P.is_v4 = true; P.l4do = true; P.a_lo = 14; P.a_hi = 34; P.b_lo = 34; P.b_hi = (int)len; P.et = slot[sh + 12];
-#endif
         const int p0 = P.a_lo + sh, p1 = P.a_hi + sh, p2 = P.b_lo + sh, p3 = P.b_hi + sh;
         uint32_t tA = 0, tB = 0;
-#ifndef PNET_XP_NOWS
         window_sums(slot, p0, p1, min(p2, kWin), min(p3, kWin), tA, tB);
-#endif
         if (P.l4do && p3 > kWin) {
             // slot bytes [128, fend) = P(TE) - P(TS) + the end granule's bytes below fend
             const int e = (int)((fend - 1u) & 15u) + 1;
@@ -1202,11 +1202,7 @@ __global__ __launch_bounds__(kWave) void rx_stream_kernel(RxArgs a) {
         uint32_t ipc = 0, l4c = 0;
         finalize(P, tA, tB, (off & 1) != 0, ipc, l4c);
         st_mark = icount;
-#ifndef PNET_XP_NOST
         store_columns(a.cols, f0, lane, in_batch, P, ipc, l4c, slot, sh);
-#else
-        if (in_batch) a.cols.status[f0 + lane] = (uint16_t)(P.st + ipc + l4c);
-#endif
         if (a.cols.counters) K.add(in_batch, len, P.st);
         wave_sync();   // slots and records are rewritten by the next run
     }
