@@ -84,7 +84,7 @@ __global__ __launch_bounds__(64) void rw_kernel(const uint8_t* __restrict__ in, 
         const uint4 v = *reinterpret_cast<const uint4*>(&ring[cslot * kStep + 64 * lane]);
         const uint32_t x = v.x ^ v.y ^ v.z ^ v.w;
         acc += x;
-        if (sthis) {
+        if (sthis && MODE != 3) {
             if (MODE == 2) wait_vm<0>();   // drain every load before the stores
 #pragma unroll
             for (int k = 0; k < K; ++k)
@@ -92,6 +92,15 @@ __global__ __launch_bounds__(64) void rw_kernel(const uint8_t* __restrict__ in, 
             if (MODE == 1) issue();
         }
         cslot = cslot == S - 1 ? 0 : cslot + 1;
+    }
+    if (MODE == 3) {   // every deferred store of the range at the end
+        for (size_t s = sbeg; s < send; ++s) {
+            if (EVERY == 1 || s % EVERY == 0) {
+#pragma unroll
+                for (int k = 0; k < K; ++k)
+                    st<NB, NT>(out + (s / EVERY) * kW + (size_t)k * 64 * NB + (size_t)lane * NB, acc + k);
+            }
+        }
     }
     if (acc == 0x12345678u) o[0] = acc;
 }
@@ -145,6 +154,10 @@ int main() {
     rw("r + 1x 128B nt every 24", rw_kernel<2, 1, true, 24>, 128 / 24);
     rw("r + 2x 1KiB nt every 24", rw_kernel<16, 2, true, 24>, 2048 / 24);
     rw("r + 2x 1KiB nt every 24, same addr", rw_kernel<16, 2, true, 24, true>, 2048 / 24);
+    rw("r + 16x 128B nt every 24, at end", rw_kernel<2, 16, true, 24, false, 3>, 2048 / 24);
+    rw("r + 2x 1KiB nt every 24, at end", rw_kernel<16, 2, true, 24, false, 3>, 2048 / 24);
+    rw("r + 13x 128B nt every step, at end", rw_kernel<2, 13, true, 1, false, 3>, 1664);
+    rw("r + 13x 128B nt every step", rw_kernel<2, 13, true, 1, false, 0>, 1664);
     rw("r + 8x 1KiB nt every 96", rw_kernel<16, 8, true, 96>, 8192 / 96);
     rw("r + 32x 1KiB nt every 384", rw_kernel<16, 32, true, 384>, 32768 / 384);
     rw("r + 8x 1KiB plain every 96", rw_kernel<16, 8, false, 96>, 8192 / 96);
