@@ -24,6 +24,16 @@ __device__ __forceinline__ void glds16_nt_s(const void* sbase, uint32_t voff, ui
 template <int N>
 __device__ __forceinline__ void wait_vm() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
 
+// dword store with explicit gfx950 cache-policy bits (POL: 0 none, 1 nt, 2 sc0 sc1, 3 sc0 sc1 nt, 4 sc1, 5 sc0)
+template <int POL>
+__device__ __forceinline__ void st_pol(uint8_t* p, uint32_t x) {
+    if constexpr (POL == 0) asm volatile("global_store_dword %0, %1, off" ::"v"(p), "v"(x) : "memory");
+    else if constexpr (POL == 1) asm volatile("global_store_dword %0, %1, off nt" ::"v"(p), "v"(x) : "memory");
+    else if constexpr (POL == 2) asm volatile("global_store_dword %0, %1, off sc0 sc1" ::"v"(p), "v"(x) : "memory");
+    else if constexpr (POL == 3) asm volatile("global_store_dword %0, %1, off sc0 sc1 nt" ::"v"(p), "v"(x) : "memory");
+    else if constexpr (POL == 4) asm volatile("global_store_dword %0, %1, off sc1" ::"v"(p), "v"(x) : "memory");
+    else asm volatile("global_store_dword %0, %1, off sc0" ::"v"(p), "v"(x) : "memory");
+}
 template <int NB, bool NT>
 __device__ __forceinline__ void st(uint8_t* p, uint32_t x) {
     if constexpr (NB == 16) {
@@ -105,6 +115,86 @@ __global__ __launch_bounds__(64) void rw_kernel(const uint8_t* __restrict__ in, 
     if (acc == 0x12345678u) o[0] = acc;
 }
 
+// register-staged read stream (2 steps of 4 KiB in flight per wave) + the same sparse writes
+template <int NB, int K, int EVERY, int WPB>
+__global__ __launch_bounds__(64 * WPB) void rw_reg_kernel(const uint8_t* __restrict__ in, size_t bytes, uint8_t* out,
+                                                          uint32_t* o) {
+    const int lane = threadIdx.x & 63;
+    const size_t nsteps = bytes / 4096;
+    const size_t nw = (size_t)gridDim.x * WPB, w = (size_t)blockIdx.x * WPB + (threadIdx.x >> 6);
+    const size_t q = nsteps / nw, rem = nsteps % nw;
+    const size_t sbeg = q * w + min(w, rem), send = sbeg + q + (w < rem ? 1 : 0);
+    typedef unsigned int v4 __attribute__((ext_vector_type(4)));
+    auto ld = [&](size_t st, uint4* v) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            v4 t = __builtin_nontemporal_load(reinterpret_cast<const v4*>(in + st * 4096 + 1024 * i + 16 * lane));
+            v[i] = make_uint4(t.x, t.y, t.z, t.w);
+        }
+    };
+    uint4 a[4], b[4];
+    if (sbeg < send) ld(sbeg, a);
+    if (sbeg + 1 < send) ld(sbeg + 1, b);
+    uint32_t acc = 0;
+    constexpr size_t kW = (size_t)64 * NB * K;
+    for (size_t s = sbeg; s < send; ++s) {
+        uint32_t x = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) x += a[i].x ^ a[i].y ^ a[i].z ^ a[i].w;
+        acc += x;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) a[i] = b[i];
+        if (s + 2 < send) ld(s + 2, b);
+        if (K > 0 && s % EVERY == 0) {
+#pragma unroll
+            for (int k = 0; k < K; ++k) st<NB, true>(out + (s / EVERY) * kW + (size_t)k * 64 * NB + (size_t)lane * NB, x + k);
+        }
+    }
+    if (acc == 0x12345678u) o[0] = acc;
+}
+
+// LDS-DMA read stream + K dword stores (256 B per instruction) every EVERY steps, policy POL
+template <int K, int EVERY, int POL>
+__global__ __launch_bounds__(64) void rw_pol_kernel(const uint8_t* __restrict__ in, size_t bytes, uint8_t* out, uint32_t* o) {
+    constexpr int S = 3, kStep = 4096;
+    __shared__ __attribute__((aligned(16))) uint8_t ring[S * kStep + 10240];
+    const int lane = threadIdx.x;
+    const size_t nsteps = bytes / kStep;
+    const size_t nw = gridDim.x, w = blockIdx.x;
+    const size_t q = nsteps / nw, rem = nsteps % nw;
+    const size_t sbeg = q * w + min(w, rem), send = sbeg + q + (w < rem ? 1 : 0);
+    const uint32_t src_off = (uint32_t)(lane & ~3) * 16u + ((uint32_t)((lane & 3) - (lane >> 4)) & 3u) * 16u;
+    const uint32_t ring0 = (uint32_t)(uintptr_t)(lds_ptr_t)&ring[0];
+    size_t is = sbeg;
+    uint32_t islot = 0;
+    auto issue = [&]() {
+        if (is >= send) return;
+        const uint8_t* sp = in + is * kStep;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) glds16_nt_s(sp, src_off + 1024u * i, ring0 + islot * kStep + 1024u * i);
+        islot = islot == S - 1 ? 0 : islot + 1;
+        ++is;
+    };
+    issue(); issue();
+    uint32_t acc = 0, cslot = 0;
+    constexpr size_t kW = (size_t)256 * K;
+    for (size_t s = sbeg; s < send; ++s) {
+        issue();
+        if (s + S - 1 < send) wait_vm<(4 * (S - 1) + K * (S - 1) > 63 ? 63 : 4 * (S - 1) + K * (S - 1))>();
+        else wait_vm<0>();
+        const uint4 v = *reinterpret_cast<const uint4*>(&ring[cslot * kStep + 64 * lane]);
+        const uint32_t x = v.x ^ v.y ^ v.z ^ v.w;
+        acc += x;
+        if (K > 0 && s % EVERY == 0) {
+#pragma unroll
+            for (int k = 0; k < K; ++k) st_pol<POL>(out + (s / EVERY) * kW + (size_t)k * 256 + (size_t)lane * 4, x + k);
+        }
+        cslot = cslot == S - 1 ? 0 : cslot + 1;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (acc == 0x12345678u) o[0] = acc;
+}
+
 template <class F>
 float time_it(F f, int reps) {
     hipEvent_t a, b;
@@ -154,6 +244,31 @@ int main() {
     rw("r + 1x 128B nt every 24", rw_kernel<2, 1, true, 24>, 128 / 24);
     rw("r + 2x 1KiB nt every 24", rw_kernel<16, 2, true, 24>, 2048 / 24);
     rw("r + 2x 1KiB nt every 24, same addr", rw_kernel<16, 2, true, 24, true>, 2048 / 24);
+    auto rwr = [&](const char* label, auto kern, int wpb, size_t wstep) {
+        int nb = 0;
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, 64 * wpb, 0);
+        const int grid = 256 * nb;
+        kern<<<grid, 64 * wpb>>>(in, rbytes, out, o);
+        CK(hipDeviceSynchronize());
+        float ms = time_it([&] { kern<<<grid, 64 * wpb>>>(in, rbytes, out, o); }, 20);
+        const double wb = (double)(rbytes / 4096) * wstep;
+        printf("%-40s waves/CU=%2d: %7.1f us %6.0f GB/s (w %0.0f MB)\n", label, nb * wpb, ms * 1e3,
+               (rbytes + wb) / ms / 1e6, wb / 1e6);
+        return 0;
+    };
+    rw("pol none  8x256B every 24", rw_pol_kernel<8, 24, 0>, 2048 / 24);
+    rw("pol nt    8x256B every 24", rw_pol_kernel<8, 24, 1>, 2048 / 24);
+    rw("pol sc0sc1 8x256B every 24", rw_pol_kernel<8, 24, 2>, 2048 / 24);
+    rw("pol sc0sc1nt 8x256B every 24", rw_pol_kernel<8, 24, 3>, 2048 / 24);
+    rw("pol sc1   8x256B every 24", rw_pol_kernel<8, 24, 4>, 2048 / 24);
+    rw("pol sc0   8x256B every 24", rw_pol_kernel<8, 24, 5>, 2048 / 24);
+    rw("pol none  7x256B every step", rw_pol_kernel<7, 1, 0>, 1792);
+    rw("pol nt    7x256B every step", rw_pol_kernel<7, 1, 1>, 1792);
+    rw("pol sc0sc1 7x256B every step", rw_pol_kernel<7, 1, 2>, 1792);
+    rw("pol sc0sc1nt 7x256B every step", rw_pol_kernel<7, 1, 3>, 1792);
+    rwr("reg read only", rw_reg_kernel<2, 0, 24, 4>, 4, 0);
+    rwr("reg r + 16x 128B nt every 24", rw_reg_kernel<2, 16, 24, 4>, 4, 2048 / 24);
+    rwr("reg r + 2x 1KiB nt every 24", rw_reg_kernel<16, 2, 24, 4>, 4, 2048 / 24);
     rw("r + 16x 128B nt every 24, at end", rw_kernel<2, 16, true, 24, false, 3>, 2048 / 24);
     rw("r + 2x 1KiB nt every 24, at end", rw_kernel<16, 2, true, 24, false, 3>, 2048 / 24);
     rw("r + 13x 128B nt every step, at end", rw_kernel<2, 13, true, 1, false, 3>, 1664);
