@@ -10,7 +10,7 @@ L4 offset/length, ports, addresses) plus counters. Multi-GPU: one process per
 GPU (torchrun), each with its own shard (weak scaling, no data-path collective);
 RCCL only all-reduces the counters once at the end and takes the max time.
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu] [--no-e2e]
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu] [--no-e2e] [--no-extra]
 """
 import argparse
 import json
@@ -205,6 +205,72 @@ def e2e_ring_rate(sh, seconds=3.0):
                     "columns, 3 rotating slots of 1 Mi frames"}
 
 
+def time_launches(fn, steps, warmup, stream):
+    """Average duration (ms) of `steps` launches of fn(stream), HIP events on that stream."""
+    for _ in range(warmup):
+        fn(stream)
+    stream.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    for a, b in ev:
+        a.record(stream)
+        fn(stream)
+        b.record(stream)
+    stream.synchronize()
+    return float(np.mean([a.elapsed_time(b) for a, b in ev]))
+
+
+def tx_fill_rate(sh, steps, warmup, device):
+    """Sender side (configs[0] builds and checksums frames
+    the way benches/rs_sender.rs:38-39,70-71 does): pnetgpu_tx_fill_checksums over
+    a device copy of the batch, every IPv4 header and L4 checksum written in place,
+    plus the status column. Beside it, the oracle's scalar oracle_tx_fill on one
+    core over the first 2^20 frames."""
+    from oracle import coracle  # CPU baseline only
+    w = sh.w
+    if not w.stride:
+        return None
+    data = sh.data.clone()
+    res = lp.RxResult(sh.n, device, ("status",), counters=False)
+    stream = torch.cuda.Stream(device)
+    ms = time_launches(lambda s: lp.tx_fill_checksums(data, stride=w.stride, frame_len=w.frame_len, n_frames=sh.n,
+                                                      out=res, stream=s), steps, warmup, stream)
+    alg = sh.frame_bytes + sh.n * (4 + 2)   # frames read, two checksum fields + status written
+    n1 = min(sh.n, 1 << 20)
+    t0 = time.perf_counter()
+    coracle.tx_fill(w.buf[: n1 * w.stride], n1, stride=w.stride, frame_len=w.frame_len)
+    cpu = n1 / (time.perf_counter() - t0) / 1e6
+    del data
+    return {"mpkts_s": round(sh.n / (ms * 1e-3) / 1e6, 1), "kernel_avg_ms": round(ms, 4),
+            "achieved_gbs": round(alg / (ms * 1e-3) / 1e9, 1), "frac": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "cpu_port_1core_mpkts_s": round(cpu, 2),
+            "note": "device-resident tx_fill_checksums (IPv4 header + L4 checksum patched in place), kernel time; "
+                    f"CPU: oracle_tx_fill, 1 core, first {n1} frames"}
+
+
+def slices_rate(sh, steps, warmup, device):
+    """Batched util::ipv4_checksum (pnetgpu_ipv4_checksum_slices, the
+    tcp::ipv4_checksum call of tcp.rs:239-248) over every TCP segment of the
+    1500-B batch: slice = frame[34, 1500), skipword 8, the frame's own addresses."""
+    w = sh.w
+    if not w.stride or sh.name != "tcp1500":
+        return None
+    n = sh.n
+    base = np.arange(n, dtype=np.int64) * w.stride
+    offs = torch.from_numpy(base + 34).to(device)
+    lens = torch.full((n,), w.frame_len - 34, dtype=torch.int32, device=device)
+    skips = torch.full((n,), 8, dtype=torch.int32, device=device)
+    frames = w.buf[: n * w.stride].reshape(n, w.stride)
+    addrs = torch.from_numpy(np.ascontiguousarray(frames[:, 26:34])).to(device)
+    protos = torch.full((n,), 6, dtype=torch.uint8, device=device)
+    stream = torch.cuda.Stream(device)
+    ms = time_launches(lambda s: lp.ipv4_checksum_slices(sh.data, offs, lens, skips, addrs, protos, stream=s),
+                       steps, warmup, stream)
+    alg = n * (w.frame_len - 34 + 8 + 12 + 4 + 1 + 2)   # slice + addrs + descriptor + skipword + proto + result
+    return {"mslices_s": round(n / (ms * 1e-3) / 1e6, 1), "kernel_avg_ms": round(ms, 4),
+            "achieved_gbs": round(alg / (ms * 1e-3) / 1e9, 1), "frac": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "note": f"{n} TCP segments of {w.frame_len - 34} B, util::ipv4_checksum per slice, kernel time"}
+
+
 def load_traffic(workload):
     """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/), if present."""
     p = os.path.join(ROOT, "profiles", f"pmc_{workload}.json")
@@ -226,6 +292,7 @@ def main():
     ap.add_argument("--workloads", default="udp64,tcp1500")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--no-extra", action="store_true", help="skip the TX-fill and checksum-slices rates")
     ap.add_argument("--seed", type=int, default=1)
     args = ap.parse_args()
 
@@ -330,6 +397,11 @@ def main():
             for name, r in results.items():
                 if name != primary:
                     line["workloads"][name]["cpu_baseline"] = cpu_baseline(r["sh"], budget_cpu_s=6.0)
+        if world == 1 and not args.no_extra:
+            line["tx_fill"] = tx_fill_rate(sh, args.steps, args.warmup, device)
+            if "tcp1500" in results:
+                line["workloads"]["tcp1500"]["ipv4_checksum_slices"] = slices_rate(results["tcp1500"]["sh"], args.steps,
+                                                                                   args.warmup, device)
         if world == 1 and not args.no_e2e:
             line["e2e_pcie"] = e2e_rate(sh, device)
             line["e2e_ring"] = e2e_ring_rate(sh)

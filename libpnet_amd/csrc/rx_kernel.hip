@@ -652,8 +652,27 @@ __global__ __launch_bounds__(kBlock, PNET_SMALL_WAVES) void rx_small_kernel(RxAr
                 finalize(P, tA, tB, false, ipc, l4c);
             }
         }
-        if (TX && in_batch)
-            tx_write(const_cast<uint8_t*>(a.data) + (a.first + a.delta) + (f0 + lane) * a.stride, P, ipc, l4c);
+        if (TX) {
+            // patch the frame's LDS copy, then write the run's granules back the
+            // way they were loaded (four coalesced 1-KiB wave stores): whole
+            // lines instead of four scattered byte stores per frame, which left
+            // every line of the batch partially dirty (0.63 ms -> see DESIGN.md)
+            if (in_batch) tx_write(slot, P, ipc, l4c);
+            wave_sync();
+            const uint32_t span = (a.frame_len + 15u) >> 4;
+            const uint32_t c = (uint32_t)(lane & 3);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const uint64_t f = f0 + 16 * i + (lane >> 2);
+                if (f < a.n && c < span) {
+                    const uint4 v = *reinterpret_cast<const uint4*>(lds_slots[wv] + (16 * i + (lane >> 2)) * kSmallSlot +
+                                                                    16 * c);
+                    __builtin_nontemporal_store(u32x4_t{v.x, v.y, v.z, v.w},
+                                                reinterpret_cast<u32x4_t*>(const_cast<uint8_t*>(a.data) +
+                                                                           (a.first + a.delta) + f * a.stride + 16u * c));
+                }
+            }
+        }
         store_columns(a.cols, f0, lane, in_batch, P, ipc, l4c, slot, 0);
         if (a.cols.counters) K.add(in_batch, len, P.st);
         wave_sync();
