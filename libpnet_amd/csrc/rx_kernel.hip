@@ -1235,24 +1235,38 @@ __global__ __launch_bounds__(kWave) void rx_stream_kernel(RxArgs a) {
 // 16-B granules, masked sums, shuffle reduce, lane 0 of the group finalizes.
 
 // Weighted byte sum of [off, off+len) (absolute offsets into a.data) by one
-// 16-lane group: coalesced aligned granules, masked at both ends, shuffle-reduced
-// so every lane of the group returns the total.
+// 16-lane group: coalesced aligned granules, U loads in flight per lane (the
+// 16 lanes cover 256 B per load round), byte masks only on the slice's first
+// and last granule, shuffle-reduced so every lane of the group returns the total.
 __device__ __forceinline__ uint32_t group_range_sum(const uint8_t* data, uint64_t off, uint32_t len, int j) {
-    constexpr int G = 16;
+    constexpr int G = 16, U = 4;
     const int sh = (int)(off & 15);
     const uint8_t* fb = data + (off - (uint64_t)sh);
     const int e = sh + (int)len;
     const uint32_t nneed = len ? (uint32_t)((e + 15) >> 4) : 0u;
     uint32_t acc = 0;
 #pragma unroll 1
-    for (uint32_t c = j; c < nneed; c += G) {
-        const uint4 v = *reinterpret_cast<const uint4*>(fb + 16u * c);
-        const uint32_t dw[4] = {v.x, v.y, v.z, v.w};
-        const int p = (int)(16u * c);
+    for (uint32_t c0 = j; c0 < nneed; c0 += G * U) {
+        uint4 v[U];
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            const uint32_t mk = first_bytes(clamp04(e - p - 4 * t)) & ~first_bytes(clamp04(sh - p - 4 * t));
-            acc = sad(dw[t] & mk, acc);
+        for (int u = 0; u < U; ++u) {
+            const uint32_t c = c0 + u * G;
+            v[u] = c < nneed ? *reinterpret_cast<const uint4*>(fb + 16u * c) : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t c = c0 + u * G;
+            const uint32_t dw[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+            if (c == 0 || c + 1 == nneed) {          // edge granule (zero when c >= nneed)
+                const int p = (int)(16u * c);
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    const uint32_t mk = first_bytes(clamp04(e - p - 4 * t)) & ~first_bytes(clamp04(sh - p - 4 * t));
+                    acc = sad(dw[t] & mk, acc);
+                }
+            } else {
+                acc = sad(dw[3], sad(dw[2], sad(dw[1], sad(dw[0], acc))));
+            }
         }
     }
 #pragma unroll
