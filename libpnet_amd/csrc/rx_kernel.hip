@@ -15,8 +15,10 @@
 //                   loads are issued before the current run is processed
 //                   (software pipelining). IPv4 with IHL 5 (and every trivially
 //                   classified frame) takes a register-only fast path with
-//                   compile-time field positions; anything else (IPv6, IPv4
-//                   options) takes the generic parse on its LDS slot.
+//                   compile-time field positions (small_fast); anything else
+//                   (IPv6, IPv4 options) takes the generic parse on its LDS
+//                   slot. TX patches the LDS copy and writes the run back with
+//                   the same four coalesced 1-KiB wave instructions.
 //
 //  rx_kernel        everything else (descriptor mode, any alignment, any size).
 //                   Per run: descriptors (prefetched a run ahead); the window
@@ -29,6 +31,12 @@
 //                   and trims the tail sum to the L4 range. Shapes per kind
 //                   (mixed / MTU / jumbo) and the unified pass, where the group
 //                   loop also fills the window, are at the end of this file.
+//
+//  rx_stream_kernel opt-in (PNETGPU_RX_KIND=4) for fixed strides >= 1 KiB: each
+//                   wave streams its contiguous frame range through an LDS-DMA
+//                   ring (global_load_lds_dwordx4) and derives every frame's
+//                   tail from prefix sums of the byte stream; bit-exact, 1.00x
+//                   traffic, slower than rx_kernel here.
 //
 //  slice_kernel     the batched util::checksum / ipv4_checksum / ipv6_checksum
 //                   (and *_adv) entry points: 16 lanes per slice.
@@ -1234,12 +1242,15 @@ __global__ __launch_bounds__(kWave) void rx_stream_kernel(RxArgs a) {
 // One group of 16 lanes per slice (4 slices per wave per step): coalesced
 // 16-B granules, masked sums, shuffle reduce, lane 0 of the group finalizes.
 
+#ifndef PNET_SLICE_U
+#define PNET_SLICE_U 4   // loads in flight per lane in the slice kernels
+#endif
 // Weighted byte sum of [off, off+len) (absolute offsets into a.data) by one
 // 16-lane group: coalesced aligned granules, U loads in flight per lane (the
 // 16 lanes cover 256 B per load round), byte masks only on the slice's first
 // and last granule, shuffle-reduced so every lane of the group returns the total.
 __device__ __forceinline__ uint32_t group_range_sum(const uint8_t* data, uint64_t off, uint32_t len, int j) {
-    constexpr int G = 16, U = 4;
+    constexpr int G = 16, U = PNET_SLICE_U;
     const int sh = (int)(off & 15);
     const uint8_t* fb = data + (off - (uint64_t)sh);
     const int e = sh + (int)len;
