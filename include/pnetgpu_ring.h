@@ -61,6 +61,28 @@ int pnetgpu_ring_push_many(pnetgpu_ring* ring, const uint8_t* buf, const uint64_
                            const uint32_t* lengths, uint64_t n, uint64_t* pushed);
 /* Ship the filling batch (no-op returning 0 with *id = UINT64_MAX if empty). */
 int pnetgpu_ring_submit(pnetgpu_ring* ring, uint64_t* id);
+/* Zero-copy submit: ship frames base[offsets[i], +lengths[i]) straight from the
+ * caller's memory (one H2D of their span; no copy into the ring's pinned batch).
+ * The frames must ascend without overlapping; the longest prefix whose span and
+ * count fit the ring's batch is taken (*taken; then call again with the rest).
+ * The region must stay unchanged and alive until the batch has been waited, and
+ * the waited batch's `frames` points into it (offsets rebased to offsets[0]).
+ * With memory registered through pnetgpu_host_register (e.g. an mmap of a pcap
+ * file or of an AF_PACKET TPACKET ring) the copy is a direct DMA; pageable memory
+ * works too, at the HIP runtime's staged-copy rate. Returns 0, PNETGPU_EBUSY
+ * (wait first), PNETGPU_EFULL (frames were pushed into the filling batch: submit
+ * them first; or the first frame exceeds batch_bytes) or PNETGPU_EINVAL. */
+int pnetgpu_ring_submit_region(pnetgpu_ring* ring, const uint8_t* base, const uint64_t* offsets,
+                               const uint32_t* lengths, uint64_t n, uint64_t* taken, uint64_t* id);
+/* Columns later submissions compute and copy back: bit k selects the k-th
+ * column of pnetgpu_rx_columns in struct order (status = bit 0 ... l3_offset =
+ * bit 15); default all 16. A waited batch's unselected columns are NULL. Fewer
+ * columns = fewer result bytes over PCIe (all 16: 61 B/frame; the IPv4 set,
+ * bits 0-11: 26 B/frame). */
+int pnetgpu_ring_set_columns(pnetgpu_ring* ring, uint32_t column_mask);
+/* Page-lock existing host memory for direct DMA (hipHostRegister) and undo it. */
+int pnetgpu_host_register(void* p, uint64_t bytes);
+int pnetgpu_host_unregister(void* p);
 /* Block for the oldest submitted batch: 0 (fills *out) or PNETGPU_EEMPTY. */
 int pnetgpu_ring_wait(pnetgpu_ring* ring, pnetgpu_ring_batch* out);
 
@@ -71,6 +93,13 @@ typedef struct pnetgpu_pcap pnetgpu_pcap;
 int  pnetgpu_pcap_open(const char* path, pnetgpu_pcap** out);
 int  pnetgpu_pcap_next(pnetgpu_pcap* p, const uint8_t** frame, uint32_t* len);
 void pnetgpu_pcap_close(pnetgpu_pcap* p);
+/* Index an in-memory classic pcap image (e.g. an mmap of the whole file) for
+ * pnetgpu_ring_submit_region: from byte *pos (0 = start of file) fill up to cap
+ * record descriptors (offset of each record's captured bytes in img, incl_len),
+ * *n = records found, *pos = where the next call resumes (img_bytes at the end).
+ * PNETGPU_EFORMAT for a bad header or a truncated record. */
+int pnetgpu_pcap_scan(const uint8_t* img, uint64_t img_bytes, uint64_t* pos, uint64_t* offsets, uint32_t* lengths,
+                      uint64_t cap, uint64_t* n);
 
 #ifdef __cplusplus
 }

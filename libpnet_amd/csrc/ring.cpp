@@ -40,6 +40,8 @@ struct Slot {
     uint32_t n = 0;
     uint64_t bytes = 0;
     uint64_t id = 0;
+    const uint8_t* frames_view = nullptr;   // what the waited batch's `frames` points at
+    uint32_t col_mask = 0;                   // columns this batch computed
     SlotState state = kFree;
 };
 
@@ -59,6 +61,7 @@ struct pnetgpu_ring {
     uint64_t cap_bytes = 0;
     uint32_t cap_frames = 0;
     uint32_t flags = 0;
+    uint32_t col_mask = (1u << kNumCols) - 1;   // columns computed and copied back (bit k: struct order)
     Slot slots[kSlots];
     int filling = -1;
     int held = -1;
@@ -221,16 +224,15 @@ int pnetgpu_ring_push_many(pnetgpu_ring* r, const uint8_t* buf, const uint64_t* 
     return PNETGPU_OK;
 }
 
-int pnetgpu_ring_submit(pnetgpu_ring* r, uint64_t* id) {
-    if (!r) return PNETGPU_EINVAL;
-    if (id) *id = UINT64_MAX;
-    if (r->filling < 0) return PNETGPU_OK;
-    Slot& s = r->slots[r->filling];
-    if (s.n == 0) return PNETGPU_OK;
+// Ship slot s: H2D of the frames from `src` (the slot's pinned batch, or a
+// caller region for submit_region) and of the descriptors, receive kernel, D2H
+// of every record column and the counters, completion event.
+static int ship_slot(pnetgpu_ring* r, Slot& s, const uint8_t* src, uint64_t* id) {
     if (hipSetDevice(r->device) != hipSuccess) return PNETGPU_EHIP;
     const hipStream_t st = s.stream;
-    // granule rule: the tail past the last frame is readable (zeroed once at create)
-    if (hipMemcpyAsync(s.d_frames, s.h_frames, s.bytes, hipMemcpyHostToDevice, st) != hipSuccess ||
+    // granule rule: the tail past the last frame is readable (32 zero bytes)
+    if (hipMemcpyAsync(s.d_frames, src, s.bytes, hipMemcpyHostToDevice, st) != hipSuccess ||
+        (src != s.h_frames && hipMemsetAsync(s.d_frames + s.bytes, 0, 32, st) != hipSuccess) ||
         hipMemcpyAsync(s.d_off, s.h_off, 8ull * s.n, hipMemcpyHostToDevice, st) != hipSuccess ||
         hipMemcpyAsync(s.d_len, s.h_len, 4ull * s.n, hipMemcpyHostToDevice, st) != hipSuccess ||
         hipMemsetAsync(s.d_ctr, 0, 8ull * PNETGPU_NCOUNTERS, st) != hipSuccess)
@@ -243,14 +245,16 @@ int pnetgpu_ring_submit(pnetgpu_ring* r, uint64_t* id) {
     b.lengths = s.d_len;
     b.flags = r->flags;
     pnetgpu_rx_columns c{};
-    for (int k = 0; k < kNumCols; ++k) *col_slot(c, k) = s.d_cols[k];
+    for (int k = 0; k < kNumCols; ++k) *col_slot(c, k) = (r->col_mask >> k) & 1u ? s.d_cols[k] : nullptr;
     c.counters = s.d_ctr;
     int rc = pnetgpu_rx_process(r->ctx, &b, &c, st);
     if (rc) return rc;
     for (int k = 0; k < kNumCols; ++k)
-        if (hipMemcpyAsync(s.h_cols[k], s.d_cols[k], (size_t)kColBytes[k] * s.n, hipMemcpyDeviceToHost, st) !=
-            hipSuccess)
+        if (((r->col_mask >> k) & 1u) &&
+            hipMemcpyAsync(s.h_cols[k], s.d_cols[k], (size_t)kColBytes[k] * s.n, hipMemcpyDeviceToHost, st) !=
+                hipSuccess)
             return PNETGPU_EHIP;
+    s.col_mask = r->col_mask;
     if (hipMemcpyAsync(s.h_ctr, s.d_ctr, 8ull * PNETGPU_NCOUNTERS, hipMemcpyDeviceToHost, st) != hipSuccess ||
         hipEventRecord(s.done, st) != hipSuccess)
         return PNETGPU_EHIP;
@@ -262,6 +266,44 @@ int pnetgpu_ring_submit(pnetgpu_ring* r, uint64_t* id) {
     return PNETGPU_OK;
 }
 
+int pnetgpu_ring_submit(pnetgpu_ring* r, uint64_t* id) {
+    if (!r) return PNETGPU_EINVAL;
+    if (id) *id = UINT64_MAX;
+    if (r->filling < 0) return PNETGPU_OK;
+    Slot& s = r->slots[r->filling];
+    if (s.n == 0) return PNETGPU_OK;
+    s.frames_view = s.h_frames;
+    return ship_slot(r, s, s.h_frames, id);
+}
+
+int pnetgpu_ring_submit_region(pnetgpu_ring* r, const uint8_t* base, const uint64_t* offsets, const uint32_t* lengths,
+                               uint64_t n, uint64_t* taken, uint64_t* id) {
+    if (!r || !taken || (n && (!base || !offsets || !lengths))) return PNETGPU_EINVAL;
+    *taken = 0;
+    if (id) *id = UINT64_MAX;
+    if (n == 0) return PNETGPU_OK;
+    if (r->filling < 0 && (r->filling = take_free_slot(r)) < 0) return PNETGPU_EBUSY;
+    Slot& s = r->slots[r->filling];
+    if (s.n) return PNETGPU_EFULL;               // pushed frames are waiting: submit them first
+    // the longest prefix of frames, ascending and non-overlapping, whose span fits the slot
+    const uint64_t o0 = offsets[0];
+    uint64_t k = 0, end = o0;
+    while (k < n && k < r->cap_frames) {
+        if (offsets[k] < end) return PNETGPU_EINVAL;   // frames must ascend without overlap
+        const uint64_t fe = offsets[k] + lengths[k];
+        if (fe - o0 > r->cap_bytes) break;
+        s.h_off[k] = offsets[k] - o0;
+        s.h_len[k] = lengths[k];
+        end = fe;
+        ++k;
+    }
+    if (k == 0) return PNETGPU_EFULL;            // the first frame alone exceeds batch_bytes
+    s.n = (uint32_t)k;
+    s.bytes = end - o0;
+    s.frames_view = base + o0;
+    *taken = k;
+    return ship_slot(r, s, base + o0, id);
+}
 int pnetgpu_ring_wait(pnetgpu_ring* r, pnetgpu_ring_batch* out) {
     if (!r || !out) return PNETGPU_EINVAL;
     if (r->held >= 0) {                          // the previous batch is released now
@@ -278,13 +320,29 @@ int pnetgpu_ring_wait(pnetgpu_ring* r, pnetgpu_ring_batch* out) {
     r->held = i;
     out->id = s.id;
     out->n_frames = s.n;
-    out->frames = s.h_frames;
+    out->frames = s.frames_view;
     out->offsets = s.h_off;
     out->lengths = s.h_len;
     std::memset(&out->cols, 0, sizeof(out->cols));
-    for (int k = 0; k < kNumCols; ++k) *col_slot(out->cols, k) = s.h_cols[k];
+    for (int k = 0; k < kNumCols; ++k) *col_slot(out->cols, k) = (s.col_mask >> k) & 1u ? s.h_cols[k] : nullptr;
     out->cols.counters = s.h_ctr;
     return PNETGPU_OK;
+}
+
+int pnetgpu_ring_set_columns(pnetgpu_ring* r, uint32_t column_mask) {
+    if (!r || (column_mask >> kNumCols)) return PNETGPU_EINVAL;
+    r->col_mask = column_mask;
+    return PNETGPU_OK;
+}
+
+int pnetgpu_host_register(void* p, uint64_t bytes) {
+    if (!p || !bytes) return PNETGPU_EINVAL;
+    return hipHostRegister(p, bytes, hipHostRegisterDefault) == hipSuccess ? PNETGPU_OK : PNETGPU_EHIP;
+}
+
+int pnetgpu_host_unregister(void* p) {
+    if (!p) return PNETGPU_EINVAL;
+    return hipHostUnregister(p) == hipSuccess ? PNETGPU_OK : PNETGPU_EHIP;
 }
 
 // ---- classic pcap reader -----------------------------------------------------
@@ -341,6 +399,34 @@ int pnetgpu_pcap_next(pnetgpu_pcap* p, const uint8_t** frame, uint32_t* len) {
     if (incl && std::fread(p->buf.data(), 1, incl, p->f) != incl) return PNETGPU_EFORMAT;
     *frame = p->buf.data();
     *len = incl;
+    return PNETGPU_OK;
+}
+
+int pnetgpu_pcap_scan(const uint8_t* img, uint64_t img_bytes, uint64_t* pos, uint64_t* offsets, uint32_t* lengths,
+                      uint64_t cap, uint64_t* n) {
+    if (!img || !pos || !n || (cap && (!offsets || !lengths))) return PNETGPU_EINVAL;
+    *n = 0;
+    if (img_bytes < 24) return PNETGPU_EFORMAT;
+    uint32_t magic;
+    std::memcpy(&magic, img, 4);
+    bool swap;
+    if (magic == 0xa1b2c3d4u || magic == 0xa1b23c4du) swap = false;
+    else if (magic == 0xd4c3b2a1u || magic == 0x4d3cb2a1u) swap = true;
+    else return PNETGPU_EFORMAT;
+    if (rd32(img + 20, swap) != 1u) return PNETGPU_EFORMAT;   // LINKTYPE_ETHERNET
+    uint64_t p = *pos < 24 ? 24 : *pos;
+    uint64_t k = 0;
+    while (k < cap && p < img_bytes) {
+        if (img_bytes - p < 16) return PNETGPU_EFORMAT;      // truncated record header
+        const uint32_t incl = rd32(img + p + 8, swap);
+        if (incl > (1u << 26) || incl > img_bytes - p - 16) return PNETGPU_EFORMAT;
+        offsets[k] = p + 16;
+        lengths[k] = incl;
+        p += 16ull + incl;
+        ++k;
+    }
+    *n = k;
+    *pos = p;
     return PNETGPU_OK;
 }
 

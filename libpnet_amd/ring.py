@@ -10,7 +10,7 @@ import ctypes
 
 import numpy as np
 
-from ._lib import DEFS, RxColumns, check, lib
+from ._lib import COLUMN_NAMES, DEFS, RxColumns, check, lib
 from .engine import COLUMNS, COUNTER_NAMES, context
 
 EFULL, EBUSY, EEMPTY = DEFS["PNETGPU_EFULL"], DEFS["PNETGPU_EBUSY"], DEFS["PNETGPU_EEMPTY"]
@@ -41,6 +41,16 @@ def _setup():
     lib.pnetgpu_pcap_next.argtypes = [vp, ctypes.POINTER(ctypes.POINTER(ctypes.c_uint8)), ctypes.POINTER(u32)]
     lib.pnetgpu_pcap_close.restype = None
     lib.pnetgpu_pcap_close.argtypes = [vp]
+    lib.pnetgpu_ring_set_columns.restype = i32
+    lib.pnetgpu_ring_set_columns.argtypes = [vp, u32]
+    lib.pnetgpu_ring_submit_region.restype = i32
+    lib.pnetgpu_ring_submit_region.argtypes = [vp, vp, vp, vp, u64, ctypes.POINTER(u64), ctypes.POINTER(u64)]
+    lib.pnetgpu_host_register.restype = i32
+    lib.pnetgpu_host_register.argtypes = [vp, u64]
+    lib.pnetgpu_host_unregister.restype = i32
+    lib.pnetgpu_host_unregister.argtypes = [vp]
+    lib.pnetgpu_pcap_scan.restype = i32
+    lib.pnetgpu_pcap_scan.argtypes = [vp, u64, ctypes.POINTER(u64), vp, vp, u64, ctypes.POINTER(u64)]
 
 
 _setup()
@@ -62,6 +72,8 @@ class Batch:
         self.records = {}
         for c, (_, npdt, shape) in COLUMNS.items():
             ptr = getattr(rb.cols, c)
+            if not ptr:                     # not selected (Ring(columns=...))
+                continue
             itemsize = np.dtype(npdt).itemsize
             ct = {1: ctypes.c_uint8, 2: ctypes.c_uint16, 4: ctypes.c_uint32}[itemsize]
             a = np.ctypeslib.as_array(ctypes.cast(ptr, ctypes.POINTER(ct)), (n,) + shape) if n else np.zeros(
@@ -75,7 +87,8 @@ class Batch:
 class Ring:
     """Pinned host batches -> asynchronous GPU verification (three rotating slots)."""
 
-    def __init__(self, batch_bytes=64 << 20, batch_frames=1 << 18, device=0, copy=True, flags=0):
+    def __init__(self, batch_bytes=64 << 20, batch_frames=1 << 18, device=0, copy=True, flags=0, columns=None):
+        """columns: names of the record columns to compute and copy back (default all)."""
         self.ctx = context(device)
         self.copy = copy
         h = ctypes.c_void_p()
@@ -83,6 +96,11 @@ class Ring:
               "pnetgpu_ring_create")
         self.h = h
         self.pending = 0
+        if columns is not None:
+            mask = 0
+            for c in columns:
+                mask |= 1 << COLUMN_NAMES.index(c)
+            check(lib.pnetgpu_ring_set_columns(self.h, mask), "pnetgpu_ring_set_columns")
 
     def close(self):
         if getattr(self, "h", None):
@@ -153,6 +171,38 @@ class Ring:
                 continue
             check(rc, "pnetgpu_ring_push_many")
 
+    def feed_region(self, buf, offsets, lengths):
+        """Zero-copy: ship frames buf[offsets[i], +lengths[i]) (ascending, non-overlapping)
+        straight from buf, one H2D per batch (pnetgpu_ring_submit_region); yields
+        completed batches, whose `frames` view buf. Keep buf unchanged until they
+        are consumed; register it (HostRegistration) for a direct DMA."""
+        buf = np.ascontiguousarray(buf, np.uint8)
+        offsets = np.ascontiguousarray(offsets, np.uint64)
+        lengths = np.ascontiguousarray(lengths, np.uint32)
+        i, n = 0, len(offsets)
+        taken, bid = ctypes.c_uint64(), ctypes.c_uint64()
+        while i < n:
+            rc = lib.pnetgpu_ring_submit_region(self.h, ctypes.c_void_p(buf.ctypes.data),
+                                                ctypes.c_void_p(offsets[i:].ctypes.data),
+                                                ctypes.c_void_p(lengths[i:].ctypes.data), n - i, ctypes.byref(taken),
+                                                ctypes.byref(bid))
+            if rc == 0:
+                i += taken.value
+                self.pending += 1
+                continue
+            if rc == EBUSY:
+                b = self._wait()
+                if b is not None:
+                    yield b
+                continue
+            if rc == EFULL:                      # frames pushed earlier are still filling: ship them
+                before = self.pending
+                self.submit()
+                if self.pending == before:
+                    raise ValueError(f"frame {i} ({int(lengths[i])} B) exceeds the ring's batch_bytes")
+                continue
+            check(rc, "pnetgpu_ring_submit_region")
+
     def drain(self):
         """Submit the partial batch and yield every outstanding batch."""
         self.submit()
@@ -161,6 +211,47 @@ class Ring:
             if b is None:
                 return
             yield b
+
+
+class HostRegistration:
+    """Page-locks a host numpy array for direct DMA (pnetgpu_host_register) for
+    the lifetime of the context."""
+
+    def __init__(self, arr):
+        self.arr = arr
+        self.ptr = ctypes.c_void_p(arr.ctypes.data)
+        check(lib.pnetgpu_host_register(self.ptr, arr.nbytes), "pnetgpu_host_register")
+
+    def close(self):
+        if self.ptr is not None:
+            check(lib.pnetgpu_host_unregister(self.ptr), "pnetgpu_host_unregister")
+            self.ptr = None
+
+    def __enter__(self):
+        return self.arr
+
+    def __exit__(self, *exc):
+        self.close()
+
+
+def pcap_index(img, batch=1 << 16):
+    """Record descriptors of an in-memory classic pcap image (e.g. np.fromfile or
+    np.memmap of the file): (offsets uint64, lengths uint32) of every record's
+    captured bytes within img, for Ring.feed_region (pnetgpu_pcap_scan)."""
+    img = np.ascontiguousarray(img, np.uint8)
+    pos, n = ctypes.c_uint64(0), ctypes.c_uint64()
+    offs, lens = [], []
+    while True:
+        o = np.empty(batch, np.uint64)
+        ln = np.empty(batch, np.uint32)
+        check(lib.pnetgpu_pcap_scan(ctypes.c_void_p(img.ctypes.data), img.nbytes, ctypes.byref(pos),
+                                    ctypes.c_void_p(o.ctypes.data), ctypes.c_void_p(ln.ctypes.data), batch,
+                                    ctypes.byref(n)), "pnetgpu_pcap_scan")
+        offs.append(o[:n.value])
+        lens.append(ln[:n.value])
+        if pos.value >= img.nbytes or n.value == 0:
+            break
+    return np.concatenate(offs), np.concatenate(lens)
 
 
 def pcap_frames(path):

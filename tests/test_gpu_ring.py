@@ -4,6 +4,7 @@ import numpy as np
 import pytest
 
 import libpnet_amd as lp
+from libpnet_amd._lib import PnetGpuError
 from oracle import coracle
 from tests import framegen
 from tests.pcaputil import write_pcap
@@ -20,6 +21,7 @@ def check_batches(batches, frames):
         for k in range(b.n):
             assert bytes(b.frames[b.offsets[k]:b.offsets[k] + b.lengths[k]]) == frames[i + k]
         rec = coracle.rx_batch(b.frames, b.n, offsets=b.offsets, lengths=b.lengths)
+        assert b.records, b.id
         for c, v in b.records.items():
             assert np.array_equal(v, rec[c]), (b.id, c)
         i += b.n
@@ -45,3 +47,60 @@ def test_ring_feed_many_synth():
     out = list(ring.feed_many(w.buf, w.offsets, w.lengths)) + list(ring.drain())
     check_batches(out, frames)
     assert sum(b.counters["l4_csum_bad"] for b in out) == w.expect["l4_bad"]
+
+
+@pytest.mark.parametrize("register", [False, True])
+def test_ring_zero_copy_region(register):
+    """submit_region ships frames straight from the caller's (pageable or
+    registered) buffer; records equal the oracle's, frames are views of it."""
+    w = lp.synth.make("imix", 60000, seed=8, corrupt_ppm=20000)
+    frames = [bytes(w.buf[o:o + l]) for o, l in zip(w.offsets, w.lengths)]
+    buf = np.array(w.buf, copy=True)
+    ring = lp.Ring(batch_bytes=4 << 20, batch_frames=1 << 14, copy=True)
+    reg = lp.HostRegistration(buf) if register else None
+    try:
+        out = list(ring.feed_region(buf, w.offsets, w.lengths)) + list(ring.drain())
+    finally:
+        if reg:
+            reg.close()
+    check_batches(out, frames)
+    assert sum(b.counters["l4_csum_bad"] for b in out) == w.expect["l4_bad"]
+
+
+def test_ring_zero_copy_pcap_image_after_pushes(tmp_path):
+    """A pcap file image indexed by pnetgpu_pcap_scan and shipped zero-copy, after
+    frames pushed one by one (submit_region first ships the filling batch)."""
+    rng = np.random.default_rng(10)
+    frames = framegen.edge_frames(rng) + framegen.random_frames(rng, 3000, max_len=9000)
+    p = tmp_path / "replay.pcap"
+    write_pcap(p, frames[1000:])
+    img = np.fromfile(p, dtype=np.uint8)
+    offs, lens = lp.pcap_index(img)
+    ring = lp.Ring(batch_bytes=1 << 20, batch_frames=600)
+    out = []
+    for f in frames[:1000]:
+        out.extend(ring.feed(f))
+    out.extend(ring.feed_region(img, offs, lens))
+    out.extend(ring.drain())
+    check_batches(out, frames)
+
+
+def test_ring_zero_copy_rejects_unsorted():
+    buf = np.zeros(1 << 17, np.uint8)
+    ring = lp.Ring(batch_bytes=1 << 16, batch_frames=64)
+    with pytest.raises(PnetGpuError):                  # descending offsets
+        list(ring.feed_region(buf, np.array([100, 50], np.uint64), np.array([60, 60], np.uint32)))
+    with pytest.raises(ValueError):                     # a frame larger than batch_bytes
+        list(ring.feed_region(buf, np.array([0], np.uint64), np.array([70000], np.uint32)))
+
+
+def test_ring_column_subset():
+    """Ring(columns=IPV4_COLUMNS): only those columns are computed and copied back."""
+    w = lp.synth.make("udp64", 20000, seed=12, corrupt_ppm=20000)
+    frames = [bytes(w.buf[i * 64:(i + 1) * 64]) for i in range(20000)]
+    offs = np.arange(20000, dtype=np.uint64) * 64
+    lens = np.full(20000, 64, np.uint32)
+    ring = lp.Ring(batch_bytes=1 << 20, batch_frames=1 << 13, columns=lp.IPV4_COLUMNS)
+    out = list(ring.feed_region(w.buf, offs, lens)) + list(ring.drain())
+    assert all(set(b.records) == set(lp.IPV4_COLUMNS) for b in out)
+    check_batches(out, frames)

@@ -29,3 +29,29 @@ def test_pcap_rejects_non_ethernet(tmp_path):
     q.write_bytes(b"not a pcap at all" * 4)
     with pytest.raises(PnetGpuError):
         list(lp.pcap_frames(q))
+
+
+@pytest.mark.parametrize("nanos", [False, True])
+@pytest.mark.parametrize("big", [False, True])
+def test_pcap_index_matches_reader(tmp_path, nanos, big):
+    """pnetgpu_pcap_scan over the file image finds the same records as the streaming
+    reader, in several resumed calls (batch smaller than the record count)."""
+    frames = framegen.random_frames(np.random.default_rng(5), 500) + [b""]
+    p = tmp_path / "t.pcap"
+    write_pcap(p, frames, nanos=nanos, big_endian=big)
+    img = np.fromfile(p, dtype=np.uint8)
+    offs, lens = lp.pcap_index(img, batch=64)
+    assert len(offs) == len(frames)
+    assert [bytes(img[o:o + n]) for o, n in zip(offs, lens)] == frames
+
+
+def test_pcap_index_rejects_truncated_and_non_ethernet(tmp_path):
+    p = tmp_path / "t.pcap"
+    write_pcap(p, [b"\x01" * 100, b"\x02" * 60])
+    img = np.fromfile(p, dtype=np.uint8)
+    with pytest.raises(PnetGpuError):
+        lp.pcap_index(img[:-10])                        # last record cut short
+    bad = img.copy()
+    bad[20] = 101                                       # LINKTYPE_RAW
+    with pytest.raises(PnetGpuError):
+        lp.pcap_index(bad)
