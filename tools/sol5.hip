@@ -209,7 +209,7 @@ float time_it(F f, int reps) {
     return t[t.size() / 2];
 }
 
-int main() {
+int main(int argc, char** argv) {
     const size_t rbytes = 1ull << 30, wbytes = 416ull << 20;
     uint8_t *in, *out; uint32_t* o;
     CK(hipMalloc(&in, rbytes)); CK(hipMalloc(&out, 1ull << 30)); CK(hipMalloc(&o, 64));
@@ -256,6 +256,19 @@ int main() {
                (rbytes + wb) / ms / 1e6, wb / 1e6);
         return 0;
     };
+    if (argc > 1) {   // dense writes (the 64-B workload's 26 B/frame) in bursts of M steps
+        rw("read only", rw_kernel<2, 0, true, 1>, 0);
+        rw("r + 13x 128B nt every step", rw_kernel<2, 13, true, 1, false, 0>, 1664);
+        rw("r + 13x 128B nt every step, at end", rw_kernel<2, 13, true, 1, false, 3>, 1664);
+        rw("r + 104x 128B nt every 8", rw_kernel<2, 104, true, 8, false, 0>, 1664);
+        rw("r + 13x 1KiB nt every 8", rw_kernel<16, 13, true, 8, false, 0>, 1664);
+        rw("r + 13x 1KiB plain every 8", rw_kernel<16, 13, false, 8, false, 0>, 1664);
+        rw("r + 52x 1KiB nt every 32", rw_kernel<16, 52, true, 32, false, 0>, 1664);
+        rw("r + 13x 1KiB nt every 8, drain first", rw_kernel<16, 13, true, 8, false, 2>, 1664);
+        rw("r + 13x 1KiB nt every 8, st before ld", rw_kernel<16, 13, true, 8, false, 1>, 1664);
+        rw("r + 13x 128B nt every step", rw_kernel<2, 13, true, 1, false, 0>, 1664);
+        return 0;
+    }
     rw("pol none  8x256B every 24", rw_pol_kernel<8, 24, 0>, 2048 / 24);
     rw("pol nt    8x256B every 24", rw_pol_kernel<8, 24, 1>, 2048 / 24);
     rw("pol sc0sc1 8x256B every 24", rw_pol_kernel<8, 24, 2>, 2048 / 24);
