@@ -74,25 +74,31 @@ class Shard:
 
 
 def time_shard(sh, steps, warmup, stream, dist_on):
+    """Wall time of exactly `steps` back-to-back launches, and the kernel's average
+    launch duration from one HIP event pair on the launch stream around the same
+    region (elapsed / steps: includes the few-us launch gaps, so it is an upper
+    bound on the kernel time). Per-launch event pairs are not used: every timed
+    event record adds ~6 us to the interval around the 64-B kernel (a 2.5 %
+    inflation measured on MI355X, tools/launch_gap.py)."""
     for _ in range(warmup):
         sh.step(stream)
     stream.synchronize()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    a = torch.cuda.Event(enable_timing=True)
+    b = torch.cuda.Event(enable_timing=True)
     if dist_on:
         torch.distributed.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for a, b in ev:
-        a.record(stream)
+    a.record(stream)
+    for _ in range(steps):
         sh.step(stream)
-        b.record(stream)
+    b.record(stream)
     stream.synchronize()
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
     if dist_on:
         torch.distributed.barrier()
-    kern_ms = [a.elapsed_time(b) for a, b in ev]
-    return wall, kern_ms
+    return wall, a.elapsed_time(b) / steps
 
 
 def check_counters(sh):
@@ -244,17 +250,19 @@ def e2e_zero_copy_rate(sh, seconds=3.0):
 
 
 def time_launches(fn, steps, warmup, stream):
-    """Average duration (ms) of `steps` launches of fn(stream), HIP events on that stream."""
+    """Average duration (ms) of `steps` back-to-back launches of fn(stream): one HIP
+    event pair on that stream around all of them (see time_shard)."""
     for _ in range(warmup):
         fn(stream)
     stream.synchronize()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
-    for a, b in ev:
-        a.record(stream)
+    a = torch.cuda.Event(enable_timing=True)
+    b = torch.cuda.Event(enable_timing=True)
+    a.record(stream)
+    for _ in range(steps):
         fn(stream)
-        b.record(stream)
+    b.record(stream)
     stream.synchronize()
-    return float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    return a.elapsed_time(b) / steps
 
 
 def tx_fill_rate(sh, steps, warmup, device):
@@ -281,6 +289,9 @@ def tx_fill_rate(sh, steps, warmup, device):
     return {"mpkts_s": round(sh.n / (ms * 1e-3) / 1e6, 1), "kernel_avg_ms": round(ms, 4),
             "achieved_gbs": round(alg / (ms * 1e-3) / 1e9, 1), "frac": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             "cpu_port_1core_mpkts_s": round(cpu, 2),
+            # the kernel writes every patched frame back whole (coalesced 1-KiB stores:
+            # 2-B patches at scattered offsets ran 1.7x slower), so it moves ~2x the frame bytes
+            "rewrite_gbs": round((2 * sh.frame_bytes + 2 * sh.n) / (ms * 1e-3) / 1e9, 1),
             "note": "device-resident tx_fill_checksums (IPv4 header + L4 checksum patched in place), kernel time; "
                     f"CPU: oracle_tx_fill, 1 core, first {n1} frames"}
 
@@ -359,19 +370,18 @@ def main():
             log(f"[bench] {name}: built {sh.n} frames ({sh.frame_bytes / 2**30:.2f} GiB) in {time.perf_counter() - t:.1f}s")
         ok, ctr = check_counters(sh)
         stream = torch.cuda.Stream(device)
-        wall, kern_ms = time_shard(sh, args.steps, args.warmup, stream, dist_on)
+        wall, avg_ms = time_shard(sh, args.steps, args.warmup, stream, dist_on)
         # counters: one RCCL all-reduce at the end (the "final throughput reduction")
         ctr_t = torch.tensor([ctr[k] for k in lp.COUNTER_NAMES] + [int(ok)], dtype=torch.int64, device=device)
         shard.all_reduce_counters(ctr_t)
         wall = shard.all_reduce_max(wall, device)
         frames_all = sh.n * world * args.steps
-        avg_ms = float(np.mean(kern_ms))
         achieved = sh.alg_bytes / (avg_ms * 1e-3) / 1e9
         results[name] = {
             "sh": sh, "wall": wall, "ms_per_step": wall / args.steps * 1e3,
             "mpkts_s": frames_all / wall / 1e6,
             "gb_s": sh.frame_bytes * world * args.steps / wall / 1e9,
-            "kernel_avg_ms": avg_ms, "kernel_min_ms": float(np.min(kern_ms)),
+            "kernel_avg_ms": avg_ms,
             "achieved_gbs": achieved, "counters_ok": bool(ctr_t[-1].item() == world),
             "counters": {k: int(v) for k, v in zip(lp.COUNTER_NAMES, ctr_t[:-1].tolist())},
         }
