@@ -112,6 +112,24 @@ def check_counters(sh):
     return ok, c
 
 
+def host_cpu():
+    """The host the CPU baseline ran on (record nproc and the model)."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    model = ln.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        usable = None
+    return {"cpu_model": model, "host_cpus": os.cpu_count(), "usable_cpus": usable}
+
+
 def cpu_baseline(sh, budget_cpu_s=12.0):
     """The oracle (scalar C restatement, 'port') on this host's cores over a bounded sample."""
     from oracle import coracle  # checker / baseline only
@@ -144,7 +162,7 @@ def cpu_baseline(sh, budget_cpu_s=12.0):
         if e1 >= 3.0:
             break
     return {"value": round(mpps, 2), "unit": "Mpkts/s", "cores": nthreads, "kind": "port",
-            "value_1core": round(f1 / e1 / 1e6, 2),
+            "value_1core": round(f1 / e1 / 1e6, 2), **host_cpu(),
             "gbps": round(frames * (w.expect["bytes"] / sh.n) / el / 1e9, 2),
             "sample": f"first {n} frames of the same {sh.name} batch x{reps} passes ({el:.1f} s wall, "
                       f"{nthreads} threads, oracle/pnet_oracle.c scalar per-frame restatement)"}
