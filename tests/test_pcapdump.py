@@ -1,0 +1,129 @@
+"""examples/pcapdump.c: packetdump.rs over a pcap file with the per-packet work
+on the GPU. CPU: the Rust-Display restatements the expected text relies on, and
+that the binary is built. GPU: its stdout equals packetdump's lines (restated in
+tests/packetdump_fmt.py from the oracle's records) for edge, random, ARP,
+unknown-ethertype, ICMP echo and IPv6-address-format frames, with and without
+the checksum suffix."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from tests import framegen
+from tests.packetdump_fmt import line, v6
+from tests.pcaputil import write_pcap
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+EXE = os.path.join(ROOT, "libpnet_amd", "build", "pcapdump")
+
+
+def a6(*segs):
+    return b"".join(s.to_bytes(2, "big") for s in segs)
+
+
+@pytest.mark.parametrize("segs,text", [
+    # Rust std Ipv6Addr Display examples (core::net docs and tests)
+    ((0, 0, 0, 0, 0, 0, 0, 0), "::"),
+    ((0, 0, 0, 0, 0, 0, 0, 1), "::1"),
+    ((0, 0, 0, 0, 0, 0xffff, 0xc00a, 0x2ff), "::ffff:192.10.2.255"),
+    ((0x2001, 0xdb8, 0, 0, 0, 0, 0, 1), "2001:db8::1"),
+    ((1, 0, 0, 2, 0, 0, 0, 3), "1:0:0:2::3"),
+    ((1, 0, 0, 2, 0, 0, 3, 4), "1::2:0:0:3:4"),
+    ((1, 0, 2, 0, 3, 0, 4, 0), "1:0:2:0:3:0:4:0"),
+    ((0, 0, 0, 0, 0, 0, 0xc00a, 0x2ff), "::c00a:2ff"),
+    ((0xfe80, 0, 0, 0, 0, 0, 0, 0), "fe80::"),
+])
+def test_ipv6_display(segs, text):
+    assert v6(a6(*segs)) == text
+
+
+def test_pcapdump_built():
+    assert os.access(EXE, os.X_OK), "run `make -C libpnet_amd` (build())"
+
+
+def special_frames(rng):
+    out = []
+    # ARP request/reply (42 B and 60 B padded) and a truncated one
+    for op, pad in ((1, 0), (2, 18)):
+        f = bytearray(rng.integers(0, 256, 42 + pad, dtype=np.uint8).tobytes())
+        f[12:14] = b"\x08\x06"
+        f[14 + 6:14 + 8] = op.to_bytes(2, "big")
+        out.append(bytes(f))
+    f = bytearray(rng.integers(0, 256, 14 + 27, dtype=np.uint8).tobytes())
+    f[12:14] = b"\x08\x06"
+    out.append(bytes(f))
+    # unknown ethertypes (LLDP, VLAN with flags 0, a random one)
+    for et in (0x88CC, 0x8100, 0x1234):
+        f = bytearray(rng.integers(0, 256, 60, dtype=np.uint8).tobytes())
+        f[12:14] = et.to_bytes(2, "big")
+        out.append(bytes(f))
+    # ICMP echo request / reply / other types, over IPv4 and IPv6, short echoes
+    for kind in ("icmp", "icmp_over6"):
+        for t in (0, 8, 3, 11):
+            for l4 in (4, 7, 8, 64):
+                f = bytearray(framegen.build_frame(rng, kind, l4))
+                f[-l4] = t
+                out.append(bytes(f))
+    # IPv6 address formats
+    for src, dst in ((a6(0, 0, 0, 0, 0, 0, 0, 1), a6(0, 0, 0, 0, 0, 0xffff, 0x0a00, 0x0001)),
+                     (a6(0x2001, 0xdb8, 0, 0, 1, 0, 0, 1), a6(0, 0, 0, 0, 0, 0, 0, 0)),
+                     (a6(0xfe80, 0, 0, 0, 0x1234, 0, 0, 0), a6(1, 2, 3, 4, 5, 6, 7, 8))):
+        for kind in ("udp6", "tcp6", "icmp6"):
+            f = bytearray(framegen.build_frame(rng, kind, 40))
+            f[22:38], f[38:54] = src, dst
+            out.append(bytes(f))
+    # unknown protocols (IPv4 GRE, IPv6 hop-by-hop with flags 0)
+    f = bytearray(framegen.build_frame(rng, "udp", 30))
+    f[23] = 47
+    out.append(bytes(f))
+    f = bytearray(framegen.build_frame(rng, "udp6", 30))
+    f[20] = 0
+    out.append(bytes(f))
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("csum", [False, True])
+def test_pcapdump_matches_packetdump_lines(tmp_path, csum):
+    rng = np.random.default_rng(77)
+    frames = special_frames(rng) + framegen.edge_frames(rng) + framegen.random_frames(rng, 3000)
+    p = tmp_path / "dump.pcap"
+    write_pcap(p, frames)
+    args = [EXE, "-i", "eth7"] + (["-c"] if csum else []) + [str(p)]
+    r = subprocess.run(args, capture_output=True, text=True, timeout=100)
+    assert r.returncode == 0, r.stderr
+    got = r.stdout.splitlines()
+    want = [line(f, "eth7", csum) for f in frames]
+    assert len(got) == len(want)
+    for i, (g, w) in enumerate(zip(got, want)):
+        assert g == w, f"frame {i} ({len(frames[i])} B): got {g!r} want {w!r}"
+
+
+@pytest.mark.gpu
+def test_pcapdump_many_batches(tmp_path):
+    """More records than one ring slot holds (2^18 frames): order and text kept
+    across slots, waits and a partly filled last batch."""
+    rng = np.random.default_rng(78)
+    base = framegen.random_frames(rng, 500, max_len=200)
+    frames = [base[i % len(base)] for i in range(300_001)]
+    p = tmp_path / "big.pcap"
+    write_pcap(p, frames)
+    r = subprocess.run([EXE, str(p)], capture_output=True, text=True, timeout=100)
+    assert r.returncode == 0, r.stderr
+    want_base = [line(f) for f in base]
+    got = r.stdout.splitlines()
+    assert len(got) == len(frames)
+    assert all(g == want_base[i % len(base)] for i, g in enumerate(got))
+
+
+@pytest.mark.gpu
+def test_pcapdump_empty_and_bad(tmp_path):
+    p = tmp_path / "empty.pcap"
+    write_pcap(p, [])
+    r = subprocess.run([EXE, str(p)], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0 and r.stdout == ""
+    q = tmp_path / "bad.pcap"
+    q.write_bytes(b"not a pcap at all" * 4)
+    r = subprocess.run([EXE, str(q)], capture_output=True, text=True, timeout=60)
+    assert r.returncode != 0 and "pcapdump" in r.stderr
