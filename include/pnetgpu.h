@@ -106,9 +106,17 @@ extern "C" {
  *                        offset (value & ~3) != 0 sets FRAGMENT and stops); a
  *                        truncated header sets L4_MALFORMED. ip_proto reports
  *                        the protocol after the walk; the L4 pseudo-header uses
- *                        the base header's addresses and the L4 slice length. */
+ *                        the base header's addresses and the L4 slice length.
+ *   PNETGPU_RX_L3        frames begin at the IP header (pnet_transport's Layer3
+ *                        receive, pnet_transport/src/lib.rs:342-374, and raw-IP
+ *                        captures): no Ethernet header; the version nibble picks
+ *                        the chain (4 -> Ipv4Packet, 6 -> Ipv6Packet), anything
+ *                        else or an empty frame sets UNKNOWN_ETHERTYPE. ethertype
+ *                        reports 0x0800 / 0x86DD (0 otherwise), l3_offset 0;
+ *                        PNETGPU_RX_VLAN has no effect. */
 #define PNETGPU_RX_VLAN           0x1u
 #define PNETGPU_RX_IPV6_EXT       0x2u
+#define PNETGPU_RX_L3             0x4u
 
 /* ---- batch-wide counters (rx columns .counters, uint64 each, accumulated) */
 #define PNETGPU_CTR_FRAMES        0  /* frames with a valid descriptor            */

@@ -97,7 +97,7 @@ static int rx_common(pnetgpu_ctx* ctx, const pnetgpu_batch* b, const pnetgpu_rx_
         (cols->dst_ipv6 && (reinterpret_cast<uintptr_t>(cols->dst_ipv6) & 15)))
         return PNETGPU_EINVAL;
     if (b->n_frames > (UINT64_MAX - kRunFrames) / 2) return PNETGPU_EINVAL;
-    if ((b->flags & ~(PNETGPU_RX_VLAN | PNETGPU_RX_IPV6_EXT)) || b->reserved) return PNETGPU_EINVAL;
+    if ((b->flags & ~(PNETGPU_RX_VLAN | PNETGPU_RX_IPV6_EXT | PNETGPU_RX_L3)) || b->reserved) return PNETGPU_EINVAL;
     int rc = set_device(ctx);
     if (rc) return rc;
 

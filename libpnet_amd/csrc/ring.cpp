@@ -110,7 +110,7 @@ extern "C" {
 int pnetgpu_ring_create(pnetgpu_ctx* ctx, uint64_t batch_bytes, uint32_t batch_frames, uint32_t flags,
                         pnetgpu_ring** out) {
     if (!ctx || !out || batch_bytes == 0 || batch_frames == 0) return PNETGPU_EINVAL;
-    if (flags & ~(PNETGPU_RX_VLAN | PNETGPU_RX_IPV6_EXT)) return PNETGPU_EINVAL;
+    if (flags & ~(PNETGPU_RX_VLAN | PNETGPU_RX_IPV6_EXT | PNETGPU_RX_L3)) return PNETGPU_EINVAL;
     *out = nullptr;
     auto* r = new (std::nothrow) pnetgpu_ring;
     if (!r) return PNETGPU_ENOMEM;

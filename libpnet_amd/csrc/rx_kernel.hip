@@ -145,13 +145,21 @@ __device__ __forceinline__ bool is_vlan_tpid(uint32_t et) { return et == 0x8100u
 // bounds (decorator.rs:713-769). Mirrors oracle_rx_frame_ex.
 __device__ __forceinline__ Parsed parse_frame(const FrameBytes& F, uint32_t len, uint32_t flags) {
     Parsed P{};
-    if (len < 14) {
-        P.st = PNET_ST_ETH_MALFORMED;                  // EthernetPacket::new == None
-        return P;
+    uint32_t et;
+    int l3;
+    if (flags & PNETGPU_RX_L3) {                       // IP header at byte 0: version nibble
+        const uint32_t ver = len ? F.near8(0) >> 4 : 0u;
+        et = ver == 4u ? 0x0800u : ver == 6u ? 0x86DDu : 0u;
+        l3 = 0;
+    } else {
+        if (len < 14) {
+            P.st = PNET_ST_ETH_MALFORMED;              // EthernetPacket::new == None
+            return P;
+        }
+        et = F.near16(12);
+        l3 = 14;
     }
-    uint32_t et = F.near16(12);
-    int l3 = 14;
-    if (flags & PNETGPU_RX_VLAN) {
+    if ((flags & (PNETGPU_RX_VLAN | PNETGPU_RX_L3)) == PNETGPU_RX_VLAN) {
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
             if (!is_vlan_tpid(et)) break;

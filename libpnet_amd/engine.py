@@ -46,7 +46,7 @@ assert tuple(COLUMNS) == COLUMN_NAMES
 #: every IPv4-relevant column: the bench's "checksum verify + header extract" record
 IPV4_COLUMNS = ("status", "ip_csum", "l4_csum", "ethertype", "ip_proto", "ttl", "l4_offset", "l4_length",
                 "src_port", "dst_port", "src_ipv4", "dst_ipv4")
-RX_VLAN, RX_IPV6_EXT = DEFS["PNETGPU_RX_VLAN"], DEFS["PNETGPU_RX_IPV6_EXT"]
+RX_VLAN, RX_IPV6_EXT, RX_L3 = DEFS["PNETGPU_RX_VLAN"], DEFS["PNETGPU_RX_IPV6_EXT"], DEFS["PNETGPU_RX_L3"]
 ALL_COLUMNS = COLUMN_NAMES
 NCOUNTERS = DEFS["PNETGPU_NCOUNTERS"]
 COUNTER_NAMES = ("frames", "bytes", "ipv4", "ipv6", "ip_csum_bad", "l4_csum_bad", "malformed", "unknown")

@@ -21,7 +21,7 @@ REC_DTYPE = np.dtype([
     ("vlan_tci", "<u2"), ("l3_offset", "u1"), ("_pad2", "u1"),
 ], align=True)
 
-RX_VLAN, RX_IPV6_EXT = 0x1, 0x2
+RX_VLAN, RX_IPV6_EXT, RX_L3 = 0x1, 0x2, 0x4
 
 _lib = None
 

@@ -266,10 +266,20 @@ static int is_vlan_tpid(unsigned et) {       /* EtherTypes::Vlan / PBridge / Qin
  * first and the IP header starts after them. */
 void oracle_rx_frame_ex(const uint8_t* frame, size_t len, uint32_t flags, oracle_rec* r) {
     memset(r, 0, sizeof(*r));
-    if (len < 14) { r->status = ORACLE_ST_ETH_MALFORMED; return; }  /* EthernetPacket::new, min 14 */
-    unsigned et = be16(frame + 12);                       /* ethernet.rs:27-28 */
-    size_t l3 = 14;
-    if (flags & ORACLE_RX_VLAN) {
+    unsigned et;
+    size_t l3;
+    if (flags & ORACLE_RX_L3) {
+        /* pnet_transport Layer3 receive (lib.rs:342-374): Ipv4Packet::new over the
+         * whole buffer; IPv6 by the version nibble; the IP views as below */
+        const unsigned ver = len ? frame[0] >> 4 : 0;
+        et = ver == 4 ? 0x0800u : ver == 6 ? 0x86DDu : 0u;
+        l3 = 0;
+    } else {
+        if (len < 14) { r->status = ORACLE_ST_ETH_MALFORMED; return; }  /* EthernetPacket::new, min 14 */
+        et = be16(frame + 12);                            /* ethernet.rs:27-28 */
+        l3 = 14;
+    }
+    if ((flags & (ORACLE_RX_VLAN | ORACLE_RX_L3)) == ORACLE_RX_VLAN) {
         for (int k = 0; k < 2 && is_vlan_tpid(et); ++k) {
             r->status |= ORACLE_ST_VLAN;
             if (len < l3 + 4) {                           /* VlanPacket::new == None */

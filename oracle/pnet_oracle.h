@@ -60,6 +60,7 @@ extern "C" {
 /* opt-in dispatch extensions (beyond packetdump.rs's chain) */
 #define ORACLE_RX_VLAN      0x1u   /* follow 802.1Q/802.1ad/QinQ tags, vlan.rs:62-72 (<= 2)   */
 #define ORACLE_RX_IPV6_EXT  0x2u   /* walk IPv6 extension headers, ipv6.rs:39-137 (<= 4)      */
+#define ORACLE_RX_L3        0x4u   /* frames begin at the IP header (version nibble dispatch)  */
 
 /* One receive record: the same fields as the GPU result columns. */
 typedef struct oracle_rec {

@@ -28,7 +28,7 @@ ST_UNKNOWN_PROTO = 0x1000
 ST_VLAN = 0x2000
 ST_FRAGMENT = 0x4000
 ST_DESC_INVALID = 0x8000
-RX_VLAN, RX_IPV6_EXT = 0x1, 0x2
+RX_VLAN, RX_IPV6_EXT, RX_L3 = 0x1, 0x2, 0x4
 
 FIELDS = ("status", "ip_csum", "l4_csum", "ethertype", "ip_proto", "ttl", "l4_offset",
           "l4_length", "src_port", "dst_port", "src_ipv4", "dst_ipv4", "src_ipv6", "dst_ipv6",
@@ -79,13 +79,18 @@ def rx_frame(frame, flags=0):
     r = dict.fromkeys(FIELDS, 0)
     r["src_ipv6"] = bytes(16)
     r["dst_ipv6"] = bytes(16)
-    if len(f) < 14:
-        r["status"] = ST_ETH_MALFORMED
-        return r
     st = 0
-    et = _be16(f, 12)
-    l3 = 14
-    if flags & RX_VLAN:                      # vlan.rs:62-72; TPIDs ethernet.rs:102,104,112
+    if flags & RX_L3:                        # pnet_transport Layer3: IP header at byte 0
+        ver = f[0] >> 4 if f else 0
+        et = {4: 0x0800, 6: 0x86DD}.get(ver, 0)
+        l3 = 0
+    else:
+        if len(f) < 14:
+            r["status"] = ST_ETH_MALFORMED
+            return r
+        et = _be16(f, 12)
+        l3 = 14
+    if flags & RX_VLAN and not flags & RX_L3:   # vlan.rs:62-72; TPIDs ethernet.rs:102,104,112
         for k in range(2):
             if et not in (0x8100, 0x88A8, 0x9100):
                 break

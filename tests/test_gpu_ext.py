@@ -57,3 +57,53 @@ def test_tx_fill_with_extensions(flags):
     torch.cuda.synchronize()
     assert np.array_equal(d.cpu().numpy(), want_buf)
     compare(res, want_rec)
+
+
+@pytest.mark.parametrize("flags", [4, 6, 7])
+def test_l3_packets_desc(flags):
+    """PNETGPU_RX_L3 (frames begin at the IP header) at arbitrary alignment."""
+    from tests.test_oracle_ext import ip_packets
+    rng = np.random.default_rng(50 + flags)
+    pkts = ip_packets(rng, 1500)
+    buf, offs, lens = framegen.pack(pkts, gap=11, rng=rng)
+    rec = coracle.rx_batch(buf, len(pkts), offsets=offs, lengths=lens, flags=flags)
+    for data_offset in (0, 5):
+        d = to_dev(np.concatenate([np.zeros(16, np.uint8), buf]))[data_offset:]
+        res = lp.rx_process(d, offsets=to_dev((offs + 16 - data_offset).astype(np.int64)),
+                            lengths=to_dev(lens.astype(np.int32)), columns=ALL_COLUMNS, flags=flags)
+        torch.cuda.synchronize()
+        compare(res, rec)
+
+
+def test_l3_stride_mode_and_tx_fill():
+    """Fixed-stride L3 batches (raw IPv4/UDP datagrams of a sender) through the
+    generic kernel, and the TX fill of their checksums in place."""
+    rng = np.random.default_rng(9)
+    pkts = [framegen.build_frame(rng, k, 30)[14:] for k in ("udp", "tcp", "icmp", "udp6", "tcp6") * 400]
+    stride = 96
+    buf = np.zeros(stride * len(pkts) + 32, np.uint8)
+    for i, p in enumerate(pkts):
+        buf[i * stride:i * stride + len(p)] = np.frombuffer(p, np.uint8)
+    flen = max(len(p) for p in pkts)
+    rec = coracle.rx_batch(buf, len(pkts), stride=stride, frame_len=flen, flags=4)
+    res = lp.rx_process(to_dev(buf), stride=stride, frame_len=flen, n_frames=len(pkts), columns=ALL_COLUMNS, flags=4)
+    torch.cuda.synchronize()
+    compare(res, rec)
+    st = res.numpy()["status"]
+    assert ((st & 0x100) != 0).sum() == 1200 and ((st & 0x400) != 0).all()
+    # zero every checksum field, fill them on the GPU: the original bytes come back
+    z = buf.copy()
+    for i in range(len(pkts)):
+        r = rec[i]
+        if r["status"] & 1:
+            z[i * stride + 10:i * stride + 12] = 0
+        if r["status"] & 0x200:
+            at = int(r["l4_offset"]) + {4: 6, 8: 16, 12: 2, 16: 2}[int(r["status"]) & 0x1C]
+            z[i * stride + at:i * stride + at + 2] = 0
+    d = to_dev(z)
+    lp.tx_fill_checksums(d, stride=stride, frame_len=flen, n_frames=len(pkts), flags=4)
+    torch.cuda.synchronize()
+    want, _ = coracle.tx_fill(z, len(pkts), stride=stride, frame_len=flen, flags=4)
+    got = d.cpu().numpy()
+    assert np.array_equal(got, want)
+    assert np.array_equal(got, buf)

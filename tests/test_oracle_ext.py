@@ -40,3 +40,58 @@ def test_vlan_and_ext_checksums_verify():
     assert r["l3_offset"] == 22 and r["ip_proto"] == 17 and r["vlan_tci"] == 3
     r0 = coracle.rx_frame(f, 0)
     assert r0["status"] == pyoracle.ST_UNKNOWN_ETHERTYPE and r0["ethertype"] == 0x88A8
+
+
+def ip_packets(rng, n=600):
+    """Layer-3 buffers (pnet_transport Layer3 receive): the framegen frames
+    without their Ethernet header, plus short / garbage / other-version ones."""
+    frames = framegen.extension_frames(rng) + framegen.random_frames(rng, n) + framegen.edge_frames(rng)
+    out = [f[14:] for f in frames if len(f) >= 14]
+    for k in range(40):
+        out.append(bytes([(k % 16) << 4 | 5]) + rng.integers(0, 256, int(rng.integers(0, 80)), dtype=np.uint8).tobytes())
+    out += [b"", b"\x45", b"\x60" * 39]
+    return out
+
+
+@pytest.mark.parametrize("flags", [pyoracle.RX_L3, pyoracle.RX_L3 | pyoracle.RX_IPV6_EXT,
+                                   pyoracle.RX_L3 | pyoracle.RX_VLAN | pyoracle.RX_IPV6_EXT])
+def test_l3_packets_c_vs_python(flags):
+    pkts = ip_packets(np.random.default_rng(31))
+    buf, offs, lens = framegen.pack(pkts, gap=3, rng=np.random.default_rng(4))
+    recs = coracle.rx_batch(buf, len(pkts), offsets=offs, lengths=lens, flags=flags)
+    for i, f in enumerate(pkts):
+        exp = pyoracle.rx_frame(f, flags)
+        for k in pyoracle.FIELDS:
+            g = bytes(recs[i][k]) if k.endswith("ipv6") else int(recs[i][k])
+            assert g == exp[k], (i, k, flags, f.hex())
+
+
+@pytest.mark.parametrize("ext", [0, pyoracle.RX_IPV6_EXT])
+def test_l3_mode_equals_ethernet_mode_shifted(ext):
+    """An IP packet seen at layer 3 gives the Ethernet chain's record for the same
+    packet behind a 14-B Ethernet header, with every frame offset 14 lower."""
+    rng = np.random.default_rng(32)
+    frames = framegen.random_frames(rng, 800) + framegen.edge_frames(rng) + framegen.extension_frames(rng)
+    n = 0
+    for f in frames:
+        if len(f) < 15:
+            continue
+        et, ver = (f[12] << 8) | f[13], f[14] >> 4
+        if (et, ver) not in ((0x0800, 4), (0x86DD, 6)):
+            continue
+        a, b = pyoracle.rx_frame(f, ext), pyoracle.rx_frame(f[14:], ext | pyoracle.RX_L3)
+        assert b["l3_offset"] == 0 and a["l3_offset"] == 14
+        assert b["l4_offset"] == (a["l4_offset"] - 14 if a["l4_offset"] else 0)
+        for k in pyoracle.FIELDS:
+            if k not in ("l3_offset", "l4_offset"):
+                assert a[k] == b[k], (k, f.hex())
+        n += 1
+    assert n > 400
+
+
+def test_l3_mode_version_dispatch():
+    assert pyoracle.rx_frame(b"", pyoracle.RX_L3)["status"] == pyoracle.ST_UNKNOWN_ETHERTYPE
+    r = pyoracle.rx_frame(b"\x45" + bytes(10), pyoracle.RX_L3)
+    assert r["status"] == pyoracle.ST_L3_IPV4 | pyoracle.ST_L3_MALFORMED and r["ethertype"] == 0x0800
+    r = pyoracle.rx_frame(b"\x55" + bytes(40), pyoracle.RX_L3)
+    assert r["status"] == pyoracle.ST_UNKNOWN_ETHERTYPE and r["ethertype"] == 0
