@@ -10,6 +10,12 @@
  * ICMP echo identifier / sequence_number (icmp.rs:222-232, 304-314), MAC
  * addresses and the ARP fields (arp.rs:83-104).
  *
+ * Raw-IP captures (LINKTYPE_RAW / IPV4 / IPV6, e.g. from a tun device) run with
+ * PNETGPU_RX_L3: packetdump's tun branch (packetdump.rs:250-283) wraps such
+ * packets in a zeroed Ethernet header chosen by IP version, so well-formed
+ * packets print the same lines; a version other than 4 / 6 prints
+ * "Unknown packet: IP version V".
+ *
  * Where packetdump would panic (EthernetPacket::new(..).unwrap() on a frame
  * shorter than 14 B, packetdump.rs:291; Echo*Packet::new(..).unwrap() on a
  * 4..7-B echo message, :54,:65) this prints "Malformed Ethernet Frame" /
@@ -34,6 +40,7 @@
 
 static const char* g_name = "pcap";
 static int g_csum = 0;
+static int g_l3 = 0;   /* raw-IP capture: no Ethernet header */
 
 static unsigned be16(const uint8_t* p) { return ((unsigned)p[0] << 8) | p[1]; }
 
@@ -97,6 +104,10 @@ static void dump_frame(const pnetgpu_ring_batch* b, uint64_t i) {
         return;
     }
     const unsigned l3 = st & PNET_ST_L3_MASK;
+    if (l3 == 0 && g_l3) {   /* raw IP, neither version 4 nor 6 */
+        printf("[%s]: Unknown packet: IP version %u; length: %u\n", g_name, len ? f[0] >> 4 : 0u, len);
+        return;
+    }
     if (l3 == 0) {   /* packetdump.rs:202-217: ARP, otherwise unknown */
         const unsigned et = c->ethertype[i];
         char sm[24], dm[24];
@@ -198,10 +209,15 @@ int main(int argc, char** argv) {
     /* direct DMA from the mapping when it can be page-locked, staged copies otherwise */
     const int registered = bytes && pnetgpu_host_register(img, bytes) == PNETGPU_OK;
 
+    /* Ethernet captures take packetdump's chain; raw-IP ones (tun devices,
+     * LINKTYPE_RAW / IPV4 / IPV6) start at the IP header: PNETGPU_RX_L3 */
+    uint32_t linktype = 1, flags = 0;
+    int rc = bytes ? pnetgpu_pcap_info(img, bytes, &linktype, &flags) : PNETGPU_OK;
+    g_l3 = (flags & PNETGPU_RX_L3) != 0;
     pnetgpu_ctx* ctx = NULL;
     pnetgpu_ring* ring = NULL;
-    int rc = pnetgpu_ctx_create(0, &ctx);
-    if (!rc) rc = pnetgpu_ring_create(ctx, 64u << 20, 1u << 18, 0, &ring);
+    if (!rc) rc = pnetgpu_ctx_create(0, &ctx);
+    if (!rc) rc = pnetgpu_ring_create(ctx, 64u << 20, 1u << 18, flags, &ring);
     enum { kCap = 1 << 16 };
     uint64_t* offs = (uint64_t*)malloc(sizeof(uint64_t) * kCap);
     uint32_t* lens = (uint32_t*)malloc(sizeof(uint32_t) * kCap);

@@ -97,9 +97,16 @@ void pnetgpu_pcap_close(pnetgpu_pcap* p);
  * pnetgpu_ring_submit_region: from byte *pos (0 = start of file) fill up to cap
  * record descriptors (offset of each record's captured bytes in img, incl_len),
  * *n = records found, *pos = where the next call resumes (img_bytes at the end).
- * PNETGPU_EFORMAT for a bad header or a truncated record. */
+ * PNETGPU_EFORMAT for a bad header, an unsupported link type or a truncated
+ * record. Link types: Ethernet (1) and raw IP (101, 228, 229) — check
+ * pnetgpu_pcap_info for the receive flags the records need. */
 int pnetgpu_pcap_scan(const uint8_t* img, uint64_t img_bytes, uint64_t* pos, uint64_t* offsets, uint32_t* lengths,
                       uint64_t cap, uint64_t* n);
+/* The image's link type and the pnetgpu_batch / ring flags its records need:
+ * LINKTYPE_ETHERNET (1) -> 0; LINKTYPE_RAW (101), LINKTYPE_IPV4 (228),
+ * LINKTYPE_IPV6 (229) -> PNETGPU_RX_L3 (frames begin at the IP header).
+ * PNETGPU_EFORMAT for any other link type or a bad header. */
+int pnetgpu_pcap_info(const uint8_t* img, uint64_t img_bytes, uint32_t* linktype, uint32_t* rx_flags);
 
 #ifdef __cplusplus
 }

@@ -402,18 +402,37 @@ int pnetgpu_pcap_next(pnetgpu_pcap* p, const uint8_t** frame, uint32_t* len) {
     return PNETGPU_OK;
 }
 
+// Global header of an in-memory image: byte order, and the receive flags its
+// link type needs (LINKTYPE_ETHERNET 1 -> 0; LINKTYPE_RAW 101, LINKTYPE_IPV4 228,
+// LINKTYPE_IPV6 229 -> PNETGPU_RX_L3); any other link type is EFORMAT.
+static int pcap_header(const uint8_t* img, uint64_t img_bytes, bool* swap, uint32_t* linktype, uint32_t* flags) {
+    if (img_bytes < 24) return PNETGPU_EFORMAT;
+    uint32_t magic;
+    std::memcpy(&magic, img, 4);
+    if (magic == 0xa1b2c3d4u || magic == 0xa1b23c4du) *swap = false;
+    else if (magic == 0xd4c3b2a1u || magic == 0x4d3cb2a1u) *swap = true;
+    else return PNETGPU_EFORMAT;
+    *linktype = rd32(img + 20, *swap);
+    if (*linktype == 1u) *flags = 0;
+    else if (*linktype == 101u || *linktype == 228u || *linktype == 229u) *flags = PNETGPU_RX_L3;
+    else return PNETGPU_EFORMAT;
+    return PNETGPU_OK;
+}
+
+int pnetgpu_pcap_info(const uint8_t* img, uint64_t img_bytes, uint32_t* linktype, uint32_t* rx_flags) {
+    if (!img || !linktype || !rx_flags) return PNETGPU_EINVAL;
+    bool swap;
+    return pcap_header(img, img_bytes, &swap, linktype, rx_flags);
+}
+
 int pnetgpu_pcap_scan(const uint8_t* img, uint64_t img_bytes, uint64_t* pos, uint64_t* offsets, uint32_t* lengths,
                       uint64_t cap, uint64_t* n) {
     if (!img || !pos || !n || (cap && (!offsets || !lengths))) return PNETGPU_EINVAL;
     *n = 0;
-    if (img_bytes < 24) return PNETGPU_EFORMAT;
-    uint32_t magic;
-    std::memcpy(&magic, img, 4);
     bool swap;
-    if (magic == 0xa1b2c3d4u || magic == 0xa1b23c4du) swap = false;
-    else if (magic == 0xd4c3b2a1u || magic == 0x4d3cb2a1u) swap = true;
-    else return PNETGPU_EFORMAT;
-    if (rd32(img + 20, swap) != 1u) return PNETGPU_EFORMAT;   // LINKTYPE_ETHERNET
+    uint32_t linktype, flags;
+    const int rc = pcap_header(img, img_bytes, &swap, &linktype, &flags);
+    if (rc) return rc;
     uint64_t p = *pos < 24 ? 24 : *pos;
     uint64_t k = 0;
     while (k < cap && p < img_bytes) {

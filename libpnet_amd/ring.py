@@ -51,6 +51,8 @@ def _setup():
     lib.pnetgpu_host_unregister.argtypes = [vp]
     lib.pnetgpu_pcap_scan.restype = i32
     lib.pnetgpu_pcap_scan.argtypes = [vp, u64, ctypes.POINTER(u64), vp, vp, u64, ctypes.POINTER(u64)]
+    lib.pnetgpu_pcap_info.restype = i32
+    lib.pnetgpu_pcap_info.argtypes = [vp, u64, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)]
 
 
 _setup()
@@ -252,6 +254,16 @@ def pcap_index(img, batch=1 << 16):
         if pos.value >= img.nbytes or n.value == 0:
             break
     return np.concatenate(offs), np.concatenate(lens)
+
+
+def pcap_info(img):
+    """(link type, receive flags) of an in-memory pcap image: Ethernet (1) -> 0,
+    raw IP (101 / 228 / 229) -> RX_L3 (pnetgpu_pcap_info)."""
+    img = np.ascontiguousarray(img, np.uint8)
+    lt, fl = ctypes.c_uint32(), ctypes.c_uint32()
+    check(lib.pnetgpu_pcap_info(ctypes.c_void_p(img.ctypes.data), img.nbytes, ctypes.byref(lt), ctypes.byref(fl)),
+          "pnetgpu_pcap_info")
+    return lt.value, fl.value
 
 
 def pcap_frames(path):

@@ -43,13 +43,15 @@ def v6(a):
     return ":".join(h)
 
 
-def line(frame, name="pcap", csum=False):
-    r = po.rx_frame(frame)
+def line(frame, name="pcap", csum=False, l3mode=False):
+    r = po.rx_frame(frame, po.RX_L3 if l3mode else 0)
     st = r["status"]
     f = frame
     if st & po.ST_ETH_MALFORMED:
         return f"[{name}]: Malformed Ethernet Frame"
     l3 = st & 3
+    if l3 == 0 and l3mode:
+        return f"[{name}]: Unknown packet: IP version {f[0] >> 4 if f else 0}; length: {len(f)}"
     if l3 == 0:
         et = r["ethertype"]
         if et == 0x0806:

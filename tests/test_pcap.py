@@ -52,6 +52,23 @@ def test_pcap_index_rejects_truncated_and_non_ethernet(tmp_path):
     with pytest.raises(PnetGpuError):
         lp.pcap_index(img[:-10])                        # last record cut short
     bad = img.copy()
-    bad[20] = 101                                       # LINKTYPE_RAW
+    bad[20] = 113                                       # LINKTYPE_LINUX_SLL: not supported
     with pytest.raises(PnetGpuError):
         lp.pcap_index(bad)
+    with pytest.raises(PnetGpuError):
+        lp.pcap_info(bad)
+
+
+@pytest.mark.parametrize("linktype,flags", [(1, 0), (101, 4), (228, 4), (229, 4)])
+def test_pcap_info_link_types(tmp_path, linktype, flags):
+    """Ethernet captures need no flags; raw-IP ones (LINKTYPE_RAW / IPV4 / IPV6)
+    need PNETGPU_RX_L3, and index like any other."""
+    frames = [f[14:] for f in framegen.random_frames(np.random.default_rng(6), 50)] if flags else \
+        framegen.random_frames(np.random.default_rng(6), 50)
+    p = tmp_path / "t.pcap"
+    write_pcap(p, frames, linktype=linktype)
+    img = np.fromfile(p, dtype=np.uint8)
+    assert lp.pcap_info(img) == (linktype, flags)
+    assert flags == 0 or flags == lp.engine.RX_L3
+    offs, lens = lp.pcap_index(img)
+    assert [bytes(img[o:o + n]) for o, n in zip(offs, lens)] == frames

@@ -127,3 +127,22 @@ def test_pcapdump_empty_and_bad(tmp_path):
     q.write_bytes(b"not a pcap at all" * 4)
     r = subprocess.run([EXE, str(q)], capture_output=True, text=True, timeout=60)
     assert r.returncode != 0 and "pcapdump" in r.stderr
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("linktype", [101, 229])
+def test_pcapdump_raw_ip_capture(tmp_path, linktype):
+    """A raw-IP capture (tun device) runs with PNETGPU_RX_L3: the same lines as
+    the Ethernet capture of the same packets, plus the unknown-version line."""
+    rng = np.random.default_rng(79)
+    frames = special_frames(rng) + framegen.random_frames(rng, 2000)
+    pkts = [f[14:] for f in frames if len(f) >= 14] + [b"", b"\x75" + bytes(30)]
+    p = tmp_path / "raw.pcap"
+    write_pcap(p, pkts, linktype=linktype)
+    r = subprocess.run([EXE, "-c", str(p)], capture_output=True, text=True, timeout=100)
+    assert r.returncode == 0, r.stderr
+    got = r.stdout.splitlines()
+    want = [line(f, "pcap", True, l3mode=True) for f in pkts]
+    assert got == want
+    assert got[-1] == "[pcap]: Unknown packet: IP version 7; length: 31"
+
