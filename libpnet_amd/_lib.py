@@ -67,7 +67,7 @@ def _load():
     if not os.path.exists(LIB_PATH):
         raise ImportError(f"libpnet_amd: native library {LIB_PATH} is not built "
                           "(run `python -c 'import __graft_entry__ as g; g.build()'` or `make -C libpnet_amd`)")
-    L = ctypes.CDLL(LIB_PATH)
+    L = ctypes.CDLL(LIB_PATH, use_errno=True)
     vp, u64, u32, i32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int
     L.pnetgpu_abi_version.restype = i32
     L.pnetgpu_strerror.restype = ctypes.c_char_p

@@ -12,6 +12,8 @@
 #include <new>
 
 #include "pnetgpu.h"
+#include "pnetgpu_afpacket.h"
+#include "pnetgpu_ring.h"
 #include "rx_internal.h"
 
 struct pnetgpu_ctx {
@@ -54,6 +56,11 @@ const char* pnetgpu_strerror(int code) {
         case PNETGPU_ENODEV: return "no such HIP device";
         case PNETGPU_EHIP: return "HIP runtime or kernel launch failure";
         case PNETGPU_ENOMEM: return "out of memory";
+        case PNETGPU_EFULL: return "batch full: submit first";
+        case PNETGPU_EBUSY: return "every ring slot in flight: wait first";
+        case PNETGPU_EEMPTY: return "nothing to return (no batch in flight, end of file, or timeout)";
+        case PNETGPU_EFORMAT: return "malformed or unsupported capture / block format";
+        case PNETGPU_ESYS: return "operating-system call failed (see errno)";
         default: return "unknown pnetgpu error";
     }
 }
