@@ -1,8 +1,10 @@
 // host_asan_test.cpp — AddressSanitizer/UBSan run of the library's HOST code
 // (no GPU needed): the synthetic-frame producer, the classic-pcap reader and
-// the C-ABI's argument validation. Linked from objects built with
+// in-memory indexer, the TPACKET_V3 block walk (fuzzed: it parses memory the
+// OS kernel writes) and the C-ABI's argument validation. Linked from objects built with
 // -fsanitize=address,undefined (libpnet_amd/Makefile target `asan-test`), so
 // the sanitizer runtime comes with the executable itself.
+#include <algorithm>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -11,6 +13,7 @@
 #include <vector>
 
 #include "pnetgpu.h"
+#include "pnetgpu_afpacket.h"
 #include "pnetgpu_ring.h"
 #include "pnetgpu_synth.h"
 
@@ -121,7 +124,7 @@ static void test_pcap() {
 
 static void test_abi_validation() {
     CHECK(pnetgpu_abi_version() == 2);
-    for (int c = 0; c >= -8; --c) CHECK(pnetgpu_strerror(c) != nullptr && std::strlen(pnetgpu_strerror(c)) > 0);
+    for (int c = 0; c >= -9; --c) CHECK(pnetgpu_strerror(c) != nullptr && std::strlen(pnetgpu_strerror(c)) > 0);
     CHECK(pnetgpu_strerror(-1000) != nullptr);
     pnetgpu_batch b{};
     pnetgpu_rx_columns cols{};
@@ -143,10 +146,91 @@ static void test_abi_validation() {
     pnetgpu_pcap_close(nullptr);
 }
 
+// Random mutations of valid TPACKET_V3 blocks and pcap images: every call
+// returns a code, and every descriptor it reports lies inside the buffer.
+static uint64_t rng_state = 0x9E3779B97F4A7C15ull;
+static uint32_t rnd() {
+    rng_state ^= rng_state << 13;
+    rng_state ^= rng_state >> 7;
+    rng_state ^= rng_state << 17;
+    return (uint32_t)rng_state;
+}
+
+static void test_walk_fuzz() {
+    const uint32_t kBlock = 8192;
+    int ok_blocks = 0;
+    for (int iter = 0; iter < 3000; ++iter) {
+        std::vector<uint8_t> blk(kBlock, 0);
+        const uint32_t n = rnd() % 40;
+        uint32_t p = 48, last = 48;
+        uint32_t placed = 0;
+        for (uint32_t k = 0; k < n; ++k) {
+            const uint32_t snap = rnd() % 300, mac = 66;
+            if (p + mac + snap > kBlock) break;
+            const uint32_t nxt = (mac + snap + 15) & ~15u;
+            std::memcpy(&blk[p], &nxt, 4);
+            std::memcpy(&blk[p + 12], &snap, 4);
+            std::memcpy(&blk[p + 24], &mac, 2);
+            last = p;
+            p += nxt;
+            ++placed;
+        }
+        if (placed) {
+            const uint32_t zero = 0;
+            std::memcpy(&blk[last], &zero, 4);
+        }
+        const uint32_t first = 48, blk_len = placed ? std::min<uint32_t>(p, kBlock) : 48;
+        std::memcpy(&blk[12], &placed, 4);
+        std::memcpy(&blk[16], &first, 4);
+        std::memcpy(&blk[20], &blk_len, 4);
+        const int flips = (int)(rnd() % 4);                 // 0: intact
+        for (int f = 0; f < flips; ++f) blk[rnd() % std::min<uint32_t>(kBlock, p + 64)] = (uint8_t)rnd();
+        uint64_t offs[64];
+        uint32_t lens[64], st[64];
+        uint64_t got = 0;
+        const int rc = pnetgpu_tpacket3_walk(blk.data(), kBlock, 0, offs, lens, st, 64, &got);
+        if (flips == 0) CHECK(rc == 0 && got == placed);
+        if (rc == 0) {
+            ++ok_blocks;
+            for (uint64_t k = 0; k < got; ++k) CHECK(offs[k] + lens[k] <= kBlock);
+        }
+    }
+    CHECK(ok_blocks > 1000);
+    uint64_t got = 0;
+    CHECK(pnetgpu_tpacket3_walk(nullptr, 8192, 0, nullptr, nullptr, nullptr, 0, &got) == PNETGPU_EINVAL);
+}
+
+static void test_scan_fuzz() {
+    std::vector<std::vector<uint8_t>> frames;
+    for (int i = 0; i < 30; ++i) frames.push_back(std::vector<uint8_t>(rnd() % 200, (uint8_t)i));
+    const std::string path = write_pcap("fuzz", false, false, frames);
+    FILE* f = std::fopen(path.c_str(), "rb");
+    std::vector<uint8_t> img(1 << 16);
+    img.resize(std::fread(img.data(), 1, img.size(), f));
+    std::fclose(f);
+    for (int iter = 0; iter < 3000; ++iter) {
+        std::vector<uint8_t> m = img;
+        const int flips = 1 + (int)(rnd() % 3);
+        for (int k = 0; k < flips; ++k) m[rnd() % m.size()] = (uint8_t)rnd();
+        const uint64_t cut = rnd() % 3 == 0 ? rnd() % m.size() : m.size();
+        uint64_t pos = 0, n = 0, offs[16];
+        uint32_t lens[16];
+        for (int guard = 0; guard < 100 && pos < cut; ++guard) {
+            if (pnetgpu_pcap_scan(m.data(), cut, &pos, offs, lens, 16, &n) != 0) break;
+            for (uint64_t k = 0; k < n; ++k) CHECK(offs[k] + lens[k] <= cut);
+            if (n == 0) break;
+        }
+        uint32_t lt = 0, fl = 0;
+        (void)pnetgpu_pcap_info(m.data(), cut, &lt, &fl);
+    }
+}
+
 int main() {
     test_synth();
     test_pcap();
     test_abi_validation();
+    test_walk_fuzz();
+    test_scan_fuzz();
     std::printf("%s (%d failures)\n", failures ? "FAILED" : "ok", failures);
     return failures ? 1 : 0;
 }
