@@ -31,10 +31,13 @@ struct Slot {
     uint8_t* d_frames = nullptr;
     uint64_t* d_off = nullptr;
     uint32_t* d_len = nullptr;
-    void* d_cols[kNumCols] = {};
-    void* h_cols[kNumCols] = {};
-    uint64_t* d_ctr = nullptr;
-    uint64_t* h_ctr = nullptr;
+    // record columns of a batch packed back to back (each 256-B aligned, sized
+    // for the batch's n) in one device block and one pinned block: the results
+    // come back in a single D2H copy
+    uint8_t* d_rec = nullptr;
+    uint8_t* h_rec = nullptr;
+    uint64_t col_off[kNumCols] = {};
+    uint64_t rec_bytes = 0;
     hipStream_t stream = nullptr;
     hipEvent_t done = nullptr;
     uint32_t n = 0;
@@ -79,18 +82,22 @@ static void free_slot(Slot& s) {
     if (s.h_frames) (void)hipHostFree(s.h_frames);
     if (s.h_off) (void)hipHostFree(s.h_off);
     if (s.h_len) (void)hipHostFree(s.h_len);
-    if (s.h_ctr) (void)hipHostFree(s.h_ctr);
     if (s.d_frames) (void)hipFree(s.d_frames);
     if (s.d_off) (void)hipFree(s.d_off);
     if (s.d_len) (void)hipFree(s.d_len);
-    if (s.d_ctr) (void)hipFree(s.d_ctr);
-    for (int k = 0; k < kNumCols; ++k) {
-        if (s.d_cols[k]) (void)hipFree(s.d_cols[k]);
-        if (s.h_cols[k]) (void)hipHostFree(s.h_cols[k]);
-    }
+    if (s.d_rec) (void)hipFree(s.d_rec);
+    if (s.h_rec) (void)hipHostFree(s.h_rec);
     if (s.done) (void)hipEventDestroy(s.done);
     if (s.stream) (void)hipStreamDestroy(s.stream);
     s = Slot{};
+}
+
+// Bytes of the packed record block for up to n frames: the counters, then
+// every column, each start rounded up to 256 B.
+static size_t rec_capacity(uint64_t n) {
+    size_t b = 8ull * PNETGPU_NCOUNTERS;
+    for (int k = 0; k < kNumCols; ++k) b += 256 + (size_t)kColBytes[k] * n;
+    return b;
 }
 
 static int take_free_slot(pnetgpu_ring* r) {
@@ -130,17 +137,15 @@ int pnetgpu_ring_create(pnetgpu_ctx* ctx, uint64_t batch_bytes, uint32_t batch_f
         ok = hipHostMalloc((void**)&s.h_frames, fb, hipHostMallocDefault) == hipSuccess &&
              hipHostMalloc((void**)&s.h_off, 8ull * batch_frames, hipHostMallocDefault) == hipSuccess &&
              hipHostMalloc((void**)&s.h_len, 4ull * batch_frames, hipHostMallocDefault) == hipSuccess &&
-             hipHostMalloc((void**)&s.h_ctr, 8ull * PNETGPU_NCOUNTERS, hipHostMallocDefault) == hipSuccess &&
              hipMalloc((void**)&s.d_frames, fb) == hipSuccess &&
              hipMalloc((void**)&s.d_off, 8ull * batch_frames) == hipSuccess &&
              hipMalloc((void**)&s.d_len, 4ull * batch_frames) == hipSuccess &&
-             hipMalloc((void**)&s.d_ctr, 8ull * PNETGPU_NCOUNTERS) == hipSuccess &&
              hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking) == hipSuccess &&
              hipEventCreateWithFlags(&s.done, hipEventDisableTiming) == hipSuccess;
-        for (int k = 0; k < kNumCols && ok; ++k) {
-            const size_t cb = (size_t)kColBytes[k] * batch_frames;
-            ok = hipMalloc(&s.d_cols[k], cb) == hipSuccess &&
-                 hipHostMalloc(&s.h_cols[k], cb, hipHostMallocDefault) == hipSuccess;
+        if (ok) {
+            const size_t rb = rec_capacity(batch_frames);
+            ok = hipMalloc((void**)&s.d_rec, rb) == hipSuccess &&
+                 hipHostMalloc((void**)&s.h_rec, rb, hipHostMallocDefault) == hipSuccess;
         }
         if (ok) std::memset(s.h_frames + batch_bytes, 0, 32);
     }
@@ -235,7 +240,7 @@ static int ship_slot(pnetgpu_ring* r, Slot& s, const uint8_t* src, uint64_t* id)
         (src != s.h_frames && hipMemsetAsync(s.d_frames + s.bytes, 0, 32, st) != hipSuccess) ||
         hipMemcpyAsync(s.d_off, s.h_off, 8ull * s.n, hipMemcpyHostToDevice, st) != hipSuccess ||
         hipMemcpyAsync(s.d_len, s.h_len, 4ull * s.n, hipMemcpyHostToDevice, st) != hipSuccess ||
-        hipMemsetAsync(s.d_ctr, 0, 8ull * PNETGPU_NCOUNTERS, st) != hipSuccess)
+        hipMemsetAsync(s.d_rec, 0, 8ull * PNETGPU_NCOUNTERS, st) != hipSuccess)
         return PNETGPU_EHIP;
     pnetgpu_batch b{};
     b.data = s.d_frames;
@@ -245,17 +250,20 @@ static int ship_slot(pnetgpu_ring* r, Slot& s, const uint8_t* src, uint64_t* id)
     b.lengths = s.d_len;
     b.flags = r->flags;
     pnetgpu_rx_columns c{};
-    for (int k = 0; k < kNumCols; ++k) *col_slot(c, k) = (r->col_mask >> k) & 1u ? s.d_cols[k] : nullptr;
-    c.counters = s.d_ctr;
+    uint64_t at = 8ull * PNETGPU_NCOUNTERS;          // the counters lead the record block
+    for (int k = 0; k < kNumCols; ++k) {
+        if (!((r->col_mask >> k) & 1u)) continue;
+        at = (at + 255) & ~255ull;
+        s.col_off[k] = at;
+        *col_slot(c, k) = s.d_rec + at;
+        at += (uint64_t)kColBytes[k] * s.n;
+    }
+    s.rec_bytes = at;
+    c.counters = reinterpret_cast<uint64_t*>(s.d_rec);
     int rc = pnetgpu_rx_process(r->ctx, &b, &c, st);
     if (rc) return rc;
-    for (int k = 0; k < kNumCols; ++k)
-        if (((r->col_mask >> k) & 1u) &&
-            hipMemcpyAsync(s.h_cols[k], s.d_cols[k], (size_t)kColBytes[k] * s.n, hipMemcpyDeviceToHost, st) !=
-                hipSuccess)
-            return PNETGPU_EHIP;
     s.col_mask = r->col_mask;
-    if (hipMemcpyAsync(s.h_ctr, s.d_ctr, 8ull * PNETGPU_NCOUNTERS, hipMemcpyDeviceToHost, st) != hipSuccess ||
+    if (hipMemcpyAsync(s.h_rec, s.d_rec, at, hipMemcpyDeviceToHost, st) != hipSuccess ||   // counters + records
         hipEventRecord(s.done, st) != hipSuccess)
         return PNETGPU_EHIP;
     s.state = kInFlight;
@@ -324,8 +332,9 @@ int pnetgpu_ring_wait(pnetgpu_ring* r, pnetgpu_ring_batch* out) {
     out->offsets = s.h_off;
     out->lengths = s.h_len;
     std::memset(&out->cols, 0, sizeof(out->cols));
-    for (int k = 0; k < kNumCols; ++k) *col_slot(out->cols, k) = (s.col_mask >> k) & 1u ? s.h_cols[k] : nullptr;
-    out->cols.counters = s.h_ctr;
+    for (int k = 0; k < kNumCols; ++k)
+        *col_slot(out->cols, k) = (s.col_mask >> k) & 1u ? static_cast<void*>(s.h_rec + s.col_off[k]) : nullptr;
+    out->cols.counters = reinterpret_cast<uint64_t*>(s.h_rec);
     return PNETGPU_OK;
 }
 
