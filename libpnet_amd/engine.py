@@ -16,6 +16,7 @@ HIP kernels of libpnetgpu.so. Unsigned columns are stored in signed torch dtypes
 of the same width; RxResult.numpy() returns the unsigned views.
 """
 import ctypes
+from contextlib import nullcontext as _nullcontext
 
 import numpy as np
 import torch
@@ -104,15 +105,35 @@ def _ptr(t):
 
 
 class RxResult:
-    """Device-resident result columns of one rx_process call."""
+    """Device-resident result columns of one rx_process call, packed back to back
+    (each 256-B aligned) in one allocation, `block`: the counters first, then
+    the columns, so the whole record moves to the host in one copy (to_host)."""
 
     def __init__(self, n, device, columns=IPV4_COLUMNS, counters=True):
         self.n = n
-        self.columns = {}
+        layout, at = [], 8 * NCOUNTERS if counters else 0
         for c in columns:
             dt, _, shape = COLUMNS[c]
-            self.columns[c] = torch.empty((n,) + shape, dtype=dt, device=device)
-        self.counters = torch.zeros(NCOUNTERS, dtype=torch.int64, device=device) if counters else None
+            at = (at + 255) & ~255
+            nbytes = n * int(np.prod(shape, dtype=np.int64)) * torch.empty((), dtype=dt).element_size()
+            layout.append((c, at, nbytes, dt, shape))
+            at += nbytes
+        self.block = torch.empty(max(at, 1), dtype=torch.uint8, device=device)
+        self.columns = {c: self.block[o:o + nb].view(dt).view((n,) + shape) for c, o, nb, dt, shape in layout}
+        self.counters = None
+        if counters:
+            self.counters = self.block[:8 * NCOUNTERS].view(torch.int64)
+            self.counters.zero_()
+        self.nbytes = at
+
+    def to_host(self, out=None, stream=None):
+        """Copy counters + columns to host memory in one D2H (out: a pinned
+        uint8 tensor of at least nbytes, or None for a new one); returns out."""
+        if out is None:
+            out = torch.empty(self.nbytes, dtype=torch.uint8).pin_memory()
+        with torch.cuda.stream(stream) if stream is not None else _nullcontext():
+            out[:self.nbytes].copy_(self.block[:self.nbytes], non_blocking=True)
+        return out
 
     def c_struct(self):
         cols = RxColumns()

@@ -409,3 +409,23 @@ def test_maximum_sizes_all_ones():
     want = coracle.checksum_slices(big, offs_s.astype(np.uint64), lens_s.astype(np.uint32), skips.astype(np.uint32))
     got = lp.checksum_slices(to_dev(big), to_dev(offs_s), to_dev(lens_s), to_dev(skips))
     assert np.array_equal(got.cpu().numpy().view(np.uint16), want)
+
+
+def test_packed_result_block_to_host():
+    """RxResult keeps counters + columns in one block; to_host moves them in one
+    copy and the host bytes hold exactly the device columns."""
+    rng = np.random.default_rng(12)
+    frames = framegen.random_frames(rng, 3000)
+    buf, offs, lens = framegen.pack(frames, gap=4, rng=rng)
+    res = run_desc(buf, offs, lens)
+    host = res.to_host()
+    torch.cuda.synchronize()
+    h = host.numpy()
+    base = res.block.data_ptr()
+    for c, t in res.columns.items():
+        o = t.data_ptr() - base
+        assert o % 256 == 0
+        got = h[o:o + t.numel() * t.element_size()].view(COLUMNS[c][1]).reshape(t.shape)
+        assert np.array_equal(got, t.cpu().numpy().view(COLUMNS[c][1]))
+    assert np.array_equal(h[:64].view(np.uint64), res.counters.cpu().numpy().view(np.uint64))
+    compare(res, oracle_desc(buf, offs, lens))
