@@ -34,7 +34,7 @@ WORKLOADS = {
                                     "device-resident batch"},
     "tcp1500": {"n": 1 << 20, "kernel": "rx_kernel<8, 8, 4, false, 1, false, false> (MTU, unified pass)", "desc": "configs[2]: 1500B TCP/IPv4/Ethernet, full-MTU ones-complement sum over "
                                       "pseudo-header+payload"},
-    # not in the default run: the 8-GPU configs, per-GPU shard sizes (weak scaling)
+    # BASELINE's 8-GPU configs, per-GPU shard sizes (weak scaling); secondary lines
     "imix": {"n": 1 << 22, "kernel": "rx_kernel<8, 4, 8, false, 0, true, false> (mixed, dynamic tail queue)",
              "desc": "configs[3]: IMIX 64/576/1500B 7:4:1 Eth/IPv4/{UDP,TCP,ICMP}, descriptor mode, per-GPU shard"},
     "udp6_jumbo": {"n": 1 << 17, "kernel": "rx_kernel<8, 64, 9, true, 0, false, false> (jumbo)",
@@ -355,7 +355,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workloads", default="udp64,tcp1500")
+    ap.add_argument("--workloads", default="udp64,tcp1500,imix,udp6_jumbo",
+                    help="first one is the headline `value`; the others are reported under `workloads`")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the TX-fill and checksum-slices rates")
