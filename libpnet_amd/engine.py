@@ -161,14 +161,15 @@ def _check_u8_cuda(t, what):
 
 
 def rx_process(data, *, n_frames=None, stride=0, frame_len=None, first_offset=0, offsets=None, lengths=None,
-               columns=IPV4_COLUMNS, counters=True, out=None, stream=None, data_bytes=None, flags=0):
+               columns=IPV4_COLUMNS, counters=True, out=None, stream=None, data_bytes=None, flags=0, ctx=None):
     """Parse + verify every frame of a device-resident batch.
 
     Fixed-stride mode: stride > 0, frame i = data[first_offset + i*stride, +frame_len).
     Descriptor mode:   offsets (int64) / lengths (int32) CUDA tensors, frame i = data[off_i, +len_i).
+    ctx: a Context (default: one shared per device); one host thread per context at a time.
     Returns an RxResult (device columns, accumulated counters)."""
     return _rx_or_tx("pnetgpu_rx_process", data, n_frames, stride, frame_len, first_offset, offsets, lengths,
-                     columns, counters, out, stream, data_bytes, flags)
+                     columns, counters, out, stream, data_bytes, flags, ctx)
 
 
 def tx_fill_checksums(data, *, n_frames=None, stride=0, frame_len=None, first_offset=0, offsets=None,
@@ -183,7 +184,7 @@ def tx_fill_checksums(data, *, n_frames=None, stride=0, frame_len=None, first_of
 
 
 def _rx_or_tx(fn_name, data, n_frames, stride, frame_len, first_offset, offsets, lengths, columns, counters, out,
-              stream, data_bytes, flags):
+              stream, data_bytes, flags, ctx=None):
     _check_u8_cuda(data, "data")
     if stride:
         if n_frames is None:
@@ -204,7 +205,8 @@ def _rx_or_tx(fn_name, data, n_frames, stride, frame_len, first_offset, offsets,
               stride, frame_len, offsets.data_ptr() if offsets is not None else 0,
               lengths.data_ptr() if lengths is not None else 0, flags, 0)
     cols = out.c_struct()
-    ctx = context(data.device.index)
+    if ctx is None:
+        ctx = context(data.device.index)
     check(getattr(lib, fn_name)(ctx.handle, ctypes.byref(b), ctypes.byref(cols),
                                 _stream_handle(stream, data.device)), fn_name)
     return out

@@ -429,3 +429,40 @@ def test_packed_result_block_to_host():
         assert np.array_equal(got, t.cpu().numpy().view(COLUMNS[c][1]))
     assert np.array_equal(h[:64].view(np.uint64), res.counters.cpu().numpy().view(np.uint64))
     compare(res, oracle_desc(buf, offs, lens))
+
+
+def test_concurrent_contexts_from_host_threads():
+    """Header contract: distinct contexts are independent. Four host threads,
+    each with its own context and stream, process different batches at once
+    (ctypes releases the GIL inside the C-ABI call): every record bit-exact."""
+    import threading
+    rng = np.random.default_rng(21)
+    jobs = []
+    for t in range(4):
+        frames = framegen.random_frames(rng, 2500, max_len=3000)
+        buf, offs, lens = framegen.pack(frames, gap=t, rng=rng)
+        jobs.append((buf, offs, lens, oracle_desc(buf, offs, lens)))
+    results, errors = [None] * 4, []
+
+    def work(t):
+        try:
+            buf, offs, lens, _ = jobs[t]
+            ctx = lp.engine.Context(0)
+            s = torch.cuda.Stream(DEV)
+            with torch.cuda.stream(s):
+                d, o, ln = to_dev(buf), to_dev(offs.astype(np.int64)), to_dev(lens.astype(np.int32))
+                for _ in range(5):
+                    res = lp.rx_process(d, offsets=o, lengths=ln, columns=ALL_COLUMNS, stream=s, ctx=ctx)
+            s.synchronize()
+            results[t] = res
+        except Exception as e:                    # surfaced below
+            errors.append(e)
+
+    th = [threading.Thread(target=work, args=(t,)) for t in range(4)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not errors, errors
+    for t in range(4):
+        compare(results[t], jobs[t][3])
