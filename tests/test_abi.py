@@ -17,7 +17,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def declared_functions():
     names = set()
-    for h in _lib.HEADERS:
+    headers = sorted(os.path.join(ROOT, "include", h) for h in os.listdir(os.path.join(ROOT, "include"))
+                     if h.endswith(".h"))
+    assert set(_lib.HEADERS) == set(headers), "libpnet_amd._lib.HEADERS must list every public header"
+    for h in headers:
         src = open(h).read()
         src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
         names |= set(re.findall(r"\b(pnetgpu_\w+)\s*\(", src))
@@ -38,7 +41,7 @@ def test_exports_every_declared_symbol():
 
 def test_abi_version_and_strerror():
     assert lp.lib.pnetgpu_abi_version() == lp.DEFS["PNETGPU_ABI_VERSION"] == 2
-    for code in (0, -1, -2, -3, -4, -99):
+    for code in (0, -1, -2, -3, -4, -5, -6, -7, -8, -9, -99):
         assert lp.lib.pnetgpu_strerror(code)
 
 
@@ -69,6 +72,6 @@ def test_argument_validation_without_gpu():
 
 
 def test_include_headers_compile_as_c():
-    for h in ("pnetgpu.h", "pnetgpu_synth.h"):
+    for h in ("pnetgpu.h", "pnetgpu_synth.h", "pnetgpu_ring.h", "pnetgpu_afpacket.h"):
         subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-fsyntax-only", "-x", "c",
                         os.path.join(ROOT, "include", h)], check=True)
