@@ -39,6 +39,12 @@ WORKLOADS = {
              "desc": "configs[3]: IMIX 64/576/1500B 7:4:1 Eth/IPv4/{UDP,TCP,ICMP}, descriptor mode, per-GPU shard"},
     "udp6_jumbo": {"n": 1 << 17, "kernel": "rx_kernel<8, 64, 9, true, 0, false, false> (jumbo)",
                    "desc": "configs[4]: 9000B IPv6/UDP jumbo frames, IPv6 pseudo-header checksum, per-GPU shard"},
+    # configs[1]'s frames with the verify-only record (status + both computed
+    # checksums, R = 6 B/frame; SURVEY.md §8(d) priced the target with R = 8):
+    # the same kernel, a consumer that reads no extracted fields
+    "udp64_verify": {"n": 1 << 24, "synth": "udp64", "columns": ("status", "ip_csum", "l4_csum"),
+                     "kernel": "rx_small_kernel",
+                     "desc": "configs[1] frames, checksum verify only (status + ip_csum + l4_csum columns)"},
 }
 
 
@@ -51,16 +57,18 @@ class Shard:
 
     def __init__(self, name, n, seed, device):
         self.name, self.n = name, n
-        w = lp.synth.make(name, n, seed=seed, corrupt_ppm=10000)
+        cfg = WORKLOADS.get(name, {})
+        columns = cfg.get("columns", lp.IPV4_COLUMNS)
+        w = lp.synth.make(cfg.get("synth", name), n, seed=seed, corrupt_ppm=10000)
         self.w = w
         self.data = torch.from_numpy(w.buf).to(device)
         self.offsets = self.lengths = None
         if not w.stride:
             self.offsets = torch.from_numpy(w.offsets.view(np.int64)).to(device)
             self.lengths = torch.from_numpy(w.lengths.view(np.int32)).to(device)
-        self.res = lp.RxResult(n, device, lp.IPV4_COLUMNS, counters=True)
+        self.res = lp.RxResult(n, device, columns, counters=True)
         self.frame_bytes = w.expect["bytes"]
-        self.result_bytes = lp.column_bytes(lp.IPV4_COLUMNS)
+        self.result_bytes = lp.column_bytes(columns)
         self.desc_bytes = 0 if w.stride else 12          # u64 offset + u32 length
         # algorithmic bytes per launch: frames read once + result columns written + descriptors
         self.alg_bytes = self.frame_bytes + n * (self.result_bytes + self.desc_bytes)
@@ -355,7 +363,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workloads", default="udp64,tcp1500,imix,udp6_jumbo",
+    ap.add_argument("--workloads", default="udp64,tcp1500,imix,udp6_jumbo,udp64_verify",
                     help="first one is the headline `value`; the others are reported under `workloads`")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
@@ -456,12 +464,12 @@ def main():
                 "roofline_frac": round(r["achieved_gbs"] / HBM_PEAK_GBS, 4),
                 "achieved_gbs": round(r["achieved_gbs"], 1), "counters_ok": r["counters_ok"],
                 "traffic": load_traffic(name), "kernel": WORKLOADS[name]["kernel"],
-                "alg_bytes_per_launch": r["sh"].alg_bytes,
+                "alg_bytes_per_launch": r["sh"].alg_bytes, "result_bytes_per_frame": r["sh"].result_bytes,
             }
         if world == 1 and not args.no_cpu:
             line["cpu_baseline"] = cpu_baseline(sh)
             for name, r in results.items():
-                if name != primary:
+                if name != primary and "synth" not in WORKLOADS[name]:   # not for a re-run of the same frames
                     line["workloads"][name]["cpu_baseline"] = cpu_baseline(r["sh"], budget_cpu_s=6.0)
         if world == 1 and not args.no_extra:
             line["tx_fill"] = tx_fill_rate(sh, args.steps, args.warmup, device)
