@@ -466,3 +466,44 @@ def test_concurrent_contexts_from_host_threads():
     assert not errors, errors
     for t in range(4):
         compare(results[t], jobs[t][3])
+
+
+@pytest.mark.parametrize("kind", ["udp64", "tcp1500"])
+def test_batches_past_4gib(kind):
+    """64-bit addressing: a 4.5-5 GiB fixed-stride batch (the 1-GiB-class synth
+    batch tiled on the device) — counters are the tile's times the tile count,
+    and the records of the frames past 4 GiB equal the oracle's for their
+    source frames; then a descriptor batch whose frames all sit past 4 GiB."""
+    n0 = {"udp64": 1 << 24, "tcp1500": 1 << 20}[kind]
+    w = lp.synth.make(kind, n0, seed=3, corrupt_ppm=10000)
+    tile = torch.from_numpy(w.buf[: n0 * w.stride]).to(DEV)
+    reps = 5 if kind == "udp64" else 3
+    big = torch.cat([tile] * reps + [torch.zeros(64, dtype=torch.uint8, device=DEV)])
+    n = n0 * reps
+    assert n * w.stride > (1 << 32) + (1 << 28)
+    res = lp.rx_process(big, stride=w.stride, frame_len=w.frame_len, n_frames=n, columns=IPV4_COLS_ALL)
+    torch.cuda.synchronize()
+    c = res.counter_dict()
+    assert c["frames"] == n and c["ip_csum_bad"] == reps * w.expect["ip_bad"]
+    assert c["l4_csum_bad"] == reps * w.expect["l4_bad"] and c["bytes"] == reps * w.expect["bytes"]
+    k = 1 << 14                                    # the last k frames: all past 4 GiB
+    src0 = n0 - k
+    rec = coracle.rx_batch(w.buf[src0 * w.stride:(src0 + k) * w.stride + 64], k, stride=w.stride,
+                           frame_len=w.frame_len)
+    got = {col: t[n - k:].cpu().numpy().view(COLUMNS[col][1]) for col, t in res.columns.items()}
+    for col, v in got.items():
+        assert np.array_equal(v, rec[col]), col
+    # descriptor mode, every frame past 4 GiB (offsets > 2^32)
+    first = n - k
+    offs = (torch.arange(k, dtype=torch.int64, device=DEV) + first) * w.stride
+    lens = torch.full((k,), w.frame_len, dtype=torch.int32, device=DEV)
+    assert int(offs[0]) > (1 << 32)
+    res2 = lp.rx_process(big, offsets=offs, lengths=lens, columns=IPV4_COLS_ALL)
+    torch.cuda.synchronize()
+    for col, t in res2.columns.items():
+        assert np.array_equal(t.cpu().numpy().view(COLUMNS[col][1]), rec[col]), col
+    del big, tile, res, res2
+    torch.cuda.empty_cache()
+
+
+IPV4_COLS_ALL = lp.IPV4_COLUMNS
