@@ -19,6 +19,8 @@
 struct pnetgpu_ctx {
     int device;
     int cus;
+    // resident blocks per CU of each receive kernel (kind x EXT), queried once
+    int per_cu[8][2] = {};
 };
 
 namespace pnetgpu {
@@ -140,25 +142,30 @@ static int rx_common(pnetgpu_ctx* ctx, const pnetgpu_batch* b, const pnetgpu_rx_
         else
             kind = b->frame_len >= 4096 ? pnetgpu::kKindJumbo : pnetgpu::kKindMtu;
     }
-    if (const char* e = std::getenv("PNETGPU_RX_KIND")) {          // tuning override
-        const int v = std::atoi(e);
+    // tuning overrides (read per call: tests and tools flip them at run time)
+    const char* kind_env = std::getenv("PNETGPU_RX_KIND");
+    const char* per_cu_env = std::getenv("PNETGPU_BLOCKS_PER_CU");
+    const char* debug_env = std::getenv("PNETGPU_DEBUG");
+    const bool debug = debug_env && *debug_env == '1';
+    if (kind_env) {
+        const int v = std::atoi(kind_env);
         if ((v == pnetgpu::kKindMixed || v == pnetgpu::kKindMtu || v == pnetgpu::kKindJumbo ||
              (v == pnetgpu::kKindStream && stream_ok)) &&
             kind != pnetgpu::kKindSmall)
             kind = v;
     }
-    int numregs = 0, lds = 0;
-    int per_cu = pnetgpu::rx_blocks_per_cu(kind, b->flags != 0, &numregs, &lds);
-    if (per_cu <= 0) return PNETGPU_EHIP;
-    if (const char* e = std::getenv("PNETGPU_BLOCKS_PER_CU")) {   // tuning override
-        const int v = std::atoi(e);
-        if (v > 0) per_cu = v;
-    }
-    if (const char* e = std::getenv("PNETGPU_DEBUG")) {
-        if (*e == '1')
+    const int ext = b->flags != 0;
+    int& per_cu_cached = ctx->per_cu[kind & 7][ext];
+    if (per_cu_cached <= 0 || debug) {                             // first use of this kernel on ctx
+        int numregs = 0, lds = 0;
+        per_cu_cached = pnetgpu::rx_blocks_per_cu(kind, ext, &numregs, &lds);
+        if (debug)
             std::fprintf(stderr, "[pnetgpu] rx kind=%d regs=%d lds=%d blocks/cu=%d cus=%d\n", kind, numregs, lds,
-                         per_cu, ctx->cus);
+                         per_cu_cached, ctx->cus);
     }
+    if (per_cu_cached <= 0) return PNETGPU_EHIP;
+    const int per_cu_v = per_cu_env ? std::atoi(per_cu_env) : 0;
+    const int per_cu = per_cu_v > 0 ? per_cu_v : per_cu_cached;
     const uint64_t wpb = (uint64_t)pnetgpu::rx_waves_per_block(kind);
     const uint64_t want = (a.nruns + wpb - 1) / wpb;
     const uint64_t cap = (uint64_t)ctx->cus * (uint64_t)per_cu;

@@ -507,3 +507,16 @@ def test_batches_past_4gib(kind):
 
 
 IPV4_COLS_ALL = lp.IPV4_COLUMNS
+
+
+def test_empty_batches():
+    """n_frames == 0 is a no-op in every mode (no launch, counters untouched)."""
+    d = torch.zeros(64, dtype=torch.uint8, device=DEV)
+    e64 = torch.zeros(0, dtype=torch.int64, device=DEV)
+    e32 = torch.zeros(0, dtype=torch.int32, device=DEV)
+    res = lp.rx_process(d, offsets=e64, lengths=e32, columns=ALL_COLUMNS)
+    res2 = lp.rx_process(d, stride=64, frame_len=64, n_frames=0, columns=ALL_COLUMNS)
+    lp.tx_fill_checksums(d, stride=64, frame_len=64, n_frames=0)
+    torch.cuda.synchronize()
+    assert res.counter_dict()["frames"] == 0 and res2.counter_dict()["frames"] == 0
+    assert int(d.sum()) == 0
