@@ -1,0 +1,429 @@
+// rx_common.h — shared device code: arithmetic helpers, the per-lane receive dispatch (parse_frame), window sums, finalize, TX write-back, counters and column stores
+// Part of the receive-path kernels; included once, by rx_kernel.hip (one
+// translation unit, so every kernel still sees the shared device helpers inline).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "pnetgpu.h"
+#include "rx_internal.h"
+
+namespace pnetgpu {
+namespace {
+
+constexpr int kWave = 64;
+constexpr int kWavesPerBlock = 4;
+constexpr int kBlock = kWave * kWavesPerBlock;
+
+// ---- arithmetic helpers ----------------------------------------------------
+__device__ __forceinline__ uint32_t fold16(uint32_t x) {
+    x = (x & 0xFFFFu) + (x >> 16);
+    x = (x & 0xFFFFu) + (x >> 16);
+    return x;
+}
+__device__ __forceinline__ uint32_t bswap16(uint32_t x) { return ((x & 0xFFu) << 8) | ((x >> 8) & 0xFFu); }
+// mask of the first x bytes of a dword, x in [0, 4]
+__device__ __forceinline__ uint32_t first_bytes(int x) { return (uint32_t)(0xFFFFFFFFull >> (32 - 8 * x)); }
+__device__ __forceinline__ int clamp04(int v) { return min(max(v, 0), 4); }
+// LE 16-bit halves of d added to acc (v_sad_u16 with a zero operand)
+__device__ __forceinline__ uint32_t sad(uint32_t d, uint32_t acc) { return __builtin_amdgcn_sad_u16(d, 0u, acc); }
+// 16-B streaming load (read once: non-temporal hint)
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 load16_nt(const void* p) {
+    const u32x4_t v = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+// 16-B load with the default cache policy (granules other lanes/instructions
+// of the same wave touch again: windows, strided per-lane frames)
+__device__ __forceinline__ uint4 load16(const void* p) { return *reinterpret_cast<const uint4*>(p); }
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// ---- LDS access --------------------------------------------------------------
+
+// 16 bytes of a run [p, p+16) of an LDS slot at any alignment, as 4 LE dwords.
+__device__ __forceinline__ uint4 lds_read16_unaligned(const uint8_t* slot, int p) {
+    const uint32_t* s32 = reinterpret_cast<const uint32_t*>(slot);
+    const int q = p >> 2, sh = (p & 3);
+    const uint32_t d0 = s32[q], d1 = s32[q + 1], d2 = s32[q + 2], d3 = s32[q + 3], d4 = s32[q + 4];
+    uint4 r;
+    r.x = __builtin_amdgcn_alignbyte(d1, d0, sh);
+    r.y = __builtin_amdgcn_alignbyte(d2, d1, sh);
+    r.z = __builtin_amdgcn_alignbyte(d3, d2, sh);
+    r.w = __builtin_amdgcn_alignbyte(d4, d3, sh);
+    return r;
+}
+
+// ---- the reference's receive dispatch, restated for one lane ---------------
+// Fields of one frame plus the two summed ranges, frame-relative:
+//   A = [a_lo, a_hi)  the IPv4 header, or the IPv6 pseudo-header address bytes
+//   B = [b_lo, b_hi)  the L4 slice
+// with a_lo <= a_hi <= b_lo <= b_hi (empty ranges collapse onto their neighbour).
+struct Parsed {
+    uint32_t st, et, proto, ttl, l4off, l4len, sp, dp, s4, d4, ipstored, l4stored, pseudo, vlan_tci, l3;
+    int a_lo, a_hi, b_lo, b_hi;
+    int l4csum_at;            // frame offset of the L4 checksum field (valid when l4do)
+    bool is_v4, l4do, v6pseudo;
+};
+
+// Frame bytes for the parse: the LDS window W holds bytes [0, wlim); anything
+// past it (long IPv6 extension chains, L4 headers behind them) is read from the
+// frame in HBM through G. The IPv4 header and VLAN tags always fit the window.
+struct FrameBytes {
+    const uint8_t* W;
+    const uint8_t* G;
+    int wlim;
+    __device__ __forceinline__ uint32_t near8(int p) const { return W[p]; }
+    __device__ __forceinline__ uint32_t near16(int p) const { return (near8(p) << 8) | near8(p + 1); }
+    __device__ __forceinline__ uint32_t near32(int p) const { return (near16(p) << 16) | near16(p + 2); }
+    __device__ __forceinline__ uint32_t far8(int p) const {
+        if (p < wlim) return W[p];
+        return G[p];
+    }
+    __device__ __forceinline__ uint32_t far16(int p) const { return (far8(p) << 8) | far8(p + 1); }
+};
+
+__device__ __forceinline__ bool is_vlan_tpid(uint32_t et) { return et == 0x8100u || et == 0x88A8u || et == 0x9100u; }
+
+// Generic parse of one frame of `len` bytes (FLAGS: PNET_RX_* extensions).
+// packetdump.rs:155-217 + ipv4.rs:165-178,226-243 + ipv6.rs:21-137 + vlan.rs:62-72
+// + udp/tcp/icmp layouts and minimum sizes (decorator.rs:593-600) + payload
+// bounds (decorator.rs:713-769). Mirrors oracle_rx_frame_ex.
+__device__ __forceinline__ Parsed parse_frame(const FrameBytes& F, uint32_t len, uint32_t flags) {
+    Parsed P{};
+    uint32_t et;
+    int l3;
+    if (flags & PNETGPU_RX_L3) {                       // IP header at byte 0: version nibble
+        const uint32_t ver = len ? F.near8(0) >> 4 : 0u;
+        et = ver == 4u ? 0x0800u : ver == 6u ? 0x86DDu : 0u;
+        l3 = 0;
+    } else {
+        if (len < 14) {
+            P.st = PNET_ST_ETH_MALFORMED;              // EthernetPacket::new == None
+            return P;
+        }
+        et = F.near16(12);
+        l3 = 14;
+    }
+    if ((flags & (PNETGPU_RX_VLAN | PNETGPU_RX_L3)) == PNETGPU_RX_VLAN) {
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            if (!is_vlan_tpid(et)) break;
+            P.st |= PNET_ST_VLAN;
+            if (len < (uint32_t)l3 + 4u) {               // VlanPacket::new == None
+                P.et = et;
+                P.st |= PNET_ST_L3_MALFORMED;
+                return P;
+            }
+            if (k == 0) P.vlan_tci = F.near16(l3);
+            et = F.near16(l3 + 2);
+            l3 += 4;
+        }
+    }
+    P.et = et;
+    P.l3 = (uint32_t)l3;
+    const uint32_t eplen = len - (uint32_t)l3;            // Ethernet payload: unbounded
+    bool l3ok = false, v6 = false;
+    uint32_t l4s = 0, l4n = 0;                            // L4 slice [l4s, l4s + l4n)
+    bool has_l4 = false;
+    if (et == 0x0800u) {
+        P.st |= PNET_ST_L3_IPV4;
+        if (eplen < 20) {
+            P.st |= PNET_ST_L3_MALFORMED;
+        } else {
+            l3ok = true;
+            P.is_v4 = true;
+            const uint32_t ihl4 = (F.near8(l3) & 15u) * 4u;
+            const uint32_t hl = min(max(ihl4, 20u), eplen);   // ipv4.rs:169-175
+            const uint32_t tl = F.near16(l3 + 2);
+            P.ttl = F.near8(l3 + 8);
+            P.proto = F.near8(l3 + 9);
+            P.ipstored = F.near16(l3 + 10);
+            P.s4 = F.near32(l3 + 12);
+            P.d4 = F.near32(l3 + 16);
+            P.a_lo = l3;
+            P.a_hi = l3 + (int)hl;
+            const uint32_t start = max(20u, ihl4);             // 20 + ipv4_options_length
+            const uint32_t plen = tl > ihl4 ? tl - ihl4 : 0u;  // ipv4_payload_length
+            if (eplen > start) {
+                has_l4 = true;
+                l4s = (uint32_t)l3 + start;
+                l4n = min(start + plen, eplen) - start;
+            }
+        }
+    } else if (et == 0x86DDu) {
+        P.st |= PNET_ST_L3_IPV6;
+        if (eplen < 40) {
+            P.st |= PNET_ST_L3_MALFORMED;
+        } else {
+            l3ok = true;
+            v6 = true;
+            P.proto = F.near8(l3 + 6);
+            P.ttl = F.near8(l3 + 7);
+            const uint32_t pl = F.near16(l3 + 4);
+            uint32_t pln = 0;                                   // #[length = "payload_length"]
+            if (eplen > 40) pln = min(40u + pl, eplen) - 40u;
+            const int pbase = l3 + 40;
+            uint32_t pos = 0;
+            if (flags & PNETGPU_RX_IPV6_EXT) {                  // ipv6.rs:39-137
+                uint32_t nh = P.proto;
+                for (int k = 0; k < 4; ++k) {
+                    if (nh == 0 || nh == 60 || nh == 43) {
+                        const uint32_t minl = nh == 43 ? 4u : 2u;
+                        if (pln - pos < minl) { P.proto = nh; P.st |= PNET_ST_L4_MALFORMED; return P; }
+                        const uint32_t el = F.far8(pbase + (int)pos + 1) * 8u + 8u;
+                        if (el > pln - pos) { P.proto = nh; P.st |= PNET_ST_L4_MALFORMED; return P; }
+                        nh = F.far8(pbase + (int)pos);
+                        pos += el;
+                    } else if (nh == 44) {
+                        if (pln - pos < 8u) { P.proto = nh; P.st |= PNET_ST_L4_MALFORMED; return P; }
+                        const uint32_t fo = F.far16(pbase + (int)pos + 2);
+                        nh = F.far8(pbase + (int)pos);
+                        pos += 8;
+                        if (fo & 0xFFFCu) {                     // not the first fragment
+                            P.proto = nh;
+                            P.st |= PNET_ST_FRAGMENT;
+                            if (pln > pos) {
+                                P.l4off = (uint32_t)pbase + pos;
+                                P.l4len = pln - pos;
+                            }
+                            return P;
+                        }
+                    } else {
+                        break;
+                    }
+                }
+                P.proto = nh;
+            }
+            if (pln > pos) {
+                has_l4 = true;
+                l4s = (uint32_t)pbase + pos;
+                l4n = pln - pos;
+            }
+        }
+    } else {
+        P.st |= PNET_ST_UNKNOWN_ETHERTYPE;
+    }
+    if (has_l4) {
+        P.l4off = l4s;
+        P.l4len = l4n;
+    }
+    if (l3ok) {
+        uint32_t kind = 0, minlen = 0;
+        int soff = 0;
+        switch (P.proto) {
+            case 17: kind = PNET_ST_L4_UDP; minlen = 8; soff = 6; break;
+            case 6: kind = PNET_ST_L4_TCP; minlen = 20; soff = 16; break;
+            case 1: kind = PNET_ST_L4_ICMP; minlen = 4; soff = 2; break;
+            case 58: kind = PNET_ST_L4_ICMPV6; minlen = 4; soff = 2; break;
+            default: break;
+        }
+        if (!kind) {
+            P.st |= PNET_ST_UNKNOWN_PROTO;
+        } else {
+            P.st |= kind;
+            if (l4n < minlen) {
+                P.st |= PNET_ST_L4_MALFORMED;
+            } else {
+                const int p = (int)l4s;
+                P.sp = F.far16(p);
+                if (P.proto == 17 || P.proto == 6) P.dp = F.far16(p + 2);
+                else P.dp = l4n >= 8 ? F.far16(p + 4) : 0u;
+                P.l4stored = F.far16(p + soff);
+                P.l4csum_at = p + soff;
+                if (P.proto == 1) {                            // icmp::checksum: no pseudo-header
+                    P.l4do = true;
+                } else if (v6) {                               // util::ipv6_checksum
+                    P.l4do = true;
+                    P.v6pseudo = true;
+                    P.a_lo = l3 + 8;                           // pseudo-header address bytes
+                    P.a_hi = l3 + 40;
+                    P.pseudo = P.proto + l4n;
+                } else if (P.proto != 58) {                    // util::ipv4_checksum
+                    P.l4do = true;
+                    P.pseudo = (P.s4 >> 16) + (P.s4 & 0xFFFFu) + (P.d4 >> 16) + (P.d4 & 0xFFFFu) +
+                               P.proto + l4n;
+                }
+                if (P.l4do) {
+                    P.b_lo = p;
+                    P.b_hi = p + (int)l4n;
+                }
+            }
+        }
+    }
+    // canonical empty ranges: a_lo <= a_hi <= b_lo <= b_hi
+    if (!P.l4do) { P.b_lo = P.b_hi = P.a_hi; }
+    if (P.l4do && !P.is_v4 && !P.v6pseudo) { P.a_lo = P.a_hi = P.b_lo; }   // ICMP over IPv6
+    return P;
+}
+
+// Window sums of one lane's LDS slot: tA over [p0,p1), tB over [p2,p3), slot
+// coordinates, p0 <= p1 <= p2 <= p3 <= window bytes (the slot has a readable
+// pad dword, so p3>>2 may equal the dword count). With P(x) = weighted sum of
+// the slot bytes in [4*(p0>>2), x): tA = P(p1) - P(p0), tB = P(p3) - P(p2).
+// One runtime loop over whole dwords (v_sad_u16 each) plus four masked partials.
+__device__ __forceinline__ void window_sums(const uint8_t* slot, int p0, int p1, int p2, int p3, uint32_t& tA,
+                                            uint32_t& tB) {
+    const uint32_t* s32 = reinterpret_cast<const uint32_t*>(slot);
+    const int k0 = p0 >> 2, k1 = p1 >> 2, k2 = p2 >> 2, k3 = p3 >> 2;
+    uint32_t acc = 0, c1 = 0, c2 = 0;
+#pragma unroll 1
+    for (int k = k0; k < k3; ++k) {
+        if (k == k1) c1 = acc;
+        if (k == k2) c2 = acc;
+        acc = sad(s32[k], acc);
+    }
+    if (k1 >= k3) c1 = acc;
+    if (k2 >= k3) c2 = acc;
+    const uint32_t P0 = sad(s32[k0] & first_bytes(p0 & 3), 0u);
+    const uint32_t P1 = sad(s32[k1] & first_bytes(p1 & 3), c1);
+    const uint32_t P2 = sad(s32[k2] & first_bytes(p2 & 3), c2);
+    const uint32_t P3 = sad(s32[k3] & first_bytes(p3 & 3), acc);
+    tA += P1 - P0;
+    tB += P3 - P2;
+}
+
+// Skip-word removal, fold, byte-order fix-up, pseudo-header, compare.
+// odd = frame offset parity. Returns ip and l4 checksums through P.
+__device__ __forceinline__ void finalize(Parsed& P, uint32_t tA, uint32_t tB, bool odd, uint32_t& ipc,
+                                         uint32_t& l4c) {
+    ipc = 0;
+    l4c = 0;
+    if (P.is_v4) tA -= odd ? P.ipstored : bswap16(P.ipstored);    // skipword 5 (ipv4.rs:177)
+    if (P.l4do) tB -= odd ? P.l4stored : bswap16(P.l4stored);     // skipword 3 / 8 / 1
+    uint32_t pA = fold16(tA), pB = fold16(tB);
+    if (!odd) { pA = bswap16(pA); pB = bswap16(pB); }
+    if (P.is_v4) {
+        ipc = (~pA) & 0xFFFFu;
+        if (ipc == P.ipstored) P.st |= PNET_ST_IP_CSUM_OK;
+    }
+    if (P.l4do) {
+        l4c = (~fold16(pB + P.pseudo + (P.v6pseudo ? pA : 0u))) & 0xFFFFu;
+        P.st |= PNET_ST_L4_CSUM_DONE;
+        if (l4c == P.l4stored) P.st |= PNET_ST_L4_CSUM_OK;
+    }
+}
+
+// TX: write the computed checksums into the frame's stored fields (big-endian),
+// i.e. MutableIpv4Packet::set_checksum(ipv4::checksum(..)) and the L4
+// set_checksum(udp|tcp::ipv4_checksum(..) / icmp::checksum(..)) of
+// benches/rs_sender.rs:38-39,70-71. Byte stores: the fields may sit at odd addresses.
+__device__ __forceinline__ void tx_write(uint8_t* frame, const Parsed& P, uint32_t ipc, uint32_t l4c) {
+    if (P.is_v4) {
+        frame[P.l3 + 10] = (uint8_t)(ipc >> 8);
+        frame[P.l3 + 11] = (uint8_t)ipc;
+    }
+    if (P.st & PNET_ST_L4_CSUM_DONE) {
+        frame[P.l4csum_at] = (uint8_t)(l4c >> 8);
+        frame[P.l4csum_at + 1] = (uint8_t)l4c;
+    }
+}
+
+// Per-wave counters (ballots: wave-uniform) and coalesced column stores.
+struct Counters {
+    uint32_t frames = 0, v4 = 0, v6 = 0, ipbad = 0, l4bad = 0, malf = 0, unk = 0;
+    uint64_t bytes = 0;
+    __device__ __forceinline__ void add(bool valid, uint32_t len, uint32_t st) {
+        frames += (uint32_t)__popcll(__ballot(valid));
+        bytes += len;
+        v4 += (uint32_t)__popcll(__ballot((st & PNET_ST_L3_MASK) == PNET_ST_L3_IPV4));
+        v6 += (uint32_t)__popcll(__ballot((st & PNET_ST_L3_MASK) == PNET_ST_L3_IPV6));
+        ipbad += (uint32_t)__popcll(__ballot((st & (PNET_ST_L3_MASK | PNET_ST_L3_MALFORMED | PNET_ST_IP_CSUM_OK)) ==
+                                             PNET_ST_L3_IPV4));
+        l4bad += (uint32_t)__popcll(__ballot((st & (PNET_ST_L4_CSUM_DONE | PNET_ST_L4_CSUM_OK)) ==
+                                             PNET_ST_L4_CSUM_DONE));
+        malf += (uint32_t)__popcll(__ballot((st & (PNET_ST_ETH_MALFORMED | PNET_ST_L3_MALFORMED |
+                                                   PNET_ST_L4_MALFORMED | PNET_ST_DESC_INVALID)) != 0));
+        unk += (uint32_t)__popcll(__ballot((st & (PNET_ST_UNKNOWN_ETHERTYPE | PNET_ST_UNKNOWN_PROTO)) != 0));
+    }
+    // one atomic set per wave (one-wave blocks)
+    __device__ __forceinline__ void flush_wave(uint64_t* out, int lane) {
+        for (int o = 32; o >= 1; o >>= 1) {
+            uint32_t lo = (uint32_t)bytes, hi = (uint32_t)(bytes >> 32);
+            lo = __shfl_xor(lo, o);
+            hi = __shfl_xor(hi, o);
+            bytes += ((uint64_t)hi << 32) | lo;
+        }
+        const uint64_t v[PNETGPU_NCOUNTERS] = {frames, bytes, v4, v6, ipbad, l4bad, malf, unk};
+        if (lane < PNETGPU_NCOUNTERS) {
+            uint64_t x = 0;
+#pragma unroll
+            for (int c = 0; c < PNETGPU_NCOUNTERS; ++c) x = lane == c ? v[c] : x;
+            if (x) atomicAdd(reinterpret_cast<unsigned long long*>(out + lane), (unsigned long long)x);
+        }
+    }
+    // one atomic set per block (all waves must call)
+    __device__ __forceinline__ void flush(uint64_t* out, uint64_t (*blk)[PNETGPU_NCOUNTERS], int wv, int lane) {
+        for (int o = 32; o >= 1; o >>= 1) {
+            uint32_t lo = (uint32_t)bytes, hi = (uint32_t)(bytes >> 32);
+            lo = __shfl_xor(lo, o);
+            hi = __shfl_xor(hi, o);
+            bytes += ((uint64_t)hi << 32) | lo;
+        }
+        if (lane == 0) {
+            blk[wv][PNETGPU_CTR_FRAMES] = frames;
+            blk[wv][PNETGPU_CTR_BYTES] = bytes;
+            blk[wv][PNETGPU_CTR_IPV4] = v4;
+            blk[wv][PNETGPU_CTR_IPV6] = v6;
+            blk[wv][PNETGPU_CTR_IP_CSUM_BAD] = ipbad;
+            blk[wv][PNETGPU_CTR_L4_CSUM_BAD] = l4bad;
+            blk[wv][PNETGPU_CTR_MALFORMED] = malf;
+            blk[wv][PNETGPU_CTR_UNKNOWN] = unk;
+        }
+        __syncthreads();
+        if (threadIdx.x < PNETGPU_NCOUNTERS) {
+            uint64_t v = 0;
+            for (int w = 0; w < kWavesPerBlock; ++w) v += blk[w][threadIdx.x];
+            if (v) atomicAdd(reinterpret_cast<unsigned long long*>(out + threadIdx.x), (unsigned long long)v);
+        }
+    }
+};
+
+// Column element store (streaming: written once, never re-read by the kernel)
+template <class T>
+__device__ __forceinline__ void put(T* col, uint64_t i, T v) {
+#ifdef PNET_PLAIN_STORES
+    col[i] = v;
+#else
+    __builtin_nontemporal_store(v, col + i);
+#endif
+}
+
+// Column stores for the frames of one run: the base is wave-uniform (SGPR) and
+// the lane adds its index, so each store is one coalesced wave instruction.
+__device__ __forceinline__ void store_columns(const pnetgpu_rx_columns& C, uint64_t f0, int lane, bool in_batch,
+                                              const Parsed& P, uint32_t ipc, uint32_t l4c, const uint8_t* slot,
+                                              int sh) {
+    if (!in_batch) return;
+    if (C.status) put<uint16_t>(C.status, f0 + lane, (uint16_t)P.st);
+    if (C.ip_csum) put<uint16_t>(C.ip_csum, f0 + lane, (uint16_t)ipc);
+    if (C.l4_csum) put<uint16_t>(C.l4_csum, f0 + lane, (uint16_t)l4c);
+    if (C.ethertype) put<uint16_t>(C.ethertype, f0 + lane, (uint16_t)P.et);
+    if (C.ip_proto) put<uint8_t>(C.ip_proto, f0 + lane, (uint8_t)P.proto);
+    if (C.ttl) put<uint8_t>(C.ttl, f0 + lane, (uint8_t)P.ttl);
+    if (C.l4_offset) put<uint16_t>(C.l4_offset, f0 + lane, (uint16_t)P.l4off);
+    if (C.l4_length) put<uint16_t>(C.l4_length, f0 + lane, (uint16_t)P.l4len);
+    if (C.src_port) put<uint16_t>(C.src_port, f0 + lane, (uint16_t)P.sp);
+    if (C.dst_port) put<uint16_t>(C.dst_port, f0 + lane, (uint16_t)P.dp);
+    if (C.src_ipv4) put<uint32_t>(C.src_ipv4, f0 + lane, P.s4);
+    if (C.dst_ipv4) put<uint32_t>(C.dst_ipv4, f0 + lane, P.d4);
+    if (C.vlan_tci) put<uint16_t>(C.vlan_tci, f0 + lane, (uint16_t)P.vlan_tci);
+    if (C.l3_offset) put<uint8_t>(C.l3_offset, f0 + lane, (uint8_t)P.l3);
+    if (C.src_ipv6 || C.dst_ipv6) {
+        const bool v6ok = (P.st & (PNET_ST_L3_MASK | PNET_ST_L3_MALFORMED)) == PNET_ST_L3_IPV6;
+        uint4 sv = make_uint4(0, 0, 0, 0), dv = make_uint4(0, 0, 0, 0);
+        if (v6ok) {
+            sv = lds_read16_unaligned(slot, sh + (int)P.l3 + 8);
+            dv = lds_read16_unaligned(slot, sh + (int)P.l3 + 24);
+        }
+        if (C.src_ipv6) reinterpret_cast<uint4*>(C.src_ipv6)[f0 + lane] = sv;
+        if (C.dst_ipv6) reinterpret_cast<uint4*>(C.dst_ipv6)[f0 + lane] = dv;
+    }
+}
+
+}  // namespace
+}  // namespace pnetgpu

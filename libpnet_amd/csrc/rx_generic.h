@@ -1,0 +1,272 @@
+// rx_generic.h — rx_kernel, the generic receive kernel (descriptor mode, any alignment, any length; mixed / MTU / jumbo shapes)
+// Part of the receive-path kernels; included once, by rx_kernel.hip (one
+// translation unit, so every kernel still sees the shared device helpers inline).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "pnetgpu.h"
+#include "rx_internal.h"
+#include "rx_common.h"
+
+namespace pnetgpu {
+namespace {
+
+// ============================================================================
+// rx_kernel: generic (descriptor mode, any alignment, any length).
+// ============================================================================
+template <int NW>
+struct WaveLds {
+    static constexpr int kSlot = NW * 16 + 4;   // +4 B pad: conflict-free parse reads
+    uint8_t win[kWave * kSlot];
+    uint64_t base[kWave];     // aligned byte offset of granule 0 of each frame
+    uint32_t end[kWave];      // window granules to load; then slot-relative frame end
+    uint32_t tail[kWave];     // weighted sum of the frame's bytes past the window
+    uint8_t list[kWave];      // frames with bytes past the window (longest class first)
+    uint32_t qhead;           // next list entry for a group that runs out of work
+};
+
+// Weighted sum of slot bytes [lo, hi) of a frame whose granule 0 is at fb, read
+// from memory by one lane (the rare correction when the L4 range does not run
+// from the window to the end of the frame).
+__device__ __forceinline__ uint32_t lane_range_sum(const uint8_t* fb, int lo, int hi) {
+    uint32_t acc = 0;
+#pragma unroll 1
+    for (int c = lo >> 4; 16 * c < hi; ++c) {
+        const uint4 v = load16(fb + 16 * c);
+        const uint32_t dw[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int p = 16 * c + 4 * t;
+            acc = sad(dw[t] & first_bytes(clamp04(hi - p)) & ~first_bytes(clamp04(lo - p)), acc);
+        }
+    }
+    return acc;
+}
+
+// The speculative tail: every byte of every frame past its window,
+// [kWin, end), summed before the parse by groups of G lanes that stream
+// coalesced granules (U loads in flight per lane); a group takes the next frame
+// of the wave's list as soon as it finishes one. Sums land in L.tail.
+// UNI (unified): the group streams the whole frame from granule 0 and writes
+// granules 0..NW-1 into the frame's LDS slot itself (zeros past the frame's
+// span) instead of a separate window phase: one pass per frame, so the line
+// holding the window/tail boundary and the line shared with the next frame are
+// fetched once, while they are still in L2 (the windows-first order read ~15 %
+// more than the frame bytes on MTU frames: TCC_EA0_RDREQ, profiles/).
+// DYN: a group that finishes a frame takes the next list entry from a shared
+// LDS counter instead of a fixed stride of the list, and the list holds the
+// frames needing more than one round first, so mixed sizes balance across the
+// groups (the caller sets L.qhead = kWave / G).
+template <int NW, int G, int U, bool NT, bool UNI, bool DYN>
+__device__ __forceinline__ void tail_sums(const uint8_t* data, WaveLds<NW>& L, int lane, int count) {
+    constexpr int kGroups = kWave / G;
+    constexpr int kSlot = WaveLds<NW>::kSlot;
+    constexpr uint32_t c_first = UNI ? 0u : (uint32_t)NW;
+    static_assert(!UNI || G * U >= NW, "the first round must cover the window");
+    const int j = lane % G;
+    int idx = lane / G;
+    int fl = 0;
+    uint32_t fe = 0, nneed = 0, c0 = 0, acc = 0;
+    const uint8_t* fb = data;
+    if (idx < count) {
+        fl = L.list[idx];
+        fe = L.end[fl];
+        fb = data + L.base[fl];
+        nneed = (fe + 15u) >> 4;
+        c0 = c_first + j;
+    }
+    while (__ballot(idx < count)) {
+        if (idx < count) {
+            uint4 v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t c = c0 + u * G;
+                v[u] = c < nneed ? (NT ? load16_nt(fb + 16u * c) : load16(fb + 16u * c)) : make_uint4(0, 0, 0, 0);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t c = c0 + u * G;
+                uint32_t x = v[u].x, y = v[u].y, z = v[u].z, w = v[u].w;
+                if (UNI && c < (uint32_t)NW) {                   // window granule -> the frame's slot
+                    uint32_t* dst = reinterpret_cast<uint32_t*>(L.win + fl * kSlot + 16 * c);
+                    dst[0] = x; dst[1] = y; dst[2] = z; dst[3] = w;
+                    continue;
+                }
+                const int hi = (int)fe - (int)(16u * c);
+                if (hi < 16) {                                   // the frame's last granule
+                    x &= first_bytes(clamp04(hi));
+                    y &= first_bytes(clamp04(hi - 4));
+                    z &= first_bytes(clamp04(hi - 8));
+                    w &= first_bytes(clamp04(hi - 12));
+                }
+                acc = sad(x, acc);
+                acc = sad(y, acc);
+                acc = sad(z, acc);
+                acc = sad(w, acc);
+            }
+            c0 += U * G;
+            if (c0 - j >= (nneed > c_first ? nneed : c_first + 1u)) {   // group-uniform: frame done
+#pragma unroll
+                for (int o = G / 2; o >= 1; o >>= 1) acc += __shfl_xor(acc, o);
+                if (j == 0) L.tail[fl] = acc;
+                acc = 0;
+                if (DYN) {
+                    uint32_t nidx = 0;
+                    if (j == 0) nidx = atomicAdd(&L.qhead, 1u);
+                    idx = __shfl((int)nidx, lane - j);
+                } else {
+                    idx += kGroups;
+                }
+                if (idx < count) {
+                    fl = L.list[idx];
+                    fe = L.end[fl];
+                    fb = data + L.base[fl];
+                    nneed = (fe + 15u) >> 4;
+                    c0 = c_first + j;
+                }
+            }
+        }
+    }
+}
+
+// PASS: 0 = window phase for every frame, then the tails of the long ones;
+// 1 = unified: every frame streamed once by the group loop (a hybrid - windows
+// of short frames first, long frames unified - measured 5-15 % slower on IMIX).
+// EXT: batch flags may be non-zero (VLAN / IPv6 extension dispatch); the
+// flags-0 instantiation compiles the parse without those branches (half the
+// code, SGPR spills 118 -> 14, IMIX -2 %).
+template <int NW, int G, int U, bool NT, int PASS, bool DYN, bool EXT, bool TX>
+__global__ __launch_bounds__(kBlock, 4) void rx_kernel(RxArgs a) {
+    static_assert(NW == 8, "window granules");
+    static_assert(G == 4 || G == 8 || G == 16 || G == 32 || G == 64, "tail group");
+    constexpr int kSlot = WaveLds<NW>::kSlot;
+    constexpr int kWin = NW * 16;
+
+    __shared__ WaveLds<NW> lds_all[kWavesPerBlock];
+    __shared__ uint64_t blk_ctr[kWavesPerBlock][PNETGPU_NCOUNTERS];
+
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wv = threadIdx.x / kWave;
+    WaveLds<NW>& L = lds_all[wv];
+    uint8_t* slot = L.win + lane * kSlot;
+    Counters K;
+
+    const uint64_t wave_stride = (uint64_t)gridDim.x * kWavesPerBlock;
+    // descriptor-mode offset/length of this lane's frame, loaded one run ahead
+    // so the descriptor round trip overlaps the previous run
+    uint64_t d_off = 0;
+    uint32_t d_len = 0;
+    auto fetch_desc = [&](uint64_t r) {
+        const uint64_t fr = r * kWave + lane;
+        if (!a.stride && r < a.nruns && fr < a.n) {
+            d_off = a.offsets[fr];
+            d_len = a.lengths[fr];
+        }
+    };
+    fetch_desc((uint64_t)blockIdx.x * kWavesPerBlock + wv);
+    for (uint64_t run = (uint64_t)blockIdx.x * kWavesPerBlock + wv; run < a.nruns; run += wave_stride) {
+        // ---- 1. descriptor -------------------------------------------------
+        const uint64_t f0 = run * kWave;
+        const uint64_t f = f0 + lane;
+        const bool in_batch = f < a.n;
+        uint64_t off = 0;
+        uint32_t len = 0;
+        if (in_batch) {
+            if (a.stride) {
+                off = a.first + f * a.stride;
+                len = a.frame_len;
+            } else {
+                off = d_off;
+                len = d_len;
+            }
+            off += a.delta;
+        }
+        const bool desc_bad = in_batch && (off > a.limit || (uint64_t)len > a.limit - off);
+        if (!in_batch || desc_bad) len = 0;
+        const int sh = (int)(off & 15);
+        const uint64_t base = off - (uint64_t)sh;
+        const uint32_t fend = (uint32_t)sh + len;            // slot-relative end of the frame
+        const uint32_t span = (fend + 15u) >> 4;
+        const bool long_frame = fend > (uint32_t)kWin;
+        L.base[lane] = base;
+        L.end[lane] = span < (uint32_t)NW ? span : (uint32_t)NW;   // granules to load into the window
+        wave_sync();
+
+        // ---- 2. window: NW*64 granule loads, all in flight before any store --
+        if (PASS != 1) {
+            uint4 g[NW];
+#pragma unroll
+            for (int i = 0; i < NW; ++i) {
+                const int q = i * kWave + lane;
+                const int fl = q / NW, c = q % NW;
+                g[i] = make_uint4(0, 0, 0, 0);
+                if ((uint32_t)c < L.end[fl])
+                    g[i] = load16(a.data + L.base[fl] + 16u * c);
+            }
+            fetch_desc(run + wave_stride);
+#pragma unroll
+            for (int i = 0; i < NW; ++i) {
+                const int q = i * kWave + lane;
+                const int fl = q / NW, c = q % NW;
+                uint32_t* dst = reinterpret_cast<uint32_t*>(L.win + fl * kSlot + 16 * c);
+                dst[0] = g[i].x; dst[1] = g[i].y; dst[2] = g[i].z; dst[3] = g[i].w;
+            }
+        } else {
+            fetch_desc(run + wave_stride);
+        }
+
+        // ---- 3. speculative tail: all frame bytes past the window ----------
+        // Summed before the parse (no parse state is live, so more loads fit in
+        // flight); the parse then trims it to the L4 range B, which in every
+        // well-formed frame already runs to the end of the frame. Unified pass:
+        // the group loop also fills the window of every frame.
+        const bool has_tail = PASS == 1 ? in_batch : long_frame;
+        const uint64_t tmask = __ballot(has_tail);
+        if (tmask) {
+            // DYN: frames needing more than one group round go first
+            const bool big = DYN && has_tail && span > (uint32_t)(NW + G * U);
+            const uint64_t bmask = __ballot(big);
+            const uint64_t below = (1ull << lane) - 1ull;
+            if (has_tail) {
+                const int pos = big ? __popcll(bmask & below) : __popcll(bmask) + __popcll(tmask & ~bmask & below);
+                L.list[pos] = (uint8_t)lane;
+                L.end[lane] = fend;
+            }
+            if (DYN && lane == 0) L.qhead = kWave / G;
+            wave_sync();
+            tail_sums<NW, G, U, NT, (PASS != 0), DYN>(a.data, L, lane, __popcll(tmask));
+        }
+        wave_sync();
+
+        // ---- 4. parse + window sums (lane l <-> frame l) -------------------
+        Parsed P{};
+        if (desc_bad) P.st = PNET_ST_DESC_INVALID;
+        else if (in_batch)
+            P = parse_frame(FrameBytes{slot + sh, a.data + off, kWin - sh}, len, EXT ? a.flags : 0u);
+        // A (<= 97 B into the frame) always lies in the window; B may run past it
+        const int p0 = P.a_lo + sh, p1 = P.a_hi + sh, p2 = P.b_lo + sh, p3 = P.b_hi + sh;
+        uint32_t tA = 0, tB = 0;
+        window_sums(slot, p0, p1, min(p2, kWin), min(p3, kWin), tA, tB);
+        if (P.l4do && p3 > kWin) {
+            // B past the window = the speculative tail minus [kWin, p2) and [p3, fend)
+            tB += L.tail[lane];
+            const uint8_t* fb = a.data + base;
+            if (p2 > kWin) tB -= lane_range_sum(fb, kWin, p2);
+            if ((uint32_t)p3 < fend) tB -= lane_range_sum(fb, p3, (int)fend);
+        }
+
+        // ---- 5. finalize + stores ------------------------------------------
+        uint32_t ipc = 0, l4c = 0;
+        finalize(P, tA, tB, (off & 1) != 0, ipc, l4c);
+        if (TX && in_batch && !desc_bad) tx_write(const_cast<uint8_t*>(a.data) + off, P, ipc, l4c);
+        store_columns(a.cols, f0, lane, in_batch, P, ipc, l4c, slot, sh);
+        if (a.cols.counters) K.add(in_batch && !desc_bad, len, P.st);
+        wave_sync();   // slots and lists are rewritten by the next run
+    }
+    if (a.cols.counters) K.flush(a.cols.counters, blk_ctr, wv, lane);
+}
+
+}  // namespace
+}  // namespace pnetgpu

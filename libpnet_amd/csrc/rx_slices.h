@@ -1,0 +1,124 @@
+// rx_slices.h — slice_kernel, the batched util::checksum / ipv4_checksum / ipv6_checksum (and *_adv) entry points
+// Part of the receive-path kernels; included once, by rx_kernel.hip (one
+// translation unit, so every kernel still sees the shared device helpers inline).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "pnetgpu.h"
+#include "rx_internal.h"
+#include "rx_common.h"
+
+namespace pnetgpu {
+namespace {
+
+// ---------------------------------------------------------------------------
+// Batched util::checksum / ipv4_checksum / ipv6_checksum over slices.
+// One group of 16 lanes per slice (4 slices per wave per step): coalesced
+// 16-B granules, masked sums, shuffle reduce, lane 0 of the group finalizes.
+
+#ifndef PNET_SLICE_U
+#define PNET_SLICE_U 4   // loads in flight per lane in the slice kernels
+#endif
+// Weighted byte sum of [off, off+len) (absolute offsets into a.data) by one
+// 16-lane group: coalesced aligned granules, U loads in flight per lane (the
+// 16 lanes cover 256 B per load round), byte masks only on the slice's first
+// and last granule, shuffle-reduced so every lane of the group returns the total.
+__device__ __forceinline__ uint32_t group_range_sum(const uint8_t* data, uint64_t off, uint32_t len, int j) {
+    constexpr int G = 16, U = PNET_SLICE_U;
+    const int sh = (int)(off & 15);
+    const uint8_t* fb = data + (off - (uint64_t)sh);
+    const int e = sh + (int)len;
+    const uint32_t nneed = len ? (uint32_t)((e + 15) >> 4) : 0u;
+    uint32_t acc = 0;
+#pragma unroll 1
+    for (uint32_t c0 = j; c0 < nneed; c0 += G * U) {
+        uint4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t c = c0 + u * G;
+            v[u] = c < nneed ? *reinterpret_cast<const uint4*>(fb + 16u * c) : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t c = c0 + u * G;
+            const uint32_t dw[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+            if (c == 0 || c + 1 == nneed) {          // edge granule (zero when c >= nneed)
+                const int p = (int)(16u * c);
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    const uint32_t mk = first_bytes(clamp04(e - p - 4 * t)) & ~first_bytes(clamp04(sh - p - 4 * t));
+                    acc = sad(dw[t] & mk, acc);
+                }
+            } else {
+                acc = sad(dw[3], sad(dw[2], sad(dw[1], sad(dw[0], acc))));
+            }
+        }
+    }
+#pragma unroll
+    for (int o = G / 2; o >= 1; o >>= 1) acc += __shfl_xor(acc, o);
+    return acc;
+}
+
+// PSEUDO: 0 = util::checksum, 4 = util::ipv4_checksum, 16 = util::ipv6_checksum.
+// EXTRA: the *_checksum_adv form with an extra_data slice (util.rs:109-114).
+template <int PSEUDO, bool EXTRA>
+__global__ __launch_bounds__(kBlock) void slice_kernel(SliceArgs a) {
+    constexpr int G = 16;
+    const int lane = threadIdx.x & (kWave - 1);
+    const int j = lane % G;
+    const uint64_t gid = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) / G;
+    const uint64_t ngroups = (uint64_t)gridDim.x * kBlock / G;
+    // groups are 16-lane aligned, so every shuffle stays inside one group, whose
+    // lanes share i (and therefore control flow)
+    for (uint64_t i = gid; i < a.n; i += ngroups) {
+        const uint64_t off = a.offsets[i] + a.delta;
+        uint32_t len = a.lengths[i];
+        const uint32_t skip = a.skipwords[i];
+        if (off > a.limit || (uint64_t)len > a.limit - off) len = 0;
+        uint32_t acc = group_range_sum(a.data, off, len, j);
+        uint32_t pe = 0, elen = 0;
+        if (EXTRA) {
+            // sum_be_words(extra, extra.len() / 2): every whole word, never the odd
+            // trailing byte (util.rs:114; the quirk documented at udp.rs:42-44); the
+            // extra slice starts its own word alignment
+            const uint64_t eoff = a.extra_offsets[i] + a.delta;
+            elen = a.extra_lengths[i];
+            if (eoff > a.limit || (uint64_t)elen > a.limit - eoff) elen = 0;
+            const uint32_t te = group_range_sum(a.data, eoff, elen & ~1u, j);
+            pe = fold16(te);
+            if (!(eoff & 1)) pe = bswap16(pe);
+        }
+        if (j == 0) {
+            // skipped word: bytes [2*skip, 2*skip+2) of the slice that exist (util.rs:166-178)
+            const uint8_t* sb = a.data + off;
+            if ((uint64_t)skip * 2 < len) {
+                const uint64_t q = 2ull * skip;
+                const uint32_t b0 = sb[q];
+                acc -= ((off + q) & 1) ? (b0 << 8) : b0;
+                if (q + 1 < len) {
+                    const uint32_t b1 = sb[q + 1];
+                    acc -= ((off + q + 1) & 1) ? (b1 << 8) : b1;
+                }
+            }
+            uint32_t p = fold16(acc);
+            if (!(off & 1)) p = bswap16(p);
+            uint32_t r;
+            if (PSEUDO == 0) {
+                r = len ? ((~p) & 0xFFFFu) : 0u;            // util.rs:77-79
+            } else {
+                const uint8_t* ad = a.addrs + i * (2 * PSEUDO);
+                uint32_t s = 0;
+#pragma unroll
+                for (int k = 0; k < 2 * PSEUDO; k += 2) s += ((uint32_t)ad[k] << 8) | ad[k + 1];
+                s += a.protos[i] + len + elen + p + pe;     // util.rs:103-114
+                r = (~fold16(s)) & 0xFFFFu;
+            }
+            a.out[i] = (uint16_t)r;
+        }
+    }
+}
+
+}  // namespace
+}  // namespace pnetgpu
