@@ -1,0 +1,78 @@
+"""Multi-process sharding with the HIP kernel (SURVEY.md §4 implication 4, §8(e)):
+two ranks, one process each, on this box's GPU (a 1-GPU box stands in for two
+devices; the bench's N-GPU runs use RCCL). Each rank uploads and processes its
+byte-balanced slice of an IMIX batch through the C-ABI, the counter vectors are
+all-reduced, and the concatenated per-rank records equal the oracle's over the
+whole batch."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+WORLD = 2
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, port, n, q):
+    import libpnet_amd as lp
+    from libpnet_amd import shard
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    try:
+        torch.cuda.set_device(0)
+        w = lp.synth.make("imix", n, seed=91, corrupt_ppm=20000)
+        lo, hi = shard.shard_by_bytes(w.lengths, WORLD, rank)
+        b0 = int(w.offsets[lo])
+        b1 = int(w.offsets[hi - 1]) + int(w.lengths[hi - 1])
+        data = torch.from_numpy(np.concatenate([w.buf[b0:b1], np.zeros(32, np.uint8)])).to("cuda:0")
+        offs = torch.from_numpy((w.offsets[lo:hi] - b0).view(np.int64)).to("cuda:0")
+        lens = torch.from_numpy(w.lengths[lo:hi].view(np.int32)).to("cuda:0")
+        res = lp.rx_process(data, offsets=offs, lengths=lens, columns=lp.ALL_COLUMNS)
+        torch.cuda.synchronize()
+        ctr = res.counters.cpu()
+        shard.all_reduce_counters(ctr)
+        recs = {c: v for c, v in res.numpy().items()}
+        gathered = [None] * WORLD
+        dist.all_gather_object(gathered, (lo, hi, recs))
+        if rank == 0:
+            q.put((ctr.numpy().view(np.uint64).tolist(), gathered))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_ranks_gpu_shards_match_whole_batch_oracle():
+    import libpnet_amd as lp
+    from oracle import coracle
+    n = 60000
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, port, n, q)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    ctr, gathered = q.get(timeout=100)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    w = lp.synth.make("imix", n, seed=91, corrupt_ppm=20000)
+    full = coracle.rx_batch(w.buf, n, offsets=w.offsets, lengths=w.lengths)
+    spans = sorted((lo, hi) for lo, hi, _ in gathered)
+    assert spans[0][0] == 0 and spans[-1][1] == n and spans[0][1] == spans[1][0]
+    for lo, hi, recs in gathered:
+        for c, v in recs.items():
+            assert np.array_equal(v, full[c][lo:hi]), (lo, c)
+    assert ctr[0] == n and ctr[1] == int(w.lengths.astype(np.int64).sum())
+    assert ctr[4] == w.expect["ip_bad"] and ctr[5] == w.expect["l4_bad"]

@@ -2,7 +2,7 @@
 shard boundaries partition the batch, per-rank results concatenate to the
 single-process results, and the counter all-reduce equals the whole-batch
 counters. The per-rank compute here is the CPU oracle (no GPU on this host);
-the GPU box runs the same sharding with the HIP kernel (tests/test_gpu_parity.py)."""
+the GPU box runs the same sharding with the HIP kernel (tests/test_gpu_multi.py)."""
 import os
 import socket
 
