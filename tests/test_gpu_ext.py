@@ -155,3 +155,19 @@ def test_fuzz_random_bytes_bit_exact(flags):
                         columns=ALL_COLUMNS, flags=flags)
     torch.cuda.synchronize()
     compare(res, rec)
+
+
+@pytest.mark.parametrize("flags", [0, 7])
+def test_fuzz_tx_fill_bit_exact(flags):
+    """TX fill over steered random bytes: the patched buffer (every checksum field
+    the dispatch reaches, nothing else) equals the oracle's byte for byte."""
+    rng = np.random.default_rng(2000 + flags)
+    buf, offs, lens = _fuzz_batch(rng, 100_000)
+    d = to_dev(buf.copy())
+    res = lp.tx_fill_checksums(d, offsets=to_dev(offs.astype(np.int64)), lengths=to_dev(lens.astype(np.int32)),
+                               columns=ALL_COLUMNS, flags=flags)
+    want_buf, want_rec = coracle.tx_fill(buf, len(offs), offsets=offs, lengths=lens, flags=flags)
+    torch.cuda.synchronize()
+    got = d.cpu().numpy()
+    assert np.array_equal(got, want_buf), int((got != want_buf).sum())
+    compare(res, want_rec)
