@@ -171,3 +171,31 @@ def test_fuzz_tx_fill_bit_exact(flags):
     got = d.cpu().numpy()
     assert np.array_equal(got, want_buf), int((got != want_buf).sum())
     compare(res, want_rec)
+
+
+@pytest.mark.parametrize("frame_len", [14, 20, 34, 42, 47, 60, 64])
+def test_fuzz_small_kernel_bit_exact(frame_len):
+    """rx_small_kernel (fixed 64-B stride) over steered random bytes: its register
+    fast path and its fallback to the generic parse, bit-exact, TX fill too."""
+    rng = np.random.default_rng(3000 + frame_len)
+    n = 1 << 17
+    buf = rng.integers(0, 256, n * 64 + 64, dtype=np.uint8)
+    f = buf[: n * 64].reshape(n, 64)
+    r = rng.random(n)
+    f[r < 0.7, 12], f[r < 0.7, 13] = 0x08, 0x00
+    f[(r >= 0.7) & (r < 0.85), 12], f[(r >= 0.7) & (r < 0.85), 13] = 0x86, 0xDD
+    f[r < 0.7, 14] = 0x40 | rng.integers(0, 16, int((r < 0.7).sum())).astype(np.uint8)
+    f[r < 0.5, 14] = 0x45                                          # mostly the fast path
+    f[:, 23] = np.array([6, 17, 1, 58, 47], np.uint8)[rng.integers(0, 5, n)]
+    short_tl = rng.random(n) < 0.3
+    f[short_tl, 16] = 0
+    f[short_tl, 17] = rng.integers(0, 64, int(short_tl.sum())).astype(np.uint8)
+    rec = coracle.rx_batch(buf, n, stride=64, frame_len=frame_len, nthreads=16)
+    res = lp.rx_process(to_dev(buf), stride=64, frame_len=frame_len, n_frames=n, columns=ALL_COLUMNS)
+    torch.cuda.synchronize()
+    compare(res, rec)
+    d = to_dev(buf.copy())
+    lp.tx_fill_checksums(d, stride=64, frame_len=frame_len, n_frames=n)
+    want, _ = coracle.tx_fill(buf, n, stride=64, frame_len=frame_len)
+    torch.cuda.synchronize()
+    assert np.array_equal(d.cpu().numpy(), want)
