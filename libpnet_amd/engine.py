@@ -143,9 +143,14 @@ class RxResult:
         return cols
 
     def numpy(self):
+        """Every column as an unsigned numpy array (one D2H copy of the block)."""
+        h = self.block[:self.nbytes].cpu().numpy() if self.block.is_cuda else self.block[:self.nbytes].numpy()
+        base = self.block.data_ptr()
         out = {}
         for c, t in self.columns.items():
-            out[c] = t.cpu().numpy().view(COLUMNS[c][1])
+            o = t.data_ptr() - base
+            nb = t.numel() * t.element_size()
+            out[c] = h[o:o + nb].view(COLUMNS[c][1]).reshape(tuple(t.shape))
         return out
 
     def counter_dict(self):
