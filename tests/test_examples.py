@@ -10,12 +10,14 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 EXE = os.path.join(ROOT, "libpnet_amd", "build", "rx_verify")
+SENDER = os.path.join(ROOT, "libpnet_amd", "build", "rs_sender")
 
 
 def test_example_built_and_linked():
-    assert os.access(EXE, os.X_OK), "run `make -C libpnet_amd` (build())"
-    out = subprocess.run(["ldd", EXE], capture_output=True, text=True, check=True).stdout
-    assert "libpnetgpu.so" in out and "not found" not in out
+    for exe in (EXE, SENDER):
+        assert os.access(exe, os.X_OK), "run `make -C libpnet_amd` (build())"
+        out = subprocess.run(["ldd", exe], capture_output=True, text=True, check=True).stdout
+        assert "libpnetgpu.so" in out and "not found" not in out
 
 
 @pytest.mark.gpu
@@ -24,3 +26,28 @@ def test_example_runs(n):
     r = subprocess.run([EXE, str(n)], capture_output=True, text=True, timeout=100)
     assert r.returncode == 0, r.stdout + r.stderr
     assert r.stdout.strip().endswith("OK")
+
+
+@pytest.mark.gpu
+def test_rs_sender_fills_what_the_oracle_computes(tmp_path):
+    """examples/rs_sender.c: rs_sender.rs's frame batch with zero checksum fields,
+    filled on the GPU and written to a pcap; every written frame equals the
+    oracle's fill of the same frame, and frame 0 carries 0xB8CA / 0xB94C."""
+    import numpy as np
+    import libpnet_amd as lp
+    from oracle import coracle
+    p = tmp_path / "tx.pcap"
+    n = 50000
+    r = subprocess.run([SENDER, str(n), str(p)], capture_output=True, text=True, timeout=100)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "0xB8CA" in r.stdout and "0xB94C" in r.stdout
+    frames = list(lp.pcap_frames(p))
+    assert len(frames) == n and all(len(f) == 64 for f in frames)
+    buf = np.frombuffer(b"".join(frames), np.uint8).copy()
+    zeroed = buf.copy().reshape(n, 64)
+    zeroed[:, 24:26] = 0
+    zeroed[:, 40:42] = 0
+    want, _ = coracle.tx_fill(np.concatenate([zeroed.reshape(-1), np.zeros(64, np.uint8)]), n, stride=64,
+                              frame_len=64)
+    assert np.array_equal(buf, want[: n * 64])
+
