@@ -392,6 +392,10 @@ def main():
         cfg = WORKLOADS[name]
         t = time.perf_counter()
         sh = Shard(name, cfg["n"], args.seed * 1000 + rank, device)
+        if dist_on:
+            # the host copy only serves the N=1 extras (CPU baseline, PCIe lines);
+            # with 8 ranks on a node it would hold ~50 GB of host memory for nothing
+            sh.w.buf = None
         if rank == 0:
             log(f"[bench] {name}: built {sh.n} frames ({sh.frame_bytes / 2**30:.2f} GiB) in {time.perf_counter() - t:.1f}s")
         ok, ctr = check_counters(sh)
