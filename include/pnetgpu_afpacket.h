@@ -12,7 +12,9 @@
  * the same Ethernet frames (captured bytes, tp_snaplen).
  *
  * Opening a packet socket needs CAP_NET_RAW; pnetgpu_afp_open returns
- * PNETGPU_ESYS with errno preserved when it is denied.
+ * PNETGPU_ESYS with errno preserved when it is denied. Single-threaded use per
+ * pnetgpu_afp (one consumer walks and releases the blocks in ring order);
+ * distinct rings (e.g. one per PACKET_FANOUT member) are independent.
  */
 #ifndef PNETGPU_AFPACKET_H
 #define PNETGPU_AFPACKET_H
