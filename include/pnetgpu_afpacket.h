@@ -55,6 +55,21 @@ int  pnetgpu_afp_next_block(pnetgpu_afp* afp, int timeout_ms, uint64_t* offsets,
 /* Give a block back to the kernel once the batch holding its frames has been
  * waited (the ring slot no longer reads it). Blocks are released in order. */
 int  pnetgpu_afp_release_block(pnetgpu_afp* afp, uint32_t block);
+/* Join PACKET_FANOUT group `group_id` (the reference's Config::linux_fanout,
+ * pnet_datalink/src/linux.rs:156-200 and lib.rs:110-128): rings opened on the
+ * same interface with the same group share its traffic — one ring per GPU
+ * rank. type: PNETGPU_FANOUT_*; flags: PNETGPU_FANOUT_FLAG_* (defrag, rollover). */
+#define PNETGPU_FANOUT_HASH      0u
+#define PNETGPU_FANOUT_LB        1u
+#define PNETGPU_FANOUT_CPU       2u
+#define PNETGPU_FANOUT_ROLLOVER  3u
+#define PNETGPU_FANOUT_RND       4u
+#define PNETGPU_FANOUT_QM        5u
+#define PNETGPU_FANOUT_FLAG_ROLLOVER 0x1000u
+#define PNETGPU_FANOUT_FLAG_DEFRAG   0x8000u
+int  pnetgpu_afp_fanout(pnetgpu_afp* afp, uint16_t group_id, uint32_t type, uint32_t flags);
+/* Promiscuous mode on the bound interface (the reference's Config::promiscuous). */
+int  pnetgpu_afp_promiscuous(pnetgpu_afp* afp, int on);
 /* Socket statistics (PACKET_STATISTICS: packets seen / dropped since the last call). */
 int  pnetgpu_afp_stats(pnetgpu_afp* afp, uint64_t* packets, uint64_t* drops);
 

@@ -26,6 +26,11 @@ lib.pnetgpu_afp_release_block.restype = ctypes.c_int32
 lib.pnetgpu_afp_release_block.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
 lib.pnetgpu_afp_stats.restype = ctypes.c_int32
 lib.pnetgpu_afp_stats.argtypes = [ctypes.c_void_p, _u64p, _u64p]
+lib.pnetgpu_afp_fanout.restype = ctypes.c_int32
+lib.pnetgpu_afp_fanout.argtypes = [ctypes.c_void_p, ctypes.c_uint16, ctypes.c_uint32, ctypes.c_uint32]
+lib.pnetgpu_afp_promiscuous.restype = ctypes.c_int32
+lib.pnetgpu_afp_promiscuous.argtypes = [ctypes.c_void_p, ctypes.c_int]
+FANOUT = {"hash": 0, "lb": 1, "cpu": 2, "rollover": 3, "rnd": 4, "qm": 5}
 lib.pnetgpu_tpacket3_walk.restype = ctypes.c_int32
 lib.pnetgpu_tpacket3_walk.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_void_p,
                                       ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, _u64p]
@@ -85,6 +90,14 @@ class AfPacket:
 
     def release(self, block):
         check(lib.pnetgpu_afp_release_block(self.h, block), "pnetgpu_afp_release_block")
+
+    def fanout(self, group_id, fanout_type="hash", defrag=False, rollover=False):
+        """Join PACKET_FANOUT group group_id (pnet_datalink's FanoutOption)."""
+        flags = (0x8000 if defrag else 0) | (0x1000 if rollover else 0)
+        check(lib.pnetgpu_afp_fanout(self.h, group_id, FANOUT[fanout_type], flags), "pnetgpu_afp_fanout")
+
+    def promiscuous(self, on=True):
+        check(lib.pnetgpu_afp_promiscuous(self.h, 1 if on else 0), "pnetgpu_afp_promiscuous")
 
     def stats(self):
         p, d = ctypes.c_uint64(), ctypes.c_uint64()

@@ -27,6 +27,7 @@ struct pnetgpu_afp {
     uint32_t block_bytes = 0;
     uint32_t n_blocks = 0;
     uint32_t next = 0;       // next block to hand out (ring order)
+    int ifindex = 0;         // bound interface (0 = all)
 };
 
 namespace {
@@ -133,6 +134,7 @@ int pnetgpu_afp_open(const char* ifname, uint32_t block_bytes, uint32_t n_blocks
     a->map_bytes = bytes;
     a->block_bytes = block_bytes;
     a->n_blocks = n_blocks;
+    a->ifindex = (int)ifindex;
     *out = a;
     return PNETGPU_OK;
 }
@@ -178,6 +180,22 @@ int pnetgpu_afp_release_block(pnetgpu_afp* a, uint32_t block) {
     uint8_t* blk = a->map + (uint64_t)block * a->block_bytes;
     __atomic_store_n(reinterpret_cast<uint32_t*>(blk + kBlkStatus), (uint32_t)TP_STATUS_KERNEL, __ATOMIC_RELEASE);
     return PNETGPU_OK;
+}
+
+int pnetgpu_afp_fanout(pnetgpu_afp* a, uint16_t group_id, uint32_t type, uint32_t flags) {
+    if (!a || type > PNETGPU_FANOUT_QM || (flags & ~(PNETGPU_FANOUT_FLAG_ROLLOVER | PNETGPU_FANOUT_FLAG_DEFRAG)))
+        return PNETGPU_EINVAL;
+    const unsigned arg = (unsigned)group_id | ((type | flags) << 16);
+    return setsockopt(a->fd, SOL_PACKET, PACKET_FANOUT, &arg, sizeof arg) == 0 ? PNETGPU_OK : PNETGPU_ESYS;
+}
+
+int pnetgpu_afp_promiscuous(pnetgpu_afp* a, int on) {
+    if (!a || a->ifindex == 0) return PNETGPU_EINVAL;      // needs one bound interface
+    packet_mreq mr{};
+    mr.mr_ifindex = a->ifindex;
+    mr.mr_type = PACKET_MR_PROMISC;
+    const int opt = on ? PACKET_ADD_MEMBERSHIP : PACKET_DROP_MEMBERSHIP;
+    return setsockopt(a->fd, SOL_PACKET, opt, &mr, sizeof mr) == 0 ? PNETGPU_OK : PNETGPU_ESYS;
 }
 
 int pnetgpu_afp_stats(pnetgpu_afp* a, uint64_t* packets, uint64_t* drops) {

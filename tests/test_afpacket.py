@@ -6,6 +6,7 @@ packet socket (CAP_NET_RAW; the GPU boxes do not grant it, the build container
 does) — a live ring on the loopback interface receiving UDP datagrams sent to
 127.0.0.1, parsed by the oracle. GPU: blocks walked and shipped zero-copy
 through the ring (Ring.feed_region) give the oracle's records."""
+import os
 import socket
 import struct
 import time
@@ -142,3 +143,45 @@ def test_tpacket3_blocks_through_ring():
     with lp.HostRegistration(ring_img):
         out = list(ring.feed_region(ring_img, offs, lens)) + list(ring.drain())
     check_batches(out, frames)
+
+
+def test_afpacket_fanout_splits_loopback_traffic():
+    """Two rings in one PACKET_FANOUT hash group on lo (one per GPU rank in a
+    deployment) share the datagrams: together they see every one, each some."""
+    try:
+        rings = [lp.AfPacket("lo", block_bytes=1 << 16, n_blocks=8, retire_ms=5) for _ in range(2)]
+    except PermissionError:
+        pytest.skip("no CAP_NET_RAW here")
+    group = os.getpid() & 0xFFFF                           # unique per test process
+    for r in rings:
+        r.fanout(group, "hash")
+    rxs = [socket.socket(socket.AF_INET, socket.SOCK_DGRAM) for _ in range(8)]
+    for s_ in rxs:
+        s_.bind(("127.0.0.1", 0))
+    ports = [s_.getsockname()[1] for s_ in rxs]
+    tx = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+    marker = b"pnetgpu-fanout-%d-" % ports[0]
+    for i in range(400):
+        tx.sendto(marker + b"%04d" % i, ("127.0.0.1", ports[i % len(ports)]))
+    seen = [set(), set()]
+    t0 = time.time()
+    while len(seen[0] | seen[1]) < 400 and time.time() - t0 < 10:
+        for k, r in enumerate(rings):
+            blk = r.next_block(20)
+            if blk is None:
+                continue
+            b, offs, lens, _ = blk
+            for o, n in zip(offs, lens):
+                f = bytes(r.ring[o:o + n])
+                j = f.find(marker)
+                if j >= 0:
+                    seen[k].add(int(f[j + len(marker):j + len(marker) + 4]))
+            r.release(b)
+    for r in rings:
+        r.close()
+    for s_ in rxs + [tx]:
+        s_.close()
+    if not (seen[0] | seen[1]):
+        pytest.skip("no loopback traffic visible to a packet socket here")
+    assert seen[0] | seen[1] == set(range(400))
+    assert seen[0] and seen[1]
