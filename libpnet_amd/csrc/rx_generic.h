@@ -184,7 +184,10 @@ __global__ __launch_bounds__(kBlock, 4) void rx_kernel(RxArgs a) {
             off += a.delta;
         }
         const bool desc_bad = in_batch && (off > a.limit || (uint64_t)len > a.limit - off);
-        if (!in_batch || desc_bad) len = 0;
+        if (!in_batch || desc_bad) {   // nothing is loaded for it (a wild offset must not be dereferenced)
+            len = 0;
+            off = 0;
+        }
         const int sh = (int)(off & 15);
         const uint64_t base = off - (uint64_t)sh;
         const uint32_t fend = (uint32_t)sh + len;            // slot-relative end of the frame

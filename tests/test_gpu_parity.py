@@ -172,8 +172,9 @@ def test_invalid_descriptors_and_partial_columns():
     lens = lens.copy()
     offs[3] = buf.size + 100
     lens[7] = buf.size
+    offs[11] = (1 << 40) + 7   # wild and misaligned: must be flagged, never dereferenced
     rec = oracle_desc(buf, offs, lens)
-    assert rec["status"][3] == pyoracle.ST_DESC_INVALID == rec["status"][7]
+    assert rec["status"][3] == pyoracle.ST_DESC_INVALID == rec["status"][7] == rec["status"][11]
     res = run_desc(buf, offs, lens, columns=("status", "l4_csum", "src_ipv6"))
     compare(res, rec)
     assert res.counter_dict() == oracle_counters(rec, lens)
