@@ -180,6 +180,42 @@ def test_invalid_descriptors_and_partial_columns():
     assert res.counter_dict() == oracle_counters(rec, lens)
 
 
+def test_descriptors_at_the_buffer_end():
+    """Descriptors ending exactly at, one byte past, and far past the end of the
+    buffer, at every alignment: in-bounds ones parse, the others are flagged
+    DESC_INVALID (nothing is read for them), every column equal to the oracle."""
+    rng = np.random.default_rng(17)
+    frames = framegen.random_frames(rng, 300)
+    buf, offs, lens = framegen.pack(frames)
+    size = buf.size
+    offs = offs.astype(np.uint64).copy()
+    lens = lens.astype(np.uint32).copy()
+    k = 0
+    for sh in range(16):                                  # ends exactly at the buffer end
+        lens[k] = 20 + sh
+        offs[k] = size - lens[k]
+        k += 1
+    for sh in range(16):                                  # one byte past the end
+        lens[k] = 40 + sh
+        offs[k] = size - lens[k] + 1
+        k += 1
+    for v in (size, size + 1, size + 15, 2**32 + 3, 2**48 + 9, 2**63 + 5):   # start at / past the end
+        offs[k] = v
+        lens[k] = 64
+        k += 1
+    offs[k] = 0                                           # length past the end, and a length overflowing off+len
+    lens[k] = size + 1
+    offs[k + 1] = 5
+    lens[k + 1] = 2**32 - 1
+    rec = oracle_desc(buf, offs, lens)
+    st = rec["status"]
+    assert not (st[:16] & pyoracle.ST_DESC_INVALID).any()
+    assert (st[16:k + 2] & pyoracle.ST_DESC_INVALID).all()
+    res = run_desc(buf, offs.view(np.int64), lens.view(np.int32))
+    compare(res, rec)
+    assert res.counter_dict() == oracle_counters(rec, lens)
+
+
 def test_stride_mode_odd_stride_and_offset():
     rng = np.random.default_rng(8)
     frames = [framegen.build_frame(rng, k, 77) for k in ("udp", "tcp", "icmp", "udp6", "tcp6", "icmp6")] * 50
