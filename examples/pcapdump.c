@@ -21,9 +21,20 @@
  * 4..7-B echo message, :54,:65) this prints "Malformed Ethernet Frame" /
  * "Malformed ICMP Packet" and goes on.
  *
+ * Live mode (-l IFACE) is packetdump's own loop on an interface
+ * (packetdump.rs:285-300: datalink::channel, rx.next(), handle_ethernet_frame)
+ * with the per-frame receive replaced by whole TPACKET_V3 blocks
+ * (pnetgpu_afpacket.h): each retired block's frames go from the ring mapping
+ * to the GPU in one submit, are printed once the batch is waited, and the
+ * block is then given back to the kernel. Needs CAP_NET_RAW.
+ *
  * usage: pcapdump [-i NAME] [-c] FILE.pcap
- *   -i NAME  the "[interface]" label (default: pcap)
+ *        pcapdump [-i NAME] [-c] -l IFACE [-n COUNT] [-w MS]
+ *   -i NAME  the "[interface]" label (default: pcap, or IFACE in live mode)
  *   -c       append the checksum verdicts to every IP line
+ *   -l IFACE capture from IFACE instead of reading a file
+ *   -n COUNT live: stop after COUNT frames
+ *   -w MS    live: stop after MS ms without a retired block (default: wait on)
  */
 #include <errno.h>
 #include <fcntl.h>
@@ -36,6 +47,7 @@
 #include <unistd.h>
 
 #include "pnetgpu.h"
+#include "pnetgpu_afpacket.h"
 #include "pnetgpu_ring.h"
 
 static const char* g_name = "pcap";
@@ -183,16 +195,90 @@ static int drain_one(pnetgpu_ring* ring) {
     return 0;
 }
 
+/* Print every batch in flight (the frames submitted so far). */
+static int drain_all(pnetgpu_ring* ring) {
+    int rc;
+    while (!(rc = drain_one(ring))) {
+    }
+    return rc == PNETGPU_EEMPTY ? 0 : rc;
+}
+
+/* Live capture: up to `count` frames (-1 = no limit); a wait of idle_ms
+ * without a retired block ends the capture (-1 = wait on). */
+static int live(const char* ifname, long long count, int idle_ms) {
+    pnetgpu_afp* afp = NULL;
+    int rc = pnetgpu_afp_open(ifname, 1u << 20, 64, 10, &afp);
+    if (rc) {
+        fprintf(stderr, "pcapdump: %s: %s\n", ifname, rc == PNETGPU_ESYS ? strerror(errno) : pnetgpu_strerror(rc));
+        return 1;
+    }
+    const uint8_t* base = NULL;
+    uint64_t bytes = 0;
+    uint32_t block_bytes = 0, n_blocks = 0;
+    rc = pnetgpu_afp_ring(afp, &base, &bytes, &block_bytes, &n_blocks);
+    const int registered = !rc && pnetgpu_host_register((void*)base, bytes) == PNETGPU_OK;
+    pnetgpu_ctx* ctx = NULL;
+    pnetgpu_ring* ring = NULL;
+    if (!rc) rc = pnetgpu_ctx_create(0, &ctx);
+    if (!rc) rc = pnetgpu_ring_create(ctx, 64u << 20, 1u << 18, 0, &ring);
+    /* a TPACKET_V3 packet takes at least its 48-B header plus 16-B-aligned data */
+    const uint64_t cap = block_bytes / 64u + 1u;
+    uint64_t* offs = (uint64_t*)malloc(sizeof(uint64_t) * cap);
+    uint32_t* lens = (uint32_t*)malloc(sizeof(uint32_t) * cap);
+    if (!rc && (!offs || !lens)) rc = PNETGPU_ENOMEM;
+    long long seen = 0;
+    while (!rc && (count < 0 || seen < count)) {
+        uint64_t n = 0;
+        uint32_t blk = 0;
+        rc = pnetgpu_afp_next_block(afp, idle_ms < 0 ? 1000 : idle_ms, offs, lens, NULL, cap, &n, &blk);
+        if (rc == PNETGPU_EEMPTY) {
+            rc = 0;
+            if (idle_ms >= 0) break;
+            continue;
+        }
+        if (rc) break;
+        if (count >= 0 && (long long)n > count - seen) n = (uint64_t)(count - seen);
+        for (uint64_t k = 0; !rc && k < n;) {
+            uint64_t taken = 0;
+            rc = pnetgpu_ring_submit_region(ring, base, offs + k, lens + k, n - k, &taken, NULL);
+            if (rc == PNETGPU_EBUSY) rc = drain_one(ring);
+            else k += taken;
+        }
+        if (!rc) rc = drain_all(ring);   /* the block is read until its batches are waited */
+        if (!rc) rc = pnetgpu_afp_release_block(afp, blk);
+        seen += (long long)n;
+        fflush(stdout);
+    }
+    if (rc) fprintf(stderr, "pcapdump: %s\n", pnetgpu_strerror(rc));
+    if (ring) pnetgpu_ring_destroy(ring);
+    if (ctx) pnetgpu_ctx_destroy(ctx);
+    if (registered) pnetgpu_host_unregister((void*)base);
+    pnetgpu_afp_close(afp);
+    free(offs);
+    free(lens);
+    return rc ? 1 : 0;
+}
+
 int main(int argc, char** argv) {
-    int opt;
-    while ((opt = getopt(argc, argv, "i:c")) != -1) {
-        if (opt == 'i') g_name = optarg;
+    int opt, named = 0, idle_ms = -1;
+    const char* iface = NULL;
+    long long count = -1;
+    while ((opt = getopt(argc, argv, "i:cl:n:w:")) != -1) {
+        if (opt == 'i') g_name = optarg, named = 1;
         else if (opt == 'c') g_csum = 1;
+        else if (opt == 'l') iface = optarg;
+        else if (opt == 'n') count = atoll(optarg);
+        else if (opt == 'w') idle_ms = atoi(optarg);
         else return 2;
     }
-    if (optind != argc - 1) {
-        fprintf(stderr, "usage: pcapdump [-i NAME] [-c] FILE.pcap\n");
+    if (iface ? optind != argc || count < -1 : optind != argc - 1) {
+        fprintf(stderr, "usage: pcapdump [-i NAME] [-c] FILE.pcap\n"
+                        "       pcapdump [-i NAME] [-c] -l IFACE [-n COUNT] [-w MS]\n");
         return 2;
+    }
+    if (iface) {
+        if (!named) g_name = iface;
+        return live(iface, count, idle_ms);
     }
     const int fd = open(argv[optind], O_RDONLY);
     struct stat sb;

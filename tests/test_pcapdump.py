@@ -146,3 +146,58 @@ def test_pcapdump_raw_ip_capture(tmp_path, linktype):
     assert got == want
     assert got[-1] == "[pcap]: Unknown packet: IP version 7; length: 31"
 
+
+
+def test_pcapdump_live_usage_and_bad_interface():
+    """-l IFACE: argument errors exit 2; an unknown interface (or a denied
+    packet socket) exits 1 with the reason, before any GPU call."""
+    r = subprocess.run([EXE, "-l", "lo", "extra.pcap"], capture_output=True, text=True, timeout=30)
+    assert r.returncode == 2 and "-l IFACE" in r.stderr
+    r = subprocess.run([EXE, "-l", "no-such-if0", "-n", "1", "-w", "10"], capture_output=True, text=True,
+                       timeout=30)
+    assert r.returncode == 1
+    assert "no-such-if0: invalid argument" in r.stderr or "not permitted" in r.stderr
+
+
+@pytest.mark.gpu
+def test_pcapdump_live_loopback():
+    """Live mode on `lo`: UDP datagrams sent while pcapdump -l captures come
+    back as packetdump's UDP lines (ports and UDP length as sent). Skips where
+    the box grants no CAP_NET_RAW or loopback traffic is invisible."""
+    import socket
+    import time
+    rx = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+    rx.bind(("127.0.0.1", 0))
+    port = rx.getsockname()[1]
+    tx = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+    tx.bind(("127.0.0.1", 0))
+    sport = tx.getsockname()[1]
+    p = subprocess.Popen([EXE, "-l", "lo", "-w", "3000"], stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                         text=True)
+    try:
+        time.sleep(2.0)   # socket open + HIP context before the traffic starts
+        if p.poll() is not None:
+            err = p.stderr.read()
+            if "not permitted" in err:
+                pytest.skip("no CAP_NET_RAW here")
+            pytest.fail("pcapdump -l lo exited early: " + err)
+        want = set()
+        for i in range(40):
+            tx.sendto(b"pnetgpu-live" + bytes(i), ("127.0.0.1", port))
+            want.add("[lo]: UDP Packet: 127.0.0.1:%d > 127.0.0.1:%d; length: %d" % (sport, port, 8 + 12 + i))
+        try:
+            out, err = p.communicate(timeout=30)
+        except subprocess.TimeoutExpired:   # other loopback traffic keeps it from going idle
+            p.kill()
+            out, err = p.communicate()
+    finally:
+        if p.poll() is None:
+            p.kill()
+            p.wait()
+        rx.close()
+        tx.close()
+    assert p.returncode in (0, -9), err
+    got = {ln for ln in out.splitlines() if ("127.0.0.1:%d" % port) in ln}
+    if not got:
+        pytest.skip("no loopback traffic visible to a packet socket here")
+    assert got == want
