@@ -155,7 +155,9 @@ def test_afpacket_fanout_splits_loopback_traffic():
     group = os.getpid() & 0xFFFF                           # unique per test process
     for r in rings:
         r.fanout(group, "hash")
-    rxs = [socket.socket(socket.AF_INET, socket.SOCK_DGRAM) for _ in range(8)]
+    # 32 flows: the chance that the hash puts every flow on one ring is 2^-31
+    # (with 8 flows it was 1 in 128, an occasional false failure)
+    rxs = [socket.socket(socket.AF_INET, socket.SOCK_DGRAM) for _ in range(32)]
     for s_ in rxs:
         s_.bind(("127.0.0.1", 0))
     ports = [s_.getsockname()[1] for s_ in rxs]
