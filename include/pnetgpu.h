@@ -118,6 +118,13 @@ extern "C" {
 #define PNETGPU_RX_IPV6_EXT       0x2u
 #define PNETGPU_RX_L3             0x4u
 
+/* Compact descriptors (descriptor mode; ignored with stride > 0): `offsets`
+ * points to uint32_t[n_frames] and `lengths` to uint16_t[n_frames] (cast to
+ * the fields' types) — 6 B per frame instead of 12, the layout SURVEY.md
+ * §8(b) suggested. For batches under 4 GiB with frames under 64 KiB; the
+ * pinned ring (pnetgpu_ring.h) uses it whenever a batch qualifies. */
+#define PNETGPU_DESC_COMPACT      0x100u
+
 /* ---- batch-wide counters (rx columns .counters, uint64 each, accumulated) */
 #define PNETGPU_CTR_FRAMES        0  /* frames with a valid descriptor            */
 #define PNETGPU_CTR_BYTES         1  /* sum of their lengths                      */

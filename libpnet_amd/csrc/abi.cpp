@@ -106,7 +106,9 @@ static int rx_common(pnetgpu_ctx* ctx, const pnetgpu_batch* b, const pnetgpu_rx_
         (cols->dst_ipv6 && (reinterpret_cast<uintptr_t>(cols->dst_ipv6) & 15)))
         return PNETGPU_EINVAL;
     if (b->n_frames > (UINT64_MAX - kRunFrames) / 2) return PNETGPU_EINVAL;
-    if ((b->flags & ~(PNETGPU_RX_VLAN | PNETGPU_RX_IPV6_EXT | PNETGPU_RX_L3)) || b->reserved) return PNETGPU_EINVAL;
+    if ((b->flags & ~(PNETGPU_RX_VLAN | PNETGPU_RX_IPV6_EXT | PNETGPU_RX_L3 | PNETGPU_DESC_COMPACT)) || b->reserved)
+        return PNETGPU_EINVAL;
+    const uint32_t rxf = b->flags & ~PNETGPU_DESC_COMPACT;   // parse extensions only
     int rc = set_device(ctx);
     if (rc) return rc;
 
@@ -120,7 +122,8 @@ static int rx_common(pnetgpu_ctx* ctx, const pnetgpu_batch* b, const pnetgpu_rx_
     a.lengths = b->lengths;
     a.cols = *cols;
     a.nruns = (a.n + kRunFrames - 1) / kRunFrames;
-    a.flags = b->flags;
+    a.flags = rxf;
+    a.desc_compact = b->stride == 0 && (b->flags & PNETGPU_DESC_COMPACT) != 0;
 
     // Kernel choice. Small: fixed stride, every frame 16-B aligned, at most 64 B,
     // inside the buffer (the 64-B configs). Otherwise rx_kernel with the tail
@@ -137,7 +140,7 @@ static int rx_common(pnetgpu_ctx* ctx, const pnetgpu_batch* b, const pnetgpu_rx_
         // kernels): contiguous frames >= 1 KiB apart with at most 1/8 of the span in gaps
         stream_ok = !tx && fits && b->stride >= 1024 && b->stride <= (1u << 20) && b->frame_len <= b->stride &&
                     b->frame_len >= 256 && (uint64_t)b->frame_len * 8 >= (uint64_t)b->stride * 7;
-        if (base_sh == 0 && b->stride % 16 == 0 && b->frame_len <= 64 && fits && b->flags == 0)
+        if (base_sh == 0 && b->stride % 16 == 0 && b->frame_len <= 64 && fits && rxf == 0)
             kind = pnetgpu::kKindSmall;
         else
             kind = b->frame_len >= 4096 ? pnetgpu::kKindJumbo : pnetgpu::kKindMtu;
@@ -154,7 +157,7 @@ static int rx_common(pnetgpu_ctx* ctx, const pnetgpu_batch* b, const pnetgpu_rx_
             kind != pnetgpu::kKindSmall)
             kind = v;
     }
-    const int ext = b->flags != 0;
+    const int ext = rxf != 0;
     int& per_cu_cached = ctx->per_cu[kind & 7][ext];
     if (per_cu_cached <= 0 || debug) {                             // first use of this kernel on ctx
         int numregs = 0, lds = 0;

@@ -28,6 +28,11 @@ struct Slot {
     uint8_t* h_frames = nullptr;
     uint64_t* h_off = nullptr;
     uint32_t* h_len = nullptr;
+    // the same descriptors in PNETGPU_DESC_COMPACT form (u32 / u16), written
+    // alongside; shipped instead when the batch is < 4 GiB and every frame < 64 KiB
+    uint32_t* h_off32 = nullptr;
+    uint16_t* h_len16 = nullptr;
+    uint32_t max_len = 0;
     uint8_t* d_frames = nullptr;
     uint64_t* d_off = nullptr;
     uint32_t* d_len = nullptr;
@@ -82,6 +87,8 @@ static void free_slot(Slot& s) {
     if (s.h_frames) (void)hipHostFree(s.h_frames);
     if (s.h_off) (void)hipHostFree(s.h_off);
     if (s.h_len) (void)hipHostFree(s.h_len);
+    if (s.h_off32) (void)hipHostFree(s.h_off32);
+    if (s.h_len16) (void)hipHostFree(s.h_len16);
     if (s.d_frames) (void)hipFree(s.d_frames);
     if (s.d_off) (void)hipFree(s.d_off);
     if (s.d_len) (void)hipFree(s.d_len);
@@ -106,6 +113,7 @@ static int take_free_slot(pnetgpu_ring* r) {
             r->slots[i].state = kFilling;
             r->slots[i].n = 0;
             r->slots[i].bytes = 0;
+            r->slots[i].max_len = 0;
             return i;
         }
     }
@@ -137,6 +145,8 @@ int pnetgpu_ring_create(pnetgpu_ctx* ctx, uint64_t batch_bytes, uint32_t batch_f
         ok = hipHostMalloc((void**)&s.h_frames, fb, hipHostMallocDefault) == hipSuccess &&
              hipHostMalloc((void**)&s.h_off, 8ull * batch_frames, hipHostMallocDefault) == hipSuccess &&
              hipHostMalloc((void**)&s.h_len, 4ull * batch_frames, hipHostMallocDefault) == hipSuccess &&
+             hipHostMalloc((void**)&s.h_off32, 4ull * batch_frames, hipHostMallocDefault) == hipSuccess &&
+             hipHostMalloc((void**)&s.h_len16, 2ull * batch_frames, hipHostMallocDefault) == hipSuccess &&
              hipMalloc((void**)&s.d_frames, fb) == hipSuccess &&
              hipMalloc((void**)&s.d_off, 8ull * batch_frames) == hipSuccess &&
              hipMalloc((void**)&s.d_len, 4ull * batch_frames) == hipSuccess &&
@@ -177,6 +187,9 @@ int pnetgpu_ring_push(pnetgpu_ring* r, const uint8_t* frame, uint32_t len) {
     std::memcpy(s.h_frames + s.bytes, frame, len);
     s.h_off[s.n] = s.bytes;
     s.h_len[s.n] = len;
+    s.h_off32[s.n] = (uint32_t)s.bytes;
+    s.h_len16[s.n] = (uint16_t)len;
+    s.max_len = std::max(s.max_len, len);
     s.bytes += len;
     s.n += 1;
     return PNETGPU_OK;
@@ -195,6 +208,9 @@ int pnetgpu_ring_push_many(pnetgpu_ring* r, const uint8_t* buf, const uint64_t* 
     while (k < n && k < room_f && lengths[k] <= r->cap_bytes - s.bytes - bytes) {
         s.h_off[s.n + k] = s.bytes + bytes;
         s.h_len[s.n + k] = lengths[k];
+        s.h_off32[s.n + k] = (uint32_t)(s.bytes + bytes);
+        s.h_len16[s.n + k] = (uint16_t)lengths[k];
+        s.max_len = std::max(s.max_len, lengths[k]);
         bytes += lengths[k];
         ++k;
     }
@@ -235,11 +251,20 @@ int pnetgpu_ring_push_many(pnetgpu_ring* r, const uint8_t* buf, const uint64_t* 
 static int ship_slot(pnetgpu_ring* r, Slot& s, const uint8_t* src, uint64_t* id) {
     if (hipSetDevice(r->device) != hipSuccess) return PNETGPU_EHIP;
     const hipStream_t st = s.stream;
+    // compact descriptors (6 B/frame over PCIe instead of 12) whenever they can
+    // describe the batch; the full ones stay on the host for the waited batch view
+#ifdef PNETGPU_RING_FULL_DESC   // A/B build only (tools/): always the u64/u32 form
+    const bool compact = false;
+#else
+    const bool compact = s.bytes <= UINT32_MAX && s.max_len <= UINT16_MAX;
+#endif
+    const void* h_off = compact ? (const void*)s.h_off32 : (const void*)s.h_off;
+    const void* h_len = compact ? (const void*)s.h_len16 : (const void*)s.h_len;
     // granule rule: the tail past the last frame is readable (32 zero bytes)
     if (hipMemcpyAsync(s.d_frames, src, s.bytes, hipMemcpyHostToDevice, st) != hipSuccess ||
         (src != s.h_frames && hipMemsetAsync(s.d_frames + s.bytes, 0, 32, st) != hipSuccess) ||
-        hipMemcpyAsync(s.d_off, s.h_off, 8ull * s.n, hipMemcpyHostToDevice, st) != hipSuccess ||
-        hipMemcpyAsync(s.d_len, s.h_len, 4ull * s.n, hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipMemcpyAsync(s.d_off, h_off, (compact ? 4ull : 8ull) * s.n, hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipMemcpyAsync(s.d_len, h_len, (compact ? 2ull : 4ull) * s.n, hipMemcpyHostToDevice, st) != hipSuccess ||
         hipMemsetAsync(s.d_rec, 0, 8ull * PNETGPU_NCOUNTERS, st) != hipSuccess)
         return PNETGPU_EHIP;
     pnetgpu_batch b{};
@@ -248,7 +273,7 @@ static int ship_slot(pnetgpu_ring* r, Slot& s, const uint8_t* src, uint64_t* id)
     b.n_frames = s.n;
     b.offsets = s.d_off;
     b.lengths = s.d_len;
-    b.flags = r->flags;
+    b.flags = r->flags | (compact ? PNETGPU_DESC_COMPACT : 0u);
     pnetgpu_rx_columns c{};
     uint64_t at = 8ull * PNETGPU_NCOUNTERS;          // the counters lead the record block
     for (int k = 0; k < kNumCols; ++k) {
@@ -302,6 +327,9 @@ int pnetgpu_ring_submit_region(pnetgpu_ring* r, const uint8_t* base, const uint6
         if (fe - o0 > r->cap_bytes) break;
         s.h_off[k] = offsets[k] - o0;
         s.h_len[k] = lengths[k];
+        s.h_off32[k] = (uint32_t)(offsets[k] - o0);
+        s.h_len16[k] = (uint16_t)lengths[k];
+        s.max_len = std::max(s.max_len, lengths[k]);
         end = fe;
         ++k;
     }

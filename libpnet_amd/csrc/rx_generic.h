@@ -161,8 +161,13 @@ __global__ __launch_bounds__(kBlock, 4) void rx_kernel(RxArgs a) {
     auto fetch_desc = [&](uint64_t r) {
         const uint64_t fr = r * kWave + lane;
         if (!a.stride && r < a.nruns && fr < a.n) {
-            d_off = a.offsets[fr];
-            d_len = a.lengths[fr];
+            if (a.desc_compact) {   // wave-uniform
+                d_off = reinterpret_cast<const uint32_t*>(a.offsets)[fr];
+                d_len = reinterpret_cast<const uint16_t*>(a.lengths)[fr];
+            } else {
+                d_off = a.offsets[fr];
+                d_len = a.lengths[fr];
+            }
         }
     };
     fetch_desc((uint64_t)blockIdx.x * kWavesPerBlock + wv);

@@ -21,6 +21,7 @@ struct RxArgs {
     const uint32_t* lengths;
     uint64_t nruns;          // ceil(n / 64): one wave per run of 64 frames
     uint32_t flags;          // PNETGPU_RX_* (the small kernel requires 0)
+    uint32_t desc_compact;   // offsets/lengths are uint32_t/uint16_t arrays (PNETGPU_DESC_COMPACT)
     pnetgpu_rx_columns cols;
 };
 

@@ -48,6 +48,7 @@ assert tuple(COLUMNS) == COLUMN_NAMES
 IPV4_COLUMNS = ("status", "ip_csum", "l4_csum", "ethertype", "ip_proto", "ttl", "l4_offset", "l4_length",
                 "src_port", "dst_port", "src_ipv4", "dst_ipv4")
 RX_VLAN, RX_IPV6_EXT, RX_L3 = DEFS["PNETGPU_RX_VLAN"], DEFS["PNETGPU_RX_IPV6_EXT"], DEFS["PNETGPU_RX_L3"]
+DESC_COMPACT = DEFS["PNETGPU_DESC_COMPACT"]
 ALL_COLUMNS = COLUMN_NAMES
 NCOUNTERS = DEFS["PNETGPU_NCOUNTERS"]
 COUNTER_NAMES = ("frames", "bytes", "ipv4", "ipv6", "ip_csum_bad", "l4_csum_bad", "malformed", "unknown")
@@ -170,7 +171,9 @@ def rx_process(data, *, n_frames=None, stride=0, frame_len=None, first_offset=0,
     """Parse + verify every frame of a device-resident batch.
 
     Fixed-stride mode: stride > 0, frame i = data[first_offset + i*stride, +frame_len).
-    Descriptor mode:   offsets (int64) / lengths (int32) CUDA tensors, frame i = data[off_i, +len_i).
+    Descriptor mode:   offsets (int64) / lengths (int32) CUDA tensors, frame i = data[off_i, +len_i);
+                       with flags |= DESC_COMPACT, offsets (u32 as int32/uint32) / lengths
+                       (u16 as int16/uint16) — 6 B per frame of descriptors instead of 12.
     ctx: a Context (default: one shared per device); one host thread per context at a time.
     Returns an RxResult (device columns, accumulated counters)."""
     return _rx_or_tx("pnetgpu_rx_process", data, n_frames, stride, frame_len, first_offset, offsets, lengths,
@@ -201,7 +204,11 @@ def _rx_or_tx(fn_name, data, n_frames, stride, frame_len, first_offset, offsets,
             raise ValueError("descriptor mode needs offsets and lengths")
         if n_frames is None:
             n_frames = offsets.numel()
-        if offsets.dtype != torch.int64 or lengths.dtype != torch.int32 or not offsets.is_cuda:
+        if flags & DESC_COMPACT:
+            if (offsets.dtype not in (torch.int32, torch.uint32) or lengths.dtype not in (torch.int16, torch.uint16)
+                    or not offsets.is_cuda):
+                raise TypeError("DESC_COMPACT: offsets must be 32-bit and lengths 16-bit CUDA tensors")
+        elif offsets.dtype != torch.int64 or lengths.dtype != torch.int32 or not offsets.is_cuda:
             raise TypeError("offsets must be int64 and lengths int32 CUDA tensors")
         frame_len = 0
     if out is None:

@@ -1,0 +1,91 @@
+"""GPU parity of compact descriptors (PNETGPU_DESC_COMPACT: u32 offsets, u16
+lengths — SURVEY.md §8(b)'s suggested layout) vs the oracle and vs the full
+u64/u32 descriptors of the same batch: random and extension frames at any
+alignment (with and without the parse extensions), invalid descriptors, the
+full-size IMIX workload, and the pinned ring, which ships compact descriptors
+whenever a batch qualifies."""
+import numpy as np
+import pytest
+import torch
+
+import libpnet_amd as lp
+from libpnet_amd.engine import ALL_COLUMNS
+from oracle import coracle
+from tests import framegen
+from tests.test_gpu_parity import compare, oracle_counters, to_dev
+
+pytestmark = pytest.mark.gpu
+
+
+def run_compact(d, offs, lens, flags=0, columns=ALL_COLUMNS):
+    res = lp.rx_process(d, offsets=to_dev(np.asarray(offs, np.uint32).view(np.int32)),
+                        lengths=to_dev(np.asarray(lens, np.uint16).view(np.int16)), columns=columns,
+                        flags=flags | lp.DESC_COMPACT)
+    torch.cuda.synchronize()
+    return res
+
+
+@pytest.mark.parametrize("flags", [0, 3])
+def test_compact_random_and_extension_frames(flags):
+    rng = np.random.default_rng(70 + flags)
+    frames = framegen.extension_frames(rng) + framegen.random_frames(rng, 4000, max_len=9100)
+    buf, offs, lens = framegen.pack(frames, gap=13, rng=rng)
+    rec = coracle.rx_batch(buf, len(frames), offsets=offs, lengths=lens, flags=flags)
+    for data_offset in (0, 5):
+        d = to_dev(np.concatenate([np.zeros(16, np.uint8), buf]))[data_offset:]
+        res = run_compact(d, offs + 16 - data_offset, lens, flags=flags)
+        compare(res, rec)
+        assert res.counter_dict() == oracle_counters(rec, lens)
+
+
+def test_compact_invalid_descriptors():
+    """Offsets past the end (up to 2^32 - 1) and lengths running past it are
+    flagged DESC_INVALID, exactly as with full descriptors."""
+    rng = np.random.default_rng(9)
+    frames = framegen.random_frames(rng, 400)
+    buf, offs, lens = framegen.pack(frames)
+    offs = offs.astype(np.uint64).copy()
+    lens = lens.astype(np.uint32).copy()
+    size = buf.size
+    for k, (o, n) in enumerate([(size, 64), (size + 1, 14), (2**32 - 1, 60), (2**31, 1), (size - 10, 11),
+                                (size - 100, 65535), (size - 20, 20)]):
+        offs[k], lens[k] = o, n
+    rec = coracle.rx_batch(buf, len(offs), offsets=offs, lengths=lens)
+    assert (rec["status"][:6] & 0x8000).all() and not rec["status"][6] & 0x8000
+    res = run_compact(to_dev(buf), offs, lens)
+    compare(res, rec)
+    assert res.counter_dict() == oracle_counters(rec, lens)
+
+
+def test_compact_imix_full_size_equals_full_descriptors():
+    w = lp.synth.make("imix", 1 << 22, seed=5, corrupt_ppm=10000)
+    d = to_dev(w.buf)
+    full = lp.rx_process(d, offsets=to_dev(w.offsets.astype(np.int64)),
+                         lengths=to_dev(w.lengths.astype(np.int32)), columns=lp.IPV4_COLUMNS)
+    comp = run_compact(d, w.offsets, w.lengths, columns=lp.IPV4_COLUMNS)
+    a, b = full.numpy(), comp.numpy()
+    for c in lp.IPV4_COLUMNS:
+        assert np.array_equal(a[c], b[c]), c
+    assert full.counter_dict() == comp.counter_dict()
+    assert comp.counter_dict()["frames"] == 1 << 22
+
+
+def test_ring_ships_compact_descriptors_and_full_ones_for_long_frames():
+    """The ring's batches (compact when every frame < 64 KiB, full otherwise)
+    equal the oracle; a 70,000-B frame forces the full form for its batch."""
+    rng = np.random.default_rng(21)
+    frames = framegen.random_frames(rng, 3000, max_len=1600)
+    big = bytearray(framegen.build_frame(rng, "udp", 100))
+    big += bytes(70000 - len(big))
+    frames.insert(1500, bytes(big))
+    buf, offs, lens = framegen.pack(frames, gap=5, rng=rng)
+    rec = coracle.rx_batch(buf, len(offs), offsets=offs, lengths=lens)
+    ring = lp.Ring(batch_bytes=1 << 20, batch_frames=1000, columns=ALL_COLUMNS)   # copy=True: batches outlive waits
+    try:
+        got = list(ring.feed_region(buf, offs, lens)) + list(ring.drain())
+    finally:
+        ring.close()
+    assert [b.id for b in got] == list(range(len(got))) and len(got) >= 4
+    assert sum(b.n for b in got) == len(offs)
+    for c in ALL_COLUMNS:
+        assert np.array_equal(np.concatenate([b.records[c] for b in got]), rec[c]), c
