@@ -63,13 +63,22 @@ class Shard:
         self.w = w
         self.data = torch.from_numpy(w.buf).to(device)
         self.offsets = self.lengths = None
+        self.flags = 0
+        self.desc_bytes = 0
         if not w.stride:
-            self.offsets = torch.from_numpy(w.offsets.view(np.int64)).to(device)
-            self.lengths = torch.from_numpy(w.lengths.view(np.int32)).to(device)
+            # compact descriptors (u32 offset + u16 length, PNETGPU_DESC_COMPACT) when
+            # they can describe the batch, else u64 + u32
+            if w.buf.size <= 0xFFFFFFFF and int(w.lengths.max()) <= 0xFFFF:
+                self.offsets = torch.from_numpy(w.offsets.astype(np.uint32).view(np.int32)).to(device)
+                self.lengths = torch.from_numpy(w.lengths.astype(np.uint16).view(np.int16)).to(device)
+                self.flags, self.desc_bytes = lp.DESC_COMPACT, 6
+            else:
+                self.offsets = torch.from_numpy(w.offsets.view(np.int64)).to(device)
+                self.lengths = torch.from_numpy(w.lengths.view(np.int32)).to(device)
+                self.desc_bytes = 12
         self.res = lp.RxResult(n, device, columns, counters=True)
         self.frame_bytes = w.expect["bytes"]
         self.result_bytes = lp.column_bytes(columns)
-        self.desc_bytes = 0 if w.stride else 12          # u64 offset + u32 length
         # algorithmic bytes per launch: frames read once + result columns written + descriptors
         self.alg_bytes = self.frame_bytes + n * (self.result_bytes + self.desc_bytes)
 
@@ -78,7 +87,8 @@ class Shard:
             lp.rx_process(self.data, stride=self.w.stride, frame_len=self.w.frame_len, n_frames=self.n,
                           out=self.res, stream=stream)
         else:
-            lp.rx_process(self.data, offsets=self.offsets, lengths=self.lengths, out=self.res, stream=stream)
+            lp.rx_process(self.data, offsets=self.offsets, lengths=self.lengths, out=self.res, stream=stream,
+                          flags=self.flags)
 
 
 def time_shard(sh, steps, warmup, stream, dist_on):
@@ -469,6 +479,7 @@ def main():
                 "achieved_gbs": round(r["achieved_gbs"], 1), "counters_ok": r["counters_ok"],
                 "traffic": load_traffic(name), "kernel": WORKLOADS[name]["kernel"],
                 "alg_bytes_per_launch": r["sh"].alg_bytes, "result_bytes_per_frame": r["sh"].result_bytes,
+                "desc_bytes_per_frame": r["sh"].desc_bytes,
             }
         if world == 1 and not args.no_cpu:
             line["cpu_baseline"] = cpu_baseline(sh)
