@@ -15,6 +15,8 @@ Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu] [--no-e2e]
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -24,8 +26,9 @@ import torch
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-import libpnet_amd as lp  # noqa: E402
-from libpnet_amd import shard  # noqa: E402
+# libpnet_amd (the HIP library) is imported by main() only after the launcher
+# decision: a `--gpus N` parent that starts the ranks never loads it
+lp = shard = None
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (/opt/skills/guides/MI355X_MICROARCH.md:36)
 METRIC = "device-resident Mpkts/s & GB/s, checksum+parse, 64B & 1500B, 1/2/4/8 GPU"
@@ -368,9 +371,56 @@ def load_traffic(workload):
         return None
 
 
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(n):
+    """`python bench.py --gpus N` (N > 1, no WORLD_SIZE in the environment): start
+    the N ranks with torchrun as a CHILD process (one process per GPU, RANK /
+    LOCAL_RANK / WORLD_SIZE from torchrun) and exit with its status. This parent
+    never touches the GPU and never execs (the children initialise the GPUs)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "1")
+    log(f"[bench] --gpus {n}: starting {n} ranks: {' '.join(cmd)}")
+    return subprocess.run(cmd, env=env).returncode
+
+
+def launch_check(args, world, rank):
+    """--launch-check: the multi-rank harness without the GPU (CPU test of the
+    driver's `bench.py --gpus N` shape, gloo). Each rank takes its byte-balanced
+    shard of a small IMIX length vector (shard.shard_by_bytes, the configs[3]
+    partition), the counters are all-reduced and the time max-reduced exactly as
+    in a GPU run, and rank 0 prints the line."""
+    import libpnet_amd.shard as shard_mod
+    rng = np.random.default_rng(args.seed)
+    n = 100003
+    lengths = rng.choice(np.array([64, 576, 1500], dtype=np.uint32), size=n, p=[7 / 12, 4 / 12, 1 / 12])
+    t0 = time.perf_counter()
+    lo, hi = shard_mod.shard_by_bytes(lengths, world, rank)
+    ctr = torch.tensor([hi - lo, int(lengths[lo:hi].sum()), rank], dtype=torch.int64)
+    shard_mod.all_reduce_counters(ctr)
+    wall = shard_mod.all_reduce_max(time.perf_counter() - t0, "cpu")
+    ok = int(ctr[0]) == n and int(ctr[1]) == int(lengths.sum()) and int(ctr[2]) == world * (world - 1) // 2
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "launch_check": True, "n_gpus": world, "world_size": world,
+                          "frames": int(ctr[0]), "bytes": int(ctr[1]), "wall_s": wall, "counters_ok": ok}),
+              flush=True)
+    return 0 if ok else 1
+
+
 def main():
+    global lp, shard
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks (one per GPU); without WORLD_SIZE set, N > 1 starts them with torchrun")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workloads", default="udp64,tcp1500,imix,udp6_jumbo,udp64_verify",
@@ -379,12 +429,32 @@ def main():
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the TX-fill and checksum-slices rates")
     ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--launch-check", action="store_true",
+                    help="rank start-up, shard_by_bytes partition and the reductions only (no GPU; gloo)")
+    ap.add_argument("--frames-scale", type=float, default=1.0,
+                    help="scale every workload's frame count (rehearsals only; the bench line records it)")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return spawn_ranks(args.gpus)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist_on = world > 1
+    if world != args.gpus:
+        raise SystemExit(f"bench: WORLD_SIZE={world} but --gpus {args.gpus}: one rank per GPU")
+    if args.launch_check:
+        if dist_on:
+            torch.distributed.init_process_group("gloo")
+            assert torch.distributed.get_world_size() == world
+        rc = launch_check(args, world, rank)
+        if dist_on:
+            torch.distributed.destroy_process_group()
+        return rc
+
+    import libpnet_amd as _lp
+    from libpnet_amd import shard as _shard
+    lp, shard = _lp, _shard
     # one rank per GPU; the modulo only matters for a rehearsal with more ranks
     # than GPUs (PNETGPU_BENCH_BACKEND=gloo, e.g. 2 ranks on a 1-GPU box)
     local = local % max(1, torch.cuda.device_count())
@@ -394,6 +464,7 @@ def main():
         import datetime
         backend = os.environ.get("PNETGPU_BENCH_BACKEND", "nccl")   # nccl = RCCL over xGMI
         torch.distributed.init_process_group(backend, timeout=datetime.timedelta(minutes=10))
+        assert torch.distributed.get_world_size() == world
 
     names = [w for w in args.workloads.split(",") if w]
     results = {}
@@ -401,7 +472,8 @@ def main():
     for name in names:
         cfg = WORKLOADS[name]
         t = time.perf_counter()
-        sh = Shard(name, cfg["n"], args.seed * 1000 + rank, device)
+        n = max(64, int(cfg["n"] * args.frames_scale))
+        sh = Shard(name, n, args.seed * 1000 + rank, device)
         if dist_on:
             # the host copy only serves the N=1 extras (CPU baseline, PCIe lines);
             # with 8 ranks on a node it would hold ~50 GB of host memory for nothing
@@ -455,6 +527,7 @@ def main():
                 "mode": "fixed-stride" if sh.w.stride else "descriptor",
                 "result_bytes_per_frame": sh.result_bytes,
                 "parallelism": f"shard-by-index x{world}",
+                **({"frames_scale": args.frames_scale} if args.frames_scale != 1.0 else {}),
             },
             "gb_s": round(p["gb_s"], 1),
             "roofline": {
@@ -502,4 +575,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -63,7 +63,7 @@
 extern "C" {
 #endif
 
-#define PNETGPU_ABI_VERSION 2
+#define PNETGPU_ABI_VERSION 3
 
 /* ---- return codes ------------------------------------------------------- */
 #define PNETGPU_OK        0
@@ -179,10 +179,41 @@ typedef struct pnetgpu_rx_columns {
     uint16_t* vlan_tci;   /* outer VlanPacket TCI (pcp|dei|vid) when PNET_ST_VLAN  */
     uint8_t*  l3_offset;  /* frame offset of the IP header (14, or 18/22 past tags) */
     uint64_t* counters;   /* [PNETGPU_NCOUNTERS], atomically accumulated           */
+    /* ---- header-field columns (ABI v3): the remaining generated getters of
+     * each view, written only when requested. A column is 0 for a frame whose
+     * dispatch did not construct that view (its new() returned None or was
+     * never called). Multi-bit fields are the getters' values, not raw bytes. */
+    uint64_t* eth_dst;             /* EthernetPacket get_destination: MacAddr octets as a BE-valued u48  (ethernet.rs:20-30) */
+    uint64_t* eth_src;             /* EthernetPacket get_source                                         */
+    uint8_t*  ip_version;          /* Ipv4Packet / Ipv6Packet get_version (u4)          (ipv4.rs:140, ipv6.rs:23) */
+    uint8_t*  ip_header_length;    /* Ipv4 get_header_length (u4, the raw IHL)          (ipv4.rs:141)     */
+    uint8_t*  ip_dscp;             /* Ipv4 get_dscp (u6)                                (ipv4.rs:142)     */
+    uint8_t*  ip_ecn;              /* Ipv4 get_ecn (u2)                                 (ipv4.rs:143)     */
+    uint16_t* ip_total_length;     /* Ipv4 get_total_length                             (ipv4.rs:144)     */
+    uint16_t* ip_identification;   /* Ipv4 get_identification                           (ipv4.rs:145)     */
+    uint8_t*  ip_flags;            /* Ipv4 get_flags (u3)                               (ipv4.rs:146)     */
+    uint16_t* ip_fragment_offset;  /* Ipv4 get_fragment_offset (u13be)                  (ipv4.rs:147)     */
+    uint8_t*  ip6_traffic_class;   /* Ipv6 get_traffic_class (u8 across the nibbles)    (ipv6.rs:24)      */
+    uint32_t* ip6_flow_label;      /* Ipv6 get_flow_label (u20be)                       (ipv6.rs:25)      */
+    uint16_t* ip6_payload_length;  /* Ipv6 get_payload_length                           (ipv6.rs:26)      */
+    uint16_t* udp_length;          /* UdpPacket get_length                              (udp.rs:27)       */
+    uint32_t* tcp_sequence;        /* TcpPacket get_sequence                            (tcp.rs:59)       */
+    uint32_t* tcp_acknowledgement; /* TcpPacket get_acknowledgement                     (tcp.rs:60)       */
+    uint8_t*  tcp_data_offset;     /* TcpPacket get_data_offset (u4)                    (tcp.rs:61)       */
+    uint8_t*  tcp_reserved;        /* TcpPacket get_reserved (u4)                       (tcp.rs:62)       */
+    uint8_t*  tcp_flags;           /* TcpPacket get_flags (u8)                          (tcp.rs:63)       */
+    uint16_t* tcp_window;          /* TcpPacket get_window                              (tcp.rs:64)       */
+    uint16_t* tcp_urgent_ptr;      /* TcpPacket get_urgent_ptr                          (tcp.rs:66)       */
+    uint16_t* icmp_sequence;       /* Icmp(v6) echo get_sequence_number: BE16 at +6 when the ICMP(v6)
+                                    * slice holds >= 8 B, the EchoRequest/EchoReply view (icmp.rs:221-232,
+                                    * 303-314); its identifier is dst_port                                */
 } pnetgpu_rx_columns;
 
 int         pnetgpu_abi_version(void);
 const char* pnetgpu_strerror(int code);
+/* The hipError_t behind the last PNETGPU_EHIP a kernel launch returned on the
+ * calling thread (0 if none); PNETGPU_DEBUG=1 also prints it to stderr. */
+int         pnetgpu_last_hip_error(void);
 int         pnetgpu_device_count(int* count);
 
 int  pnetgpu_ctx_create(int device, pnetgpu_ctx** out);

@@ -75,11 +75,13 @@ int pnetgpu_ring_submit(pnetgpu_ring* ring, uint64_t* id);
 int pnetgpu_ring_submit_region(pnetgpu_ring* ring, const uint8_t* base, const uint64_t* offsets,
                                const uint32_t* lengths, uint64_t n, uint64_t* taken, uint64_t* id);
 /* Columns later submissions compute and copy back: bit k selects the k-th
- * column of pnetgpu_rx_columns in struct order (status = bit 0 ... l3_offset =
- * bit 15); default all 16. A waited batch's unselected columns are NULL. Fewer
- * columns = fewer result bytes over PCIe (all 16: 61 B/frame; the IPv4 set,
- * bits 0-11: 26 B/frame). */
-int pnetgpu_ring_set_columns(pnetgpu_ring* ring, uint32_t column_mask);
+ * column of pnetgpu_rx_columns in struct order, counters not counted (status =
+ * bit 0 ... l3_offset = bit 15, eth_dst = bit 16 ... icmp_sequence = bit 37);
+ * default the 16 record columns (0xFFFF). A waited batch's unselected columns
+ * are NULL. Fewer columns = fewer result bytes over PCIe (bits 0-15: 61 B/frame;
+ * the IPv4 set, bits 0-11: 26 B/frame; all 38: 114 B/frame). Growing the record
+ * returns PNETGPU_EBUSY while a batch is in flight or held. */
+int pnetgpu_ring_set_columns(pnetgpu_ring* ring, uint64_t column_mask);
 /* Page-lock existing host memory for direct DMA (hipHostRegister) and undo it. */
 int pnetgpu_host_register(void* p, uint64_t bytes);
 int pnetgpu_host_unregister(void* p);

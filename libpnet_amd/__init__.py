@@ -10,7 +10,8 @@ from . import packet, synth  # noqa: F401  (packet: pnet_packet's function names
 from .ring import HostRegistration, Ring, pcap_frames, pcap_index, pcap_info  # noqa: F401
 from .afpacket import AfPacket, tpacket3_walk  # noqa: F401
 from .views import frame_view  # noqa: F401
-from .engine import (ALL_COLUMNS, COUNTER_NAMES, DESC_COMPACT, IPV4_COLUMNS, Context, RxResult,  # noqa: F401
+from .engine import (ALL_COLUMNS, COUNTER_NAMES, DESC_COMPACT, FIELD_COLUMNS, IPV4_COLUMNS, RECORD_COLUMNS,  # noqa: F401
+                     Context, RxResult,
                      checksum_adv_slices, checksum_slices, column_bytes, context, ipv4_checksum_slices,
                      ipv6_checksum_slices, rx_process, tx_fill_checksums)
 

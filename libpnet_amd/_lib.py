@@ -24,6 +24,9 @@ class PnetGpuError(RuntimeError):
     def __init__(self, code, what=""):
         self.code = code
         msg = _lib.pnetgpu_strerror(code).decode() if _lib is not None else str(code)
+        self.hip_error = _lib.pnetgpu_last_hip_error() if _lib is not None and code == -3 else 0
+        if self.hip_error:
+            msg += f", hipError_t {self.hip_error}"
         super().__init__(f"{what}: pnetgpu error {code} ({msg})")
 
 
@@ -56,12 +59,20 @@ class Batch(ctypes.Structure):
                 ("reserved", ctypes.c_uint32)]
 
 
+# pnetgpu_rx_columns in struct order: the record columns, `counters`, then the
+# header-field columns of ABI v3
 COLUMN_NAMES = ("status", "ip_csum", "l4_csum", "ethertype", "ip_proto", "ttl", "l4_offset", "l4_length",
                 "src_port", "dst_port", "src_ipv4", "dst_ipv4", "src_ipv6", "dst_ipv6", "vlan_tci", "l3_offset")
+FIELD_COLUMN_NAMES = ("eth_dst", "eth_src", "ip_version", "ip_header_length", "ip_dscp", "ip_ecn", "ip_total_length",
+                      "ip_identification", "ip_flags", "ip_fragment_offset", "ip6_traffic_class", "ip6_flow_label",
+                      "ip6_payload_length", "udp_length", "tcp_sequence", "tcp_acknowledgement", "tcp_data_offset",
+                      "tcp_reserved", "tcp_flags", "tcp_window", "tcp_urgent_ptr", "icmp_sequence")
+ALL_COLUMN_NAMES = COLUMN_NAMES + FIELD_COLUMN_NAMES
 
 
 class RxColumns(ctypes.Structure):
-    _fields_ = [(n, ctypes.c_void_p) for n in COLUMN_NAMES] + [("counters", ctypes.c_void_p)]
+    _fields_ = ([(n, ctypes.c_void_p) for n in COLUMN_NAMES] + [("counters", ctypes.c_void_p)]
+                + [(n, ctypes.c_void_p) for n in FIELD_COLUMN_NAMES])
 
 
 def _load():
@@ -73,6 +84,8 @@ def _load():
     L.pnetgpu_abi_version.restype = i32
     L.pnetgpu_strerror.restype = ctypes.c_char_p
     L.pnetgpu_strerror.argtypes = [i32]
+    L.pnetgpu_last_hip_error.restype = i32
+    L.pnetgpu_last_hip_error.argtypes = []
     L.pnetgpu_device_count.restype = i32
     L.pnetgpu_device_count.argtypes = [ctypes.POINTER(i32)]
     L.pnetgpu_ctx_create.restype = i32

@@ -25,6 +25,9 @@ struct pnetgpu_ctx {
 
 namespace pnetgpu {
 int ctx_device(const pnetgpu_ctx* ctx) { return ctx->device; }
+static thread_local int g_last_hip_error = 0;
+int last_hip_error() { return g_last_hip_error; }
+void set_last_hip_error(int e) { g_last_hip_error = e; }
 }  // namespace pnetgpu
 
 namespace {
@@ -66,6 +69,8 @@ const char* pnetgpu_strerror(int code) {
         default: return "unknown pnetgpu error";
     }
 }
+
+int pnetgpu_last_hip_error(void) { return pnetgpu::last_hip_error(); }
 
 int pnetgpu_device_count(int* count) {
     if (!count) return PNETGPU_EINVAL;
@@ -124,6 +129,13 @@ static int rx_common(pnetgpu_ctx* ctx, const pnetgpu_batch* b, const pnetgpu_rx_
     a.nruns = (a.n + kRunFrames - 1) / kRunFrames;
     a.flags = rxf;
     a.desc_compact = b->stride == 0 && (b->flags & PNETGPU_DESC_COMPACT) != 0;
+    a.l3mode = (rxf & PNETGPU_RX_L3) != 0;
+    a.field_cols = cols->eth_dst || cols->eth_src || cols->ip_version || cols->ip_header_length || cols->ip_dscp ||
+                   cols->ip_ecn || cols->ip_total_length || cols->ip_identification || cols->ip_flags ||
+                   cols->ip_fragment_offset || cols->ip6_traffic_class || cols->ip6_flow_label ||
+                   cols->ip6_payload_length || cols->udp_length || cols->tcp_sequence || cols->tcp_acknowledgement ||
+                   cols->tcp_data_offset || cols->tcp_reserved || cols->tcp_flags || cols->tcp_window ||
+                   cols->tcp_urgent_ptr || cols->icmp_sequence;
 
     // Kernel choice. Small: fixed stride, every frame 16-B aligned, at most 64 B,
     // inside the buffer (the 64-B configs). Otherwise rx_kernel with the tail
@@ -138,7 +150,7 @@ static int rx_common(pnetgpu_ctx* ctx, const pnetgpu_batch* b, const pnetgpu_rx_
                           last_end <= a.limit;
         // stream kernel (opt-in through PNETGPU_RX_KIND=4 until it beats the per-frame
         // kernels): contiguous frames >= 1 KiB apart with at most 1/8 of the span in gaps
-        stream_ok = !tx && fits && b->stride >= 1024 && b->stride <= (1u << 20) && b->frame_len <= b->stride &&
+        stream_ok = !tx && !a.field_cols && fits && b->stride >= 1024 && b->stride <= (1u << 20) && b->frame_len <= b->stride &&
                     b->frame_len >= 256 && (uint64_t)b->frame_len * 8 >= (uint64_t)b->stride * 7;
         if (base_sh == 0 && b->stride % 16 == 0 && b->frame_len <= 64 && fits && rxf == 0)
             kind = pnetgpu::kKindSmall;
@@ -173,7 +185,12 @@ static int rx_common(pnetgpu_ctx* ctx, const pnetgpu_batch* b, const pnetgpu_rx_
     const uint64_t want = (a.nruns + wpb - 1) / wpb;
     const uint64_t cap = (uint64_t)ctx->cus * (uint64_t)per_cu;
     const int blocks = (int)std::max<uint64_t>(1, std::min(want, cap));
-    if (pnetgpu::launch_rx(a, kind, blocks, tx, static_cast<hipStream_t>(stream)) != 0) return PNETGPU_EHIP;
+    if (const int e = pnetgpu::launch_rx(a, kind, blocks, tx, static_cast<hipStream_t>(stream))) {
+        pnetgpu::set_last_hip_error(e);
+        if (debug)
+            std::fprintf(stderr, "[pnetgpu] rx launch failed: %s (%d)\n", hipGetErrorString((hipError_t)e), e);
+        return PNETGPU_EHIP;
+    }
     return PNETGPU_OK;
 }
 
@@ -211,7 +228,10 @@ static int slices_common(pnetgpu_ctx* ctx, const uint8_t* data, uint64_t data_by
     const uint64_t groups_per_block = kBlock / 16;
     const uint64_t want = (n + groups_per_block - 1) / groups_per_block;
     const int blocks = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)ctx->cus * 8));
-    if (pnetgpu::launch_slices(a, pseudo, blocks, static_cast<hipStream_t>(stream)) != 0) return PNETGPU_EHIP;
+    if (const int e = pnetgpu::launch_slices(a, pseudo, blocks, static_cast<hipStream_t>(stream))) {
+        pnetgpu::set_last_hip_error(e);
+        return PNETGPU_EHIP;
+    }
     return PNETGPU_OK;
 }
 

@@ -18,9 +18,11 @@
 namespace {
 
 constexpr int kSlots = 3;          // filling, in flight, held by the application
-constexpr int kNumCols = 16;
-// element bytes of each pnetgpu_rx_columns column, in struct order
-constexpr uint32_t kColBytes[kNumCols] = {2, 2, 2, 2, 1, 1, 2, 2, 2, 2, 4, 4, 16, 16, 2, 1};
+constexpr int kNumCols = 38;       // the 16 record columns, then the 22 header-field columns (ABI v3)
+constexpr uint64_t kDefaultCols = 0xFFFFull;
+// element bytes of each pnetgpu_rx_columns column, in struct order (counters skipped)
+constexpr uint32_t kColBytes[kNumCols] = {2, 2, 2, 2, 1, 1, 2, 2, 2, 2, 4, 4, 16, 16, 2, 1,
+                                          8, 8, 1, 1, 1, 1, 2, 2, 1, 2, 1, 4, 2, 2, 4, 4, 1, 1, 1, 2, 2, 2};
 
 enum SlotState { kFree = 0, kFilling, kInFlight, kHeld };
 
@@ -49,7 +51,8 @@ struct Slot {
     uint64_t bytes = 0;
     uint64_t id = 0;
     const uint8_t* frames_view = nullptr;   // what the waited batch's `frames` points at
-    uint32_t col_mask = 0;                   // columns this batch computed
+    uint64_t col_mask = 0;                   // columns this batch computed
+    size_t rec_cap = 0;                      // bytes of d_rec / h_rec
     SlotState state = kFree;
 };
 
@@ -57,7 +60,14 @@ void** col_slot(pnetgpu_rx_columns& c, int k) {
     void** p[kNumCols] = {(void**)&c.status,    (void**)&c.ip_csum,   (void**)&c.l4_csum,   (void**)&c.ethertype,
                           (void**)&c.ip_proto,  (void**)&c.ttl,       (void**)&c.l4_offset, (void**)&c.l4_length,
                           (void**)&c.src_port,  (void**)&c.dst_port,  (void**)&c.src_ipv4,  (void**)&c.dst_ipv4,
-                          (void**)&c.src_ipv6,  (void**)&c.dst_ipv6,  (void**)&c.vlan_tci,  (void**)&c.l3_offset};
+                          (void**)&c.src_ipv6,  (void**)&c.dst_ipv6,  (void**)&c.vlan_tci,  (void**)&c.l3_offset,
+                          (void**)&c.eth_dst, (void**)&c.eth_src, (void**)&c.ip_version, (void**)&c.ip_header_length,
+                          (void**)&c.ip_dscp, (void**)&c.ip_ecn, (void**)&c.ip_total_length,
+                          (void**)&c.ip_identification, (void**)&c.ip_flags, (void**)&c.ip_fragment_offset,
+                          (void**)&c.ip6_traffic_class, (void**)&c.ip6_flow_label, (void**)&c.ip6_payload_length,
+                          (void**)&c.udp_length, (void**)&c.tcp_sequence, (void**)&c.tcp_acknowledgement,
+                          (void**)&c.tcp_data_offset, (void**)&c.tcp_reserved, (void**)&c.tcp_flags,
+                          (void**)&c.tcp_window, (void**)&c.tcp_urgent_ptr, (void**)&c.icmp_sequence};
     return p[k];
 }
 
@@ -69,7 +79,7 @@ struct pnetgpu_ring {
     uint64_t cap_bytes = 0;
     uint32_t cap_frames = 0;
     uint32_t flags = 0;
-    uint32_t col_mask = (1u << kNumCols) - 1;   // columns computed and copied back (bit k: struct order)
+    uint64_t col_mask = kDefaultCols;           // columns computed and copied back (bit k: struct order)
     Slot slots[kSlots];
     int filling = -1;
     int held = -1;
@@ -100,11 +110,24 @@ static void free_slot(Slot& s) {
 }
 
 // Bytes of the packed record block for up to n frames: the counters, then
-// every column, each start rounded up to 256 B.
-static size_t rec_capacity(uint64_t n) {
+// every selected column, each start rounded up to 256 B.
+static size_t rec_capacity(uint64_t n, uint64_t mask) {
     size_t b = 8ull * PNETGPU_NCOUNTERS;
-    for (int k = 0; k < kNumCols; ++k) b += 256 + (size_t)kColBytes[k] * n;
+    for (int k = 0; k < kNumCols; ++k)
+        if ((mask >> k) & 1u) b += 256 + (size_t)kColBytes[k] * n;
     return b;
+}
+
+static bool alloc_rec(Slot& s, size_t bytes) {
+    if (s.d_rec) (void)hipFree(s.d_rec);
+    if (s.h_rec) (void)hipHostFree(s.h_rec);
+    s.d_rec = s.h_rec = nullptr;
+    s.rec_cap = 0;
+    if (hipMalloc((void**)&s.d_rec, bytes) != hipSuccess ||
+        hipHostMalloc((void**)&s.h_rec, bytes, hipHostMallocDefault) != hipSuccess)
+        return false;
+    s.rec_cap = bytes;
+    return true;
 }
 
 static int take_free_slot(pnetgpu_ring* r) {
@@ -152,11 +175,7 @@ int pnetgpu_ring_create(pnetgpu_ctx* ctx, uint64_t batch_bytes, uint32_t batch_f
              hipMalloc((void**)&s.d_len, 4ull * batch_frames) == hipSuccess &&
              hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking) == hipSuccess &&
              hipEventCreateWithFlags(&s.done, hipEventDisableTiming) == hipSuccess;
-        if (ok) {
-            const size_t rb = rec_capacity(batch_frames);
-            ok = hipMalloc((void**)&s.d_rec, rb) == hipSuccess &&
-                 hipHostMalloc((void**)&s.h_rec, rb, hipHostMallocDefault) == hipSuccess;
-        }
+        if (ok) ok = alloc_rec(s, rec_capacity(batch_frames, kDefaultCols));
         if (ok) std::memset(s.h_frames + batch_bytes, 0, 32);
     }
     if (!ok) {
@@ -366,8 +385,18 @@ int pnetgpu_ring_wait(pnetgpu_ring* r, pnetgpu_ring_batch* out) {
     return PNETGPU_OK;
 }
 
-int pnetgpu_ring_set_columns(pnetgpu_ring* r, uint32_t column_mask) {
+int pnetgpu_ring_set_columns(pnetgpu_ring* r, uint64_t column_mask) {
     if (!r || (column_mask >> kNumCols)) return PNETGPU_EINVAL;
+    const size_t need = rec_capacity(r->cap_frames, column_mask);
+    bool grow = false;
+    for (const Slot& s : r->slots) grow = grow || s.rec_cap < need;
+    if (grow) {   // record blocks are resized only while no batch uses them
+        for (const Slot& s : r->slots)
+            if (s.state == kInFlight || s.state == kHeld) return PNETGPU_EBUSY;
+        if (hipSetDevice(r->device) != hipSuccess) return PNETGPU_EHIP;
+        for (Slot& s : r->slots)
+            if (s.rec_cap < need && !alloc_rec(s, need)) return PNETGPU_ENOMEM;
+    }
     r->col_mask = column_mask;
     return PNETGPU_OK;
 }

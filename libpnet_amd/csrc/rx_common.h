@@ -425,5 +425,66 @@ __device__ __forceinline__ void store_columns(const pnetgpu_rx_columns& C, uint6
     }
 }
 
+// Header-field columns (ABI v3): the remaining generated getters of the views
+// the dispatch constructed, read from the frame's bytes (LDS window, or HBM past
+// it) only for the columns a caller requested; 0 for a view that was not
+// reached. ethernet.rs:20-30, ipv4.rs:138-161, ipv6.rs:21-37, udp.rs:23-31,
+// tcp.rs:55-71, icmp.rs:221-232,303-314 (getter bit extraction:
+// pnet_macros/src/decorator.rs:1563-1670). Mirrors oracle_rx_frame_ex.
+// `l3mode`: PNETGPU_RX_L3 batch (no Ethernet view).
+__device__ __forceinline__ void store_field_columns(const pnetgpu_rx_columns& C, uint64_t i, const Parsed& P,
+                                                 const FrameBytes& F, bool l3mode) {
+    const uint32_t st = P.st;
+    const bool eth = !l3mode && !(st & (PNET_ST_ETH_MALFORMED | PNET_ST_DESC_INVALID));
+    const bool v4 = (st & (PNET_ST_L3_MASK | PNET_ST_L3_MALFORMED)) == PNET_ST_L3_IPV4;
+    const bool v6 = (st & (PNET_ST_L3_MASK | PNET_ST_L3_MALFORMED)) == PNET_ST_L3_IPV6;
+    const uint32_t l4kind = (st & (PNET_ST_L4_MALFORMED | PNET_ST_FRAGMENT)) ? 0u : (st & PNET_ST_L4_MASK);
+    const bool udp = l4kind == PNET_ST_L4_UDP, tcp = l4kind == PNET_ST_L4_TCP;
+    const bool echo = (l4kind == PNET_ST_L4_ICMP || l4kind == PNET_ST_L4_ICMPV6) && P.l4len >= 8u;
+    const int l3 = (int)P.l3, l4 = (int)P.l4off;
+    const uint32_t b0 = (v4 || v6) ? F.near8(l3) : 0u, b1 = (v4 || v6) ? F.near8(l3 + 1) : 0u;
+    if (C.eth_dst || C.eth_src) {
+        uint64_t d = 0, s = 0;
+        if (eth) {
+#pragma unroll
+            for (int k = 0; k < 6; ++k) {
+                d = (d << 8) | F.near8(k);
+                s = (s << 8) | F.near8(6 + k);
+            }
+        }
+        if (C.eth_dst) put<uint64_t>(C.eth_dst, i, d);
+        if (C.eth_src) put<uint64_t>(C.eth_src, i, s);
+    }
+    if (C.ip_version) put<uint8_t>(C.ip_version, i, (uint8_t)(b0 >> 4));                       // u4
+    if (C.ip_header_length) put<uint8_t>(C.ip_header_length, i, v4 ? (uint8_t)(b0 & 15u) : 0);  // u4
+    if (C.ip_dscp) put<uint8_t>(C.ip_dscp, i, v4 ? (uint8_t)(b1 >> 2) : 0);                     // u6
+    if (C.ip_ecn) put<uint8_t>(C.ip_ecn, i, v4 ? (uint8_t)(b1 & 3u) : 0);                       // u2
+    if (C.ip_total_length) put<uint16_t>(C.ip_total_length, i, v4 ? (uint16_t)F.near16(l3 + 2) : 0);
+    if (C.ip_identification) put<uint16_t>(C.ip_identification, i, v4 ? (uint16_t)F.near16(l3 + 4) : 0);
+    if (C.ip_flags) put<uint8_t>(C.ip_flags, i, v4 ? (uint8_t)(F.near8(l3 + 6) >> 5) : 0);     // u3
+    if (C.ip_fragment_offset)                                                                    // u13be
+        put<uint16_t>(C.ip_fragment_offset, i, v4 ? (uint16_t)(F.near16(l3 + 6) & 0x1FFFu) : 0);
+    if (C.ip6_traffic_class)                                                                     // u8 over the nibbles
+        put<uint8_t>(C.ip6_traffic_class, i, v6 ? (uint8_t)(((b0 & 15u) << 4) | (b1 >> 4)) : 0);
+    if (C.ip6_flow_label)                                                                        // u20be
+        put<uint32_t>(C.ip6_flow_label, i, v6 ? ((b1 & 15u) << 16) | F.near16(l3 + 2) : 0u);
+    if (C.ip6_payload_length) put<uint16_t>(C.ip6_payload_length, i, v6 ? (uint16_t)F.near16(l3 + 4) : 0);
+    // L4 views: an IPv6 extension chain may put them past the LDS window (far reads)
+    if (C.udp_length) put<uint16_t>(C.udp_length, i, udp ? (uint16_t)F.far16(l4 + 4) : 0);
+    if (C.tcp_sequence)
+        put<uint32_t>(C.tcp_sequence, i, tcp ? (F.far16(l4 + 4) << 16) | F.far16(l4 + 6) : 0u);
+    if (C.tcp_acknowledgement)
+        put<uint32_t>(C.tcp_acknowledgement, i, tcp ? (F.far16(l4 + 8) << 16) | F.far16(l4 + 10) : 0u);
+    if (C.tcp_data_offset || C.tcp_reserved || C.tcp_flags) {
+        const uint32_t x = tcp ? F.far16(l4 + 12) : 0u;                  // data_offset:4 reserved:4 flags:8
+        if (C.tcp_data_offset) put<uint8_t>(C.tcp_data_offset, i, (uint8_t)(x >> 12));
+        if (C.tcp_reserved) put<uint8_t>(C.tcp_reserved, i, (uint8_t)((x >> 8) & 15u));
+        if (C.tcp_flags) put<uint8_t>(C.tcp_flags, i, (uint8_t)x);
+    }
+    if (C.tcp_window) put<uint16_t>(C.tcp_window, i, tcp ? (uint16_t)F.far16(l4 + 14) : 0);
+    if (C.tcp_urgent_ptr) put<uint16_t>(C.tcp_urgent_ptr, i, tcp ? (uint16_t)F.far16(l4 + 18) : 0);
+    if (C.icmp_sequence) put<uint16_t>(C.icmp_sequence, i, echo ? (uint16_t)F.far16(l4 + 6) : 0);
+}
+
 }  // namespace
 }  // namespace pnetgpu

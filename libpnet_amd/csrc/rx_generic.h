@@ -270,6 +270,8 @@ __global__ __launch_bounds__(kBlock, 4) void rx_kernel(RxArgs a) {
         finalize(P, tA, tB, (off & 1) != 0, ipc, l4c);
         if (TX && in_batch && !desc_bad) tx_write(const_cast<uint8_t*>(a.data) + off, P, ipc, l4c);
         store_columns(a.cols, f0, lane, in_batch, P, ipc, l4c, slot, sh);
+        if (a.field_cols && in_batch)
+            store_field_columns(a.cols, f0 + lane, P, FrameBytes{slot + sh, a.data + off, kWin - sh}, EXT && a.l3mode);
         if (a.cols.counters) K.add(in_batch && !desc_bad, len, P.st);
         wave_sync();   // slots and lists are rewritten by the next run
     }

@@ -22,6 +22,8 @@ struct RxArgs {
     uint64_t nruns;          // ceil(n / 64): one wave per run of 64 frames
     uint32_t flags;          // PNETGPU_RX_* (the small kernel requires 0)
     uint32_t desc_compact;   // offsets/lengths are uint32_t/uint16_t arrays (PNETGPU_DESC_COMPACT)
+    uint32_t field_cols;     // any ABI-v3 header-field column requested (store_field_columns)
+    uint32_t l3mode;         // PNETGPU_RX_L3: frames start at the IP header (no Ethernet view)
     pnetgpu_rx_columns cols;
 };
 
@@ -55,7 +57,12 @@ int ctx_device(const pnetgpu_ctx* ctx);
 
 int rx_blocks_per_cu(int kind, bool ext, int* numregs, int* lds);
 int rx_waves_per_block(int kind);
+// both return the hipError_t of the launch (0 = hipSuccess); errors pending
+// from earlier, unrelated HIP calls are cleared first
 int launch_rx(const RxArgs& args, int kind, int blocks, bool tx, hipStream_t stream);
 int launch_slices(const SliceArgs& args, int pseudo, int blocks, hipStream_t stream);
+// the HIP error code behind the last PNETGPU_EHIP a launch returned on this thread
+int last_hip_error();
+void set_last_hip_error(int e);
 
 }  // namespace pnetgpu

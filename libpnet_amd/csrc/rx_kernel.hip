@@ -159,19 +159,21 @@ int rx_waves_per_block(int kind) { return kind == kKindStream ? 1 : kWavesPerBlo
 
 int launch_rx(const RxArgs& args, int kind, int blocks, bool tx, hipStream_t stream) {
     const bool ext = args.flags != 0;
+    (void)hipGetLastError();   // a stale error of an unrelated earlier call is not this launch's
     if (tx) ext ? launch_t<true, true>(args, kind, blocks, stream) : launch_t<false, true>(args, kind, blocks, stream);
     else ext ? launch_t<true, false>(args, kind, blocks, stream) : launch_t<false, false>(args, kind, blocks, stream);
-    return hipGetLastError() == hipSuccess ? 0 : -1;
+    return (int)hipGetLastError();
 }
 
 int launch_slices(const SliceArgs& args, int pseudo, int blocks, hipStream_t stream) {
     const bool extra = args.extra_offsets != nullptr;
+    (void)hipGetLastError();
     if (pseudo == 0) hipLaunchKernelGGL((slice_kernel<0, false>), dim3(blocks), dim3(kBlock), 0, stream, args);
     else if (pseudo == 4 && !extra) hipLaunchKernelGGL((slice_kernel<4, false>), dim3(blocks), dim3(kBlock), 0, stream, args);
     else if (pseudo == 4) hipLaunchKernelGGL((slice_kernel<4, true>), dim3(blocks), dim3(kBlock), 0, stream, args);
     else if (!extra) hipLaunchKernelGGL((slice_kernel<16, false>), dim3(blocks), dim3(kBlock), 0, stream, args);
     else hipLaunchKernelGGL((slice_kernel<16, true>), dim3(blocks), dim3(kBlock), 0, stream, args);
-    return hipGetLastError() == hipSuccess ? 0 : -1;
+    return (int)hipGetLastError();
 }
 
 }  // namespace pnetgpu

@@ -228,6 +228,7 @@ __global__ __launch_bounds__(kBlock, PNET_SMALL_WAVES) void rx_small_kernel(RxAr
             }
         }
         store_columns(a.cols, f0, lane, in_batch, P, ipc, l4c, slot, 0);
+        if (a.field_cols && in_batch) store_field_columns(a.cols, f0 + lane, P, FrameBytes{slot, slot, 64}, false);
         if (a.cols.counters) K.add(in_batch, len, P.st);
         wave_sync();
 #ifndef PNET_SMALL_NOPF

@@ -21,7 +21,7 @@ from contextlib import nullcontext as _nullcontext
 import numpy as np
 import torch
 
-from ._lib import COLUMN_NAMES, DEFS, Batch, RxColumns, check, lib
+from ._lib import ALL_COLUMN_NAMES, COLUMN_NAMES, DEFS, FIELD_COLUMN_NAMES, Batch, RxColumns, check, lib
 
 # column -> (torch storage dtype, numpy view dtype, trailing shape)
 COLUMNS = {
@@ -41,15 +41,43 @@ COLUMNS = {
     "dst_ipv6": (torch.uint8, np.uint8, (16,)),
     "vlan_tci": (torch.int16, np.uint16, ()),
     "l3_offset": (torch.uint8, np.uint8, ()),
+    # header-field columns (ABI v3): the remaining generated getters
+    "eth_dst": (torch.int64, np.uint64, ()),
+    "eth_src": (torch.int64, np.uint64, ()),
+    "ip_version": (torch.uint8, np.uint8, ()),
+    "ip_header_length": (torch.uint8, np.uint8, ()),
+    "ip_dscp": (torch.uint8, np.uint8, ()),
+    "ip_ecn": (torch.uint8, np.uint8, ()),
+    "ip_total_length": (torch.int16, np.uint16, ()),
+    "ip_identification": (torch.int16, np.uint16, ()),
+    "ip_flags": (torch.uint8, np.uint8, ()),
+    "ip_fragment_offset": (torch.int16, np.uint16, ()),
+    "ip6_traffic_class": (torch.uint8, np.uint8, ()),
+    "ip6_flow_label": (torch.int32, np.uint32, ()),
+    "ip6_payload_length": (torch.int16, np.uint16, ()),
+    "udp_length": (torch.int16, np.uint16, ()),
+    "tcp_sequence": (torch.int32, np.uint32, ()),
+    "tcp_acknowledgement": (torch.int32, np.uint32, ()),
+    "tcp_data_offset": (torch.uint8, np.uint8, ()),
+    "tcp_reserved": (torch.uint8, np.uint8, ()),
+    "tcp_flags": (torch.uint8, np.uint8, ()),
+    "tcp_window": (torch.int16, np.uint16, ()),
+    "tcp_urgent_ptr": (torch.int16, np.uint16, ()),
+    "icmp_sequence": (torch.int16, np.uint16, ()),
 }
-assert tuple(COLUMNS) == COLUMN_NAMES
+assert tuple(COLUMNS) == ALL_COLUMN_NAMES
 
 #: every IPv4-relevant column: the bench's "checksum verify + header extract" record
 IPV4_COLUMNS = ("status", "ip_csum", "l4_csum", "ethertype", "ip_proto", "ttl", "l4_offset", "l4_length",
                 "src_port", "dst_port", "src_ipv4", "dst_ipv4")
 RX_VLAN, RX_IPV6_EXT, RX_L3 = DEFS["PNETGPU_RX_VLAN"], DEFS["PNETGPU_RX_IPV6_EXT"], DEFS["PNETGPU_RX_L3"]
 DESC_COMPACT = DEFS["PNETGPU_DESC_COMPACT"]
-ALL_COLUMNS = COLUMN_NAMES
+#: every column: the record columns and the ABI-v3 header-field getters
+ALL_COLUMNS = ALL_COLUMN_NAMES
+#: the record columns of ABI v2 (status, checksums, dispatch fields, addresses, VLAN, L3 offset)
+RECORD_COLUMNS = COLUMN_NAMES
+#: the header-field getter columns (eth MACs, IPv4/IPv6 header fields, UDP length, TCP header, ICMP echo sequence)
+FIELD_COLUMNS = FIELD_COLUMN_NAMES
 NCOUNTERS = DEFS["PNETGPU_NCOUNTERS"]
 COUNTER_NAMES = ("frames", "bytes", "ipv4", "ipv6", "ip_csum_bad", "l4_csum_bad", "malformed", "unknown")
 
@@ -138,7 +166,7 @@ class RxResult:
 
     def c_struct(self):
         cols = RxColumns()
-        for c in COLUMN_NAMES:
+        for c in ALL_COLUMN_NAMES:
             setattr(cols, c, self.columns[c].data_ptr() if c in self.columns else 0)
         cols.counters = self.counters.data_ptr() if self.counters is not None else 0
         return cols
@@ -202,17 +230,24 @@ def _rx_or_tx(fn_name, data, n_frames, stride, frame_len, first_offset, offsets,
     else:
         if offsets is None or lengths is None:
             raise ValueError("descriptor mode needs offsets and lengths")
+        for t, what in ((offsets, "offsets"), (lengths, "lengths")):
+            if not (isinstance(t, torch.Tensor) and t.is_cuda and t.device == data.device and t.is_contiguous()):
+                raise TypeError(f"{what} must be a contiguous CUDA tensor on {data.device}")
+        if flags & DESC_COMPACT:
+            if offsets.dtype not in (torch.int32, torch.uint32) or lengths.dtype not in (torch.int16, torch.uint16):
+                raise TypeError("DESC_COMPACT: offsets must be 32-bit and lengths 16-bit CUDA tensors")
+        elif offsets.dtype != torch.int64 or lengths.dtype != torch.int32:
+            raise TypeError("offsets must be int64 and lengths int32 CUDA tensors")
         if n_frames is None:
             n_frames = offsets.numel()
-        if flags & DESC_COMPACT:
-            if (offsets.dtype not in (torch.int32, torch.uint32) or lengths.dtype not in (torch.int16, torch.uint16)
-                    or not offsets.is_cuda):
-                raise TypeError("DESC_COMPACT: offsets must be 32-bit and lengths 16-bit CUDA tensors")
-        elif offsets.dtype != torch.int64 or lengths.dtype != torch.int32 or not offsets.is_cuda:
-            raise TypeError("offsets must be int64 and lengths int32 CUDA tensors")
+        if not 0 <= n_frames <= min(offsets.numel(), lengths.numel()):
+            raise ValueError(f"n_frames={n_frames} exceeds the descriptors ({offsets.numel()} offsets, "
+                             f"{lengths.numel()} lengths)")
         frame_len = 0
     if out is None:
         out = RxResult(n_frames, data.device, columns, counters)
+    elif out.n < n_frames:
+        raise ValueError(f"out holds {out.n} frames, the batch has {n_frames}")
     b = Batch(data.data_ptr(), data.numel() if data_bytes is None else data_bytes, n_frames, first_offset,
               stride, frame_len, offsets.data_ptr() if offsets is not None else 0,
               lengths.data_ptr() if lengths is not None else 0, flags, 0)

@@ -10,7 +10,7 @@ import ctypes
 
 import numpy as np
 
-from ._lib import COLUMN_NAMES, DEFS, RxColumns, check, lib
+from ._lib import ALL_COLUMN_NAMES, DEFS, RxColumns, check, lib
 from .engine import COLUMNS, COUNTER_NAMES, context
 
 EFULL, EBUSY, EEMPTY = DEFS["PNETGPU_EFULL"], DEFS["PNETGPU_EBUSY"], DEFS["PNETGPU_EEMPTY"]
@@ -42,7 +42,7 @@ def _setup():
     lib.pnetgpu_pcap_close.restype = None
     lib.pnetgpu_pcap_close.argtypes = [vp]
     lib.pnetgpu_ring_set_columns.restype = i32
-    lib.pnetgpu_ring_set_columns.argtypes = [vp, u32]
+    lib.pnetgpu_ring_set_columns.argtypes = [vp, u64]
     lib.pnetgpu_ring_submit_region.restype = i32
     lib.pnetgpu_ring_submit_region.argtypes = [vp, vp, vp, vp, u64, ctypes.POINTER(u64), ctypes.POINTER(u64)]
     lib.pnetgpu_host_register.restype = i32
@@ -101,7 +101,7 @@ class Ring:
         if columns is not None:
             mask = 0
             for c in columns:
-                mask |= 1 << COLUMN_NAMES.index(c)
+                mask |= 1 << ALL_COLUMN_NAMES.index(c)
             check(lib.pnetgpu_ring_set_columns(self.h, mask), "pnetgpu_ring_set_columns")
 
     def close(self):

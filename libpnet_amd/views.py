@@ -24,9 +24,13 @@ _L4 = {ST["L4_UDP"]: "udp", ST["L4_TCP"]: "tcp", ST["L4_ICMP"]: "icmp", ST["L4_I
 _L4_HEADER = {"udp": 8, "tcp": 20, "icmp": 4, "icmpv6": 4}   # payload() starts after the fixed header
 
 
-def _field(records, name, i):
+def _has(records, name):
     names = getattr(getattr(records, "dtype", None), "names", None)      # a structured record array
-    if name not in (names if names is not None else records):
+    return name in (names if names is not None else records)
+
+
+def _field(records, name, i):
+    if not _has(records, name):
         raise KeyError(f"the batch was processed without the '{name}' column")
     return records[name][i]
 
@@ -49,7 +53,8 @@ class L4View:
         """Bytes after the fixed header (UDP 8, TCP 20 + options, ICMP 4)."""
         p = self.packet()
         if self.kind == "tcp":
-            do = p[12] >> 4
+            # the GPU's tcp_data_offset column when the batch computed it
+            do = int(self._rec("tcp_data_offset")) if _has(self._r, "tcp_data_offset") else p[12] >> 4
             start = 20 + (do * 4 - 20 if do > 5 else 0)             # tcp.rs:227-236
             return p[start:] if len(p) > start else p[0:0]
         return p[_L4_HEADER[self.kind]:]
@@ -60,6 +65,42 @@ class L4View:
 
     def get_destination(self):
         return int(self._rec("dst_port"))
+
+    # ---- header-field columns (ABI v3; KeyError if the batch did not compute them)
+    def get_length(self):
+        """UdpPacket::get_length (udp.rs:27)."""
+        return int(self._rec("udp_length"))
+
+    def get_sequence(self):
+        """TcpPacket::get_sequence (tcp.rs:59)."""
+        return int(self._rec("tcp_sequence"))
+
+    def get_acknowledgement(self):
+        return int(self._rec("tcp_acknowledgement"))
+
+    def get_data_offset(self):
+        return int(self._rec("tcp_data_offset"))
+
+    def get_reserved(self):
+        return int(self._rec("tcp_reserved"))
+
+    def get_flags(self):
+        """TcpPacket::get_flags (tcp.rs:63)."""
+        return int(self._rec("tcp_flags"))
+
+    def get_window(self):
+        return int(self._rec("tcp_window"))
+
+    def get_urgent_ptr(self):
+        return int(self._rec("tcp_urgent_ptr"))
+
+    def get_identifier(self):
+        """EchoRequest/EchoReply get_identifier (icmp.rs:228,310): the slice's BE16 at +4."""
+        return int(self._rec("dst_port"))
+
+    def get_sequence_number(self):
+        """EchoRequest/EchoReply get_sequence_number (icmp.rs:229,311)."""
+        return int(self._rec("icmp_sequence"))
 
     def get_icmp_type(self):
         return int(self._rec("src_port")) >> 8
@@ -114,6 +155,43 @@ class IpView:
 
     get_hop_limit = get_ttl
 
+    # ---- header-field columns (ABI v3; KeyError if the batch did not compute them)
+    def get_version(self):
+        return int(self._rec("ip_version"))
+
+    def get_header_length(self):
+        """Ipv4 IHL (ipv4.rs:141)."""
+        return int(self._rec("ip_header_length"))
+
+    def get_dscp(self):
+        return int(self._rec("ip_dscp"))
+
+    def get_ecn(self):
+        return int(self._rec("ip_ecn"))
+
+    def get_total_length(self):
+        return int(self._rec("ip_total_length"))
+
+    def get_identification(self):
+        return int(self._rec("ip_identification"))
+
+    def get_flags(self):
+        """Ipv4 flags (u3, ipv4.rs:146)."""
+        return int(self._rec("ip_flags"))
+
+    def get_fragment_offset(self):
+        return int(self._rec("ip_fragment_offset"))
+
+    def get_traffic_class(self):
+        """Ipv6 traffic_class (ipv6.rs:24)."""
+        return int(self._rec("ip6_traffic_class"))
+
+    def get_flow_label(self):
+        return int(self._rec("ip6_flow_label"))
+
+    def get_payload_length(self):
+        return int(self._rec("ip6_payload_length"))
+
     def computed_checksum(self):
         """ipv4::checksum(&ip) (IPv4 only)."""
         return int(self._rec("ip_csum")) if self.version == 4 else None
@@ -162,11 +240,19 @@ class FrameView:
         """The inner ethertype past any VLAN tags the batch peeled."""
         return int(self._rec("ethertype"))
 
+    def _mac(self, col, at):
+        # the GPU's eth_dst / eth_src column (BE-valued u48) when the batch
+        # computed it, else the fixed-offset bytes (ethernet.rs:23,25)
+        if _has(self._r, col):
+            return int(self._rec(col)).to_bytes(6, "big")
+        return bytes(self._f[at:at + 6])
+
     def get_destination(self):
-        return bytes(self._f[0:6])
+        """MacAddr octets (6 bytes)."""
+        return self._mac("eth_dst", 0)
 
     def get_source(self):
-        return bytes(self._f[6:12])
+        return self._mac("eth_src", 6)
 
     def _ip(self, bit, version):
         st = int(self._rec("status"))

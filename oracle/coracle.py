@@ -19,6 +19,14 @@ REC_DTYPE = np.dtype([
     ("src_ipv4", "<u4"), ("dst_ipv4", "<u4"),
     ("src_ipv6", "u1", (16,)), ("dst_ipv6", "u1", (16,)),
     ("vlan_tci", "<u2"), ("l3_offset", "u1"), ("_pad2", "u1"),
+    ("eth_dst", "<u8"), ("eth_src", "<u8"),
+    ("tcp_sequence", "<u4"), ("tcp_acknowledgement", "<u4"), ("ip6_flow_label", "<u4"),
+    ("ip_total_length", "<u2"), ("ip_identification", "<u2"), ("ip_fragment_offset", "<u2"),
+    ("ip6_payload_length", "<u2"), ("udp_length", "<u2"), ("tcp_window", "<u2"), ("tcp_urgent_ptr", "<u2"),
+    ("icmp_sequence", "<u2"),
+    ("ip_version", "u1"), ("ip_header_length", "u1"), ("ip_dscp", "u1"), ("ip_ecn", "u1"), ("ip_flags", "u1"),
+    ("ip6_traffic_class", "u1"), ("tcp_data_offset", "u1"), ("tcp_reserved", "u1"), ("tcp_flags", "u1"),
+    ("_pad3", "u1", (3,)),
 ], align=True)
 
 RX_VLAN, RX_IPV6_EXT, RX_L3 = 0x1, 0x2, 0x4

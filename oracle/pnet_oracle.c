@@ -112,6 +112,7 @@ static void l4_dispatch(oracle_rec* r, int is_v6, uint8_t proto, slice_t l4,
         if (l4.len < 8) { r->status |= ORACLE_ST_L4_MALFORMED; return; }  /* UdpPacket::new */
         r->src_port = be16(l4.p + 0);
         r->dst_port = be16(l4.p + 2);
+        r->udp_length = be16(l4.p + 4);                   /* udp.rs:27 length: u16be */
         r->l4_csum = is_v6 ? oracle_ipv6_checksum(l4.p, l4.len, 3, NULL, 0, src, dst, 17)
                            : oracle_ipv4_checksum(l4.p, l4.len, 3, NULL, 0, src, dst, 17);
         r->status |= ORACLE_ST_L4_CSUM_DONE;
@@ -122,6 +123,13 @@ static void l4_dispatch(oracle_rec* r, int is_v6, uint8_t proto, slice_t l4,
         if (l4.len < 20) { r->status |= ORACLE_ST_L4_MALFORMED; return; }  /* TcpPacket::new */
         r->src_port = be16(l4.p + 0);
         r->dst_port = be16(l4.p + 2);
+        r->tcp_sequence = be32(l4.p + 4);                 /* tcp.rs:59 sequence: u32be        */
+        r->tcp_acknowledgement = be32(l4.p + 8);          /* tcp.rs:60 acknowledgement: u32be */
+        r->tcp_data_offset = l4.p[12] >> 4;               /* tcp.rs:61 data_offset: u4 (high) */
+        r->tcp_reserved = l4.p[12] & 0x0F;                /* tcp.rs:62 reserved: u4 (low)     */
+        r->tcp_flags = l4.p[13];                          /* tcp.rs:63 flags: u8              */
+        r->tcp_window = be16(l4.p + 14);                  /* tcp.rs:64 window: u16be          */
+        r->tcp_urgent_ptr = be16(l4.p + 18);              /* tcp.rs:66 urgent_ptr: u16be      */
         r->l4_csum = is_v6 ? oracle_ipv6_checksum(l4.p, l4.len, 8, NULL, 0, src, dst, 6)
                            : oracle_ipv4_checksum(l4.p, l4.len, 8, NULL, 0, src, dst, 6);
         r->status |= ORACLE_ST_L4_CSUM_DONE;
@@ -132,6 +140,7 @@ static void l4_dispatch(oracle_rec* r, int is_v6, uint8_t proto, slice_t l4,
         if (l4.len < 4) { r->status |= ORACLE_ST_L4_MALFORMED; return; }   /* IcmpPacket::new */
         r->src_port = be16(l4.p + 0);                     /* icmp_type << 8 | icmp_code */
         r->dst_port = l4.len >= 8 ? be16(l4.p + 4) : 0;   /* echo identifier, icmp.rs:221-232 */
+        r->icmp_sequence = l4.len >= 8 ? be16(l4.p + 6) : 0;   /* sequence_number, icmp.rs:229/311 */
         r->l4_csum = oracle_checksum(l4.p, l4.len, 1);
         r->status |= ORACLE_ST_L4_CSUM_DONE;
         if (r->l4_csum == be16(l4.p + 2)) r->status |= ORACLE_ST_L4_CSUM_OK;
@@ -141,6 +150,7 @@ static void l4_dispatch(oracle_rec* r, int is_v6, uint8_t proto, slice_t l4,
         if (l4.len < 4) { r->status |= ORACLE_ST_L4_MALFORMED; return; }   /* Icmpv6Packet::new */
         r->src_port = be16(l4.p + 0);
         r->dst_port = l4.len >= 8 ? be16(l4.p + 4) : 0;
+        r->icmp_sequence = l4.len >= 8 ? be16(l4.p + 6) : 0;   /* echo views, icmpv6.rs */
         if (is_v6) { /* icmpv6::checksum needs IPv6 addresses; none exists over IPv4 */
             r->l4_csum = oracle_ipv6_checksum(l4.p, l4.len, 1, NULL, 0, src, dst, 58);
             r->status |= ORACLE_ST_L4_CSUM_DONE;
@@ -159,6 +169,14 @@ static void handle_ipv4(oracle_rec* r, slice_t ep, size_t l3) {
     if (ep.len < 20) { r->status |= ORACLE_ST_L3_MALFORMED; return; }  /* Ipv4Packet::new, min 20 */
     const uint8_t* ip = ep.p;
     unsigned ihl = ip[0] & 0x0F;                          /* header_length: u4 */
+    r->ip_version = ip[0] >> 4;                           /* ipv4.rs:140 version: u4 (high)  */
+    r->ip_header_length = (uint8_t)ihl;                   /* ipv4.rs:141                     */
+    r->ip_dscp = ip[1] >> 2;                              /* ipv4.rs:142 dscp: u6 (high)     */
+    r->ip_ecn = ip[1] & 0x03;                             /* ipv4.rs:143 ecn: u2 (low)       */
+    r->ip_total_length = be16(ip + 2);                    /* ipv4.rs:144                     */
+    r->ip_identification = be16(ip + 4);                  /* ipv4.rs:145                     */
+    r->ip_flags = ip[6] >> 5;                             /* ipv4.rs:146 flags: u3 (high)    */
+    r->ip_fragment_offset = be16(ip + 6) & 0x1FFF;        /* ipv4.rs:147 u13be (low 13 bits) */
     /* ipv4.rs:165-178: clamp IHL*4 to [minimum_packet_size, packet().len()] */
     size_t hl = (size_t)ihl * 4;
     if (hl < 20) hl = 20;
@@ -203,6 +221,10 @@ static void handle_ipv6(oracle_rec* r, slice_t ep, size_t l3, uint32_t flags) {
     r->status |= ORACLE_ST_L3_IPV6;
     if (ep.len < 40) { r->status |= ORACLE_ST_L3_MALFORMED; return; }  /* Ipv6Packet::new, min 40 */
     const uint8_t* ip = ep.p;
+    r->ip_version = ip[0] >> 4;                           /* ipv6.rs:23 version: u4            */
+    r->ip6_traffic_class = (uint8_t)(((ip[0] & 0x0F) << 4) | (ip[1] >> 4));   /* ipv6.rs:24 */
+    r->ip6_flow_label = ((uint32_t)(ip[1] & 0x0F) << 16) | be16(ip + 2);    /* ipv6.rs:25 u20be */
+    r->ip6_payload_length = be16(ip + 4);                 /* ipv6.rs:26                        */
     r->ip_proto = ip[6];                                  /* next_header */
     r->ttl = ip[7];                                       /* hop_limit */
     memcpy(r->src_ipv6, ip + 8, 16);
@@ -276,6 +298,10 @@ void oracle_rx_frame_ex(const uint8_t* frame, size_t len, uint32_t flags, oracle
         l3 = 0;
     } else {
         if (len < 14) { r->status = ORACLE_ST_ETH_MALFORMED; return; }  /* EthernetPacket::new, min 14 */
+        for (int k = 0; k < 6; ++k) {                     /* ethernet.rs:23,25 MacAddr(u8 x 6) */
+            r->eth_dst = (r->eth_dst << 8) | frame[k];
+            r->eth_src = (r->eth_src << 8) | frame[6 + k];
+        }
         et = be16(frame + 12);                            /* ethernet.rs:27-28 */
         l3 = 14;
     }

@@ -81,6 +81,30 @@ typedef struct oracle_rec {
     uint16_t vlan_tci;    /* outer VLAN tag control information (RX_VLAN)   */
     uint8_t  l3_offset;   /* frame offset of the IP header                 */
     uint8_t  _pad;
+    /* header-field getters (0 unless the dispatch constructed that view) */
+    uint64_t eth_dst;             /* ethernet.rs:23 MacAddr octets, BE-valued u48 */
+    uint64_t eth_src;             /* ethernet.rs:25                             */
+    uint32_t tcp_sequence;        /* tcp.rs:59                                  */
+    uint32_t tcp_acknowledgement; /* tcp.rs:60                                  */
+    uint32_t ip6_flow_label;      /* ipv6.rs:25 u20be                           */
+    uint16_t ip_total_length;     /* ipv4.rs:144                                */
+    uint16_t ip_identification;   /* ipv4.rs:145                                */
+    uint16_t ip_fragment_offset;  /* ipv4.rs:147 u13be                          */
+    uint16_t ip6_payload_length;  /* ipv6.rs:26                                 */
+    uint16_t udp_length;          /* udp.rs:27                                  */
+    uint16_t tcp_window;          /* tcp.rs:64                                  */
+    uint16_t tcp_urgent_ptr;      /* tcp.rs:66                                  */
+    uint16_t icmp_sequence;       /* icmp.rs:229/311 echo views (slice >= 8 B)  */
+    uint8_t  ip_version;          /* ipv4.rs:140 / ipv6.rs:23 u4                */
+    uint8_t  ip_header_length;    /* ipv4.rs:141 u4                             */
+    uint8_t  ip_dscp;             /* ipv4.rs:142 u6                             */
+    uint8_t  ip_ecn;              /* ipv4.rs:143 u2                             */
+    uint8_t  ip_flags;            /* ipv4.rs:146 u3                             */
+    uint8_t  ip6_traffic_class;   /* ipv6.rs:24 u8 (across the nibbles)         */
+    uint8_t  tcp_data_offset;     /* tcp.rs:61 u4                               */
+    uint8_t  tcp_reserved;        /* tcp.rs:62 u4                               */
+    uint8_t  tcp_flags;           /* tcp.rs:63 u8                               */
+    uint8_t  _pad3[3];
 } oracle_rec;
 
 /* util.rs:158-181 */

@@ -30,9 +30,42 @@ ST_FRAGMENT = 0x4000
 ST_DESC_INVALID = 0x8000
 RX_VLAN, RX_IPV6_EXT, RX_L3 = 0x1, 0x2, 0x4
 
+# Header-field getters, restated from the #[packet] declarations: each layout
+# lists (getter, bit width) in declaration order, and a generated getter reads
+# its width of bits at the running bit offset, most significant bit first
+# (pnet_macros/src/decorator.rs:1563-1670). Names starting with "_" are fields
+# this record does not keep (or keeps under a dispatch name).
+ETHERNET = (("eth_dst", 48), ("eth_src", 48), ("_ethertype", 16))                        # ethernet.rs:20-30
+IPV4 = (("ip_version", 4), ("ip_header_length", 4), ("ip_dscp", 6), ("ip_ecn", 2),       # ipv4.rs:138-161
+        ("ip_total_length", 16), ("ip_identification", 16), ("ip_flags", 3), ("ip_fragment_offset", 13))
+IPV6 = (("ip_version", 4), ("ip6_traffic_class", 8), ("ip6_flow_label", 20),             # ipv6.rs:21-37
+        ("ip6_payload_length", 16))
+UDP = (("_source", 16), ("_destination", 16), ("udp_length", 16))                        # udp.rs:23-31
+TCP = (("_source", 16), ("_destination", 16), ("tcp_sequence", 32), ("tcp_acknowledgement", 32),  # tcp.rs:55-71
+       ("tcp_data_offset", 4), ("tcp_reserved", 4), ("tcp_flags", 8), ("tcp_window", 16), ("_checksum", 16),
+       ("tcp_urgent_ptr", 16))
+ECHO = (("_icmp_type", 8), ("_icmp_code", 8), ("_checksum", 16), ("_identifier", 16),     # icmp.rs:221-232
+        ("icmp_sequence", 16))
+
+HEADER_FIELDS = tuple(dict.fromkeys(n for lay in (ETHERNET, IPV4, IPV6, UDP, TCP, ECHO) for n, _ in lay
+                                    if not n.startswith("_")))
+
 FIELDS = ("status", "ip_csum", "l4_csum", "ethertype", "ip_proto", "ttl", "l4_offset",
           "l4_length", "src_port", "dst_port", "src_ipv4", "dst_ipv4", "src_ipv6", "dst_ipv6",
-          "vlan_tci", "l3_offset")
+          "vlan_tci", "l3_offset") + HEADER_FIELDS
+
+
+def getters(buf, layout):
+    """Values of a view's generated getters over the first bytes of buf."""
+    bits = sum(w for _, w in layout)
+    nbytes = (bits + 7) // 8
+    v = int.from_bytes(bytes(buf[:nbytes]), "big")
+    out, at = {}, 0
+    for name, w in layout:
+        if not name.startswith("_"):
+            out[name] = (v >> (8 * nbytes - at - w)) & ((1 << w) - 1)
+        at += w
+    return out
 
 
 def sum_be_words(d, skip):
@@ -90,6 +123,7 @@ def rx_frame(frame, flags=0):
             return r
         et = _be16(f, 12)
         l3 = 14
+        r.update(getters(f, ETHERNET))
     if flags & RX_VLAN and not flags & RX_L3:   # vlan.rs:62-72; TPIDs ethernet.rs:102,104,112
         for k in range(2):
             if et not in (0x8100, 0x88A8, 0x9100):
@@ -110,6 +144,7 @@ def rx_frame(frame, flags=0):
         if len(ep) < 20:
             r["status"] = st | ST_L3_MALFORMED
             return r
+        r.update(getters(ep, IPV4))
         ihl = ep[0] & 15
         hl = min(max(ihl * 4, 20), len(ep))
         r["ip_csum"] = checksum(ep[:hl], 5)
@@ -130,6 +165,7 @@ def rx_frame(frame, flags=0):
         if len(ep) < 40:
             r["status"] = st | ST_L3_MALFORMED
             return r
+        r.update(getters(ep, IPV6))
         r["ip_proto"], r["ttl"] = ep[6], ep[7]
         r["src_ipv6"], r["dst_ipv6"] = ep[8:24], ep[24:40]
         pl = ep[40:min(40 + _be16(ep, 4), len(ep))] if len(ep) > 40 else b""
@@ -177,8 +213,11 @@ def rx_frame(frame, flags=0):
     r["src_port"] = _be16(l4, 0)
     if proto in (17, 6):
         r["dst_port"] = _be16(l4, 2)
+        r.update(getters(l4, UDP if proto == 17 else TCP))
     else:
         r["dst_port"] = _be16(l4, 4) if len(l4) >= 8 else 0
+        if len(l4) >= 8:                     # EchoRequest/EchoReply view (minimum 8 bytes)
+            r.update(getters(l4, ECHO))
     c = None
     if proto == 1:
         c = checksum(l4, 1)

@@ -153,6 +153,31 @@ def main():
     v.append(kat("tcp_payload_invalid_offset", "tcp_payload_len", "pnet_packet/src/tcp.rs:421-433",
                  0, data=t20))
 
+    # ---- header-field getters: the values the reference's tests assert after
+    # their setter calls, over the bytes the same tests assert were written ----
+    v.append(kat("ethernet_getters", "getters", "pnet_packet/src/ethernet.rs:33-54",
+                 {"eth_dst": 0xDEF012344567, "eth_src": 0x123456789ABC}, view="ethernet", data=eth))
+    v.append(kat("ipv4_getters", "getters", "pnet_packet/src/ipv4.rs:292-357",
+                 {"ip_version": 4, "ip_header_length": 5, "ip_dscp": 4, "ip_ecn": 1, "ip_total_length": 115,
+                  "ip_identification": 257, "ip_flags": 2, "ip_fragment_offset": 257, "ttl": 64, "ip_proto": 17},
+                 view="ipv4", data=hdr))
+    ip6h = bytes([0x61, 0x11, 0x01, 0x01, 0x01, 0x01, 0x00, 0x01]) + bytes([0x01, 0x10, 0x10, 0x01] * 8)
+    v.append(kat("ipv6_getters", "getters", "pnet_packet/src/ipv6.rs:147-180,270-290",
+                 {"ip_version": 6, "ip6_traffic_class": 17, "ip6_flow_label": 0x10101,
+                  "ip6_payload_length": 0x0101, "ttl": 1, "ip_proto": 0}, view="ipv6", data=ip6h))
+    v.append(kat("udp_getters", "getters", "pnet_packet/src/udp.rs:59-100",
+                 {"src_port": 12345, "dst_port": 54321, "udp_length": 12}, view="udp", data=udp))
+    v.append(kat("tcp_getters", "getters", "pnet_packet/src/tcp.rs:288-357",
+                 {"src_port": 49511, "dst_port": 9000, "tcp_sequence": 0x9037D2B8,
+                  "tcp_acknowledgement": 0x944BB276, "tcp_data_offset": 8, "tcp_reserved": 0,
+                  "tcp_flags": 0x18, "tcp_window": 4015, "tcp_urgent_ptr": 0},
+                 view="tcp", data=tcp))
+    # echo identifier / sequence_number over the icmpv6.rs:88-110 echo request
+    # bytes: layout-derived (icmp.rs:221-232,303-314), no reference assertion
+    v.append(kat("icmpv6_echo_getters", "getters", "pnet_packet/src/icmp.rs:303-314 layout (derived)",
+                 {"src_port": 0x8000, "dst_port": 0, "icmp_sequence": 1}, view="icmpv6", data=echo,
+                 derived=True))
+
     # ---- derived (no reference assertion) -------------
     # benches/rs_sender.rs:25-101: the 64-B Eth/IPv4/UDP frame, dst/src MAC zero
     fr = bytearray(64)

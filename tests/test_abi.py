@@ -40,7 +40,7 @@ def test_exports_every_declared_symbol():
 
 
 def test_abi_version_and_strerror():
-    assert lp.lib.pnetgpu_abi_version() == lp.DEFS["PNETGPU_ABI_VERSION"] == 2
+    assert lp.lib.pnetgpu_abi_version() == lp.DEFS["PNETGPU_ABI_VERSION"] == 3
     for code in (0, -1, -2, -3, -4, -5, -6, -7, -8, -9, -99):
         assert lp.lib.pnetgpu_strerror(code)
 

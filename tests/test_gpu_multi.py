@@ -76,3 +76,26 @@ def test_two_ranks_gpu_shards_match_whole_batch_oracle():
             assert np.array_equal(v, full[c][lo:hi]), (lo, c)
     assert ctr[0] == n and ctr[1] == int(w.lengths.astype(np.int64).sum())
     assert ctr[4] == w.expect["ip_bad"] and ctr[5] == w.expect["l4_bad"]
+
+
+def test_bench_two_ranks_one_gpu():
+    """The driver's `python bench.py --gpus 2` end to end with the HIP kernel:
+    the parent starts two ranks (torchrun child), both run on this box's one GPU
+    (gloo stands in for RCCL: two ranks cannot share one device under RCCL), and
+    rank 0's single line reports n_gpus 2 with every planted corruption counted."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["PNETGPU_BENCH_BACKEND"] = "gloo"
+    p = subprocess.run([sys.executable, "-u", os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "3",
+                        "--warmup", "1", "--frames-scale", "0.01", "--workloads", "udp64,imix", "--no-cpu",
+                        "--no-e2e", "--no-extra"], cwd=root, env=env, capture_output=True, text=True, timeout=100)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [json.loads(ln) for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    line = lines[0]
+    assert line["n_gpus"] == 2 and line["counters_ok"] is True
+    assert line["workloads"]["imix"]["counters_ok"] is True
+    assert line["config"]["frames_scale"] == 0.01

@@ -69,7 +69,8 @@ def test_l3_packets_c_vs_python(flags):
 @pytest.mark.parametrize("ext", [0, pyoracle.RX_IPV6_EXT])
 def test_l3_mode_equals_ethernet_mode_shifted(ext):
     """An IP packet seen at layer 3 gives the Ethernet chain's record for the same
-    packet behind a 14-B Ethernet header, with every frame offset 14 lower."""
+    packet behind a 14-B Ethernet header, with every frame offset 14 lower (and
+    no Ethernet view: the MAC columns are 0)."""
     rng = np.random.default_rng(32)
     frames = framegen.random_frames(rng, 800) + framegen.edge_frames(rng) + framegen.extension_frames(rng)
     n = 0
@@ -82,8 +83,9 @@ def test_l3_mode_equals_ethernet_mode_shifted(ext):
         a, b = pyoracle.rx_frame(f, ext), pyoracle.rx_frame(f[14:], ext | pyoracle.RX_L3)
         assert b["l3_offset"] == 0 and a["l3_offset"] == 14
         assert b["l4_offset"] == (a["l4_offset"] - 14 if a["l4_offset"] else 0)
+        assert b["eth_dst"] == b["eth_src"] == 0
         for k in pyoracle.FIELDS:
-            if k not in ("l3_offset", "l4_offset"):
+            if k not in ("l3_offset", "l4_offset", "eth_dst", "eth_src"):
                 assert a[k] == b[k], (k, f.hex())
         n += 1
     assert n > 400

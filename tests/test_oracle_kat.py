@@ -79,3 +79,18 @@ def test_rx_frame_derived(impl, v):
 
 def test_rec_layout():
     assert coracle.lib().oracle_rec_size() == coracle.REC_DTYPE.itemsize
+
+
+@pytest.mark.parametrize("impl", sorted(IMPLS))
+@pytest.mark.parametrize("v", kats.by_kind("getters"), ids=lambda v: v["name"])
+def test_header_getters(impl, v):
+    """Every generated getter the record carries equals the value the reference's
+    test asserts (ethernet.rs, ipv4.rs, ipv6.rs, udp.rs, tcp.rs), and the fields
+    of views the dispatch did not reach stay 0."""
+    r = IMPLS[impl].rx_frame(kats.getter_frame(v))
+    for k, want in v["expected"].items():
+        assert int(r[k]) == want, k
+    if v["view"] != "tcp":
+        assert int(r["tcp_sequence"]) == 0 and int(r["tcp_window"]) == 0
+    if v["view"] not in ("ipv6", "icmpv6"):
+        assert int(r["ip6_flow_label"]) == 0 and int(r["ip6_traffic_class"]) == 0

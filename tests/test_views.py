@@ -28,6 +28,18 @@ def check_views(records, frames, flags=0):
             continue
         seen["ipv4" if ip4 else "ipv6"] += 1
         l3 = int(records["l3_offset"][i])
+        if "ip_version" in (getattr(records, "dtype", None) and records.dtype.names or records):
+            hdr = pyoracle.getters(f[l3:], pyoracle.IPV4 if ip4 else pyoracle.IPV6)
+            assert ip.get_version() == hdr["ip_version"]
+            if ip4:
+                assert (ip.get_header_length(), ip.get_dscp(), ip.get_ecn(), ip.get_total_length(),
+                        ip.get_identification(), ip.get_flags(), ip.get_fragment_offset()) == tuple(
+                    hdr[k] for k in ("ip_header_length", "ip_dscp", "ip_ecn", "ip_total_length",
+                                     "ip_identification", "ip_flags", "ip_fragment_offset"))
+            else:
+                assert (ip.get_traffic_class(), ip.get_flow_label(), ip.get_payload_length()) == (
+                    hdr["ip6_traffic_class"], hdr["ip6_flow_label"], hdr["ip6_payload_length"])
+            assert v.get_destination() == bytes(f[0:6]) and v.get_source() == bytes(f[6:12])
         if ip4:
             assert ip.get_source() == ipaddress.IPv4Address(bytes(f[l3 + 12:l3 + 16]))
             assert ip.get_destination() == ipaddress.IPv4Address(bytes(f[l3 + 16:l3 + 20]))
@@ -44,6 +56,17 @@ def check_views(records, frames, flags=0):
             p = bytes(l4.packet())
             if kind in ("udp", "tcp"):
                 assert l4.get_source() == (p[0] << 8 | p[1]) and l4.get_destination() == (p[2] << 8 | p[3])
+            if "tcp_sequence" in (getattr(records, "dtype", None) and records.dtype.names or records):
+                if kind == "udp":
+                    assert l4.get_length() == (p[4] << 8 | p[5])
+                elif kind == "tcp":
+                    t = pyoracle.getters(p, pyoracle.TCP)
+                    assert (l4.get_sequence(), l4.get_acknowledgement(), l4.get_data_offset(), l4.get_reserved(),
+                            l4.get_flags(), l4.get_window(), l4.get_urgent_ptr()) == tuple(
+                        t[k] for k in ("tcp_sequence", "tcp_acknowledgement", "tcp_data_offset", "tcp_reserved",
+                                       "tcp_flags", "tcp_window", "tcp_urgent_ptr"))
+                elif len(p) >= 8:
+                    assert l4.get_identifier() == (p[4] << 8 | p[5]) and l4.get_sequence_number() == (p[6] << 8 | p[7])
             else:
                 assert l4.get_icmp_type() == p[0] and l4.get_icmp_code() == p[1]
             assert l4.checksum_ok() == bool(st & ST["L4_CSUM_OK"])
@@ -84,7 +107,7 @@ def test_missing_column_is_an_error():
 def test_views_over_ring_batch(tmp_path):
     rng = np.random.default_rng(17)
     frames = framegen.random_frames(rng, 4000)
-    ring = lp.Ring(batch_bytes=1 << 20, batch_frames=1000)
+    ring = lp.Ring(batch_bytes=1 << 20, batch_frames=1000, columns=lp.ALL_COLUMNS)
     batches = []
     for f in frames:
         batches.extend(ring.feed(f))

@@ -123,7 +123,7 @@ static void test_pcap() {
 }
 
 static void test_abi_validation() {
-    CHECK(pnetgpu_abi_version() == 2);
+    CHECK(pnetgpu_abi_version() == PNETGPU_ABI_VERSION);
     for (int c = 0; c >= -9; --c) CHECK(pnetgpu_strerror(c) != nullptr && std::strlen(pnetgpu_strerror(c)) > 0);
     CHECK(pnetgpu_strerror(-1000) != nullptr);
     pnetgpu_batch b{};
