@@ -371,6 +371,15 @@ def load_traffic(workload):
         return None
 
 
+def load_library():
+    """Import the HIP library's binding (ranks only; also used by tools/ that reuse Shard)."""
+    global lp, shard
+    import libpnet_amd as _lp
+    from libpnet_amd import shard as _shard
+    lp, shard = _lp, _shard
+    return _lp
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -417,7 +426,6 @@ def launch_check(args, world, rank):
 
 
 def main():
-    global lp, shard
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1,
                     help="ranks (one per GPU); without WORLD_SIZE set, N > 1 starts them with torchrun")
@@ -452,9 +460,7 @@ def main():
             torch.distributed.destroy_process_group()
         return rc
 
-    import libpnet_amd as _lp
-    from libpnet_amd import shard as _shard
-    lp, shard = _lp, _shard
+    load_library()
     # one rank per GPU; the modulo only matters for a rehearsal with more ranks
     # than GPUs (PNETGPU_BENCH_BACKEND=gloo, e.g. 2 ranks on a 1-GPU box)
     local = local % max(1, torch.cuda.device_count())

@@ -169,7 +169,7 @@ static int rx_common(pnetgpu_ctx* ctx, const pnetgpu_batch* b, const pnetgpu_rx_
             kind != pnetgpu::kKindSmall)
             kind = v;
     }
-    const int ext = rxf != 0;
+    const int ext = rxf != 0 || a.field_cols;   // the EXT instantiations (launch_rx)
     int& per_cu_cached = ctx->per_cu[kind & 7][ext];
     if (per_cu_cached <= 0 || debug) {                             // first use of this kernel on ctx
         int numregs = 0, lds = 0;

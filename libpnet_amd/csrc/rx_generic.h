@@ -134,9 +134,9 @@ __device__ __forceinline__ void tail_sums(const uint8_t* data, WaveLds<NW>& L, i
 // PASS: 0 = window phase for every frame, then the tails of the long ones;
 // 1 = unified: every frame streamed once by the group loop (a hybrid - windows
 // of short frames first, long frames unified - measured 5-15 % slower on IMIX).
-// EXT: batch flags may be non-zero (VLAN / IPv6 extension dispatch); the
-// flags-0 instantiation compiles the parse without those branches (half the
-// code, SGPR spills 118 -> 14, IMIX -2 %).
+// EXT: batch flags may be non-zero (VLAN / IPv6 extension dispatch) or
+// header-field columns may be requested; the plain instantiation compiles the
+// parse without those branches (half the code, SGPR spills 118 -> 14, IMIX -2 %).
 template <int NW, int G, int U, bool NT, int PASS, bool DYN, bool EXT, bool TX>
 __global__ __launch_bounds__(kBlock, 4) void rx_kernel(RxArgs a) {
     static_assert(NW == 8, "window granules");
@@ -270,8 +270,10 @@ __global__ __launch_bounds__(kBlock, 4) void rx_kernel(RxArgs a) {
         finalize(P, tA, tB, (off & 1) != 0, ipc, l4c);
         if (TX && in_batch && !desc_bad) tx_write(const_cast<uint8_t*>(a.data) + off, P, ipc, l4c);
         store_columns(a.cols, f0, lane, in_batch, P, ipc, l4c, slot, sh);
-        if (a.field_cols && in_batch)
+#ifndef PNET_NO_FIELD_COLUMNS   // A/B: the header-field stores compiled out
+        if (EXT && a.field_cols && in_batch)   // header-field columns: EXT instantiations only
             store_field_columns(a.cols, f0 + lane, P, FrameBytes{slot + sh, a.data + off, kWin - sh}, EXT && a.l3mode);
+#endif
         if (a.cols.counters) K.add(in_batch && !desc_bad, len, P.st);
         wave_sync();   // slots and lists are rewritten by the next run
     }

@@ -114,7 +114,7 @@ static int resident_blocks(const void* fn, int block_threads) {
 template <bool EXT, bool TX>
 const void* pick_fn(int kind) {
     switch (kind) {
-    case kKindSmall: return reinterpret_cast<const void*>(rx_small_kernel<TX>);
+    case kKindSmall: return reinterpret_cast<const void*>(rx_small_kernel<TX, EXT>);
     case kKindMtu: return reinterpret_cast<const void*>(rx_kernel<8, PNET_MTU_CFG, EXT, TX>);
     case kKindJumbo: return reinterpret_cast<const void*>(rx_kernel<8, PNET_JUMBO_CFG, EXT, TX>);
     case kKindStream: return reinterpret_cast<const void*>(rx_stream_kernel<PNET_STREAM_SLOTS, EXT>);
@@ -126,7 +126,7 @@ template <bool EXT, bool TX>
 void launch_t(const RxArgs& args, int kind, int blocks, hipStream_t stream) {
     switch (kind) {
     case kKindSmall:
-        hipLaunchKernelGGL(rx_small_kernel<TX>, dim3(blocks), dim3(kBlock), 0, stream, args);
+        hipLaunchKernelGGL((rx_small_kernel<TX, EXT>), dim3(blocks), dim3(kBlock), 0, stream, args);
         break;
     case kKindMtu:
         hipLaunchKernelGGL((rx_kernel<8, PNET_MTU_CFG, EXT, TX>), dim3(blocks), dim3(kBlock), 0, stream, args);
@@ -158,7 +158,9 @@ int rx_blocks_per_cu(int kind, bool ext, int* numregs, int* lds) {
 int rx_waves_per_block(int kind) { return kind == kKindStream ? 1 : kWavesPerBlock; }
 
 int launch_rx(const RxArgs& args, int kind, int blocks, bool tx, hipStream_t stream) {
-    const bool ext = args.flags != 0;
+    // EXT instantiations: dispatch extensions (flags; never with the small kernel)
+    // or header-field columns
+    const bool ext = args.flags != 0 || args.field_cols != 0;
     (void)hipGetLastError();   // a stale error of an unrelated earlier call is not this launch's
     if (tx) ext ? launch_t<true, true>(args, kind, blocks, stream) : launch_t<false, true>(args, kind, blocks, stream);
     else ext ? launch_t<true, false>(args, kind, blocks, stream) : launch_t<false, false>(args, kind, blocks, stream);

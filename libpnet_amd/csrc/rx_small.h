@@ -150,7 +150,9 @@ __device__ __forceinline__ bool small_fast(const uint32_t (&w)[16], uint32_t len
 #ifndef PNET_SMALL_WAVES
 #define PNET_SMALL_WAVES 4   // waves/SIMD the small kernel is register-bounded for
 #endif
-template <bool TX>
+// FIELDS: the header-field columns may be requested (a separate instantiation:
+// their code in the loop cost the plain record 3-10 % on MI355X)
+template <bool TX, bool FIELDS>
 __global__ __launch_bounds__(kBlock, PNET_SMALL_WAVES) void rx_small_kernel(RxArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t lds_slots[kWavesPerBlock][kWave * kSmallSlot];
     __shared__ uint64_t blk_ctr[kWavesPerBlock][PNETGPU_NCOUNTERS];
@@ -228,7 +230,10 @@ __global__ __launch_bounds__(kBlock, PNET_SMALL_WAVES) void rx_small_kernel(RxAr
             }
         }
         store_columns(a.cols, f0, lane, in_batch, P, ipc, l4c, slot, 0);
-        if (a.field_cols && in_batch) store_field_columns(a.cols, f0 + lane, P, FrameBytes{slot, slot, 64}, false);
+#ifndef PNET_NO_FIELD_COLUMNS   // A/B: the header-field stores compiled out
+        if (FIELDS && a.field_cols && in_batch)
+            store_field_columns(a.cols, f0 + lane, P, FrameBytes{slot, slot, 64}, false);
+#endif
         if (a.cols.counters) K.add(in_batch, len, P.st);
         wave_sync();
 #ifndef PNET_SMALL_NOPF

@@ -77,7 +77,7 @@ class Batch:
             if not ptr:                     # not selected (Ring(columns=...))
                 continue
             itemsize = np.dtype(npdt).itemsize
-            ct = {1: ctypes.c_uint8, 2: ctypes.c_uint16, 4: ctypes.c_uint32}[itemsize]
+            ct = {1: ctypes.c_uint8, 2: ctypes.c_uint16, 4: ctypes.c_uint32, 8: ctypes.c_uint64}[itemsize]
             a = np.ctypeslib.as_array(ctypes.cast(ptr, ctypes.POINTER(ct)), (n,) + shape) if n else np.zeros(
                 (0,) + shape, npdt)
             self.records[c] = cp(a).view(npdt)

@@ -3,6 +3,7 @@ sys.path.insert(0, "/root/repo")
 import numpy as np, torch
 import libpnet_amd as lp
 import bench
+bench.load_library()
 
 dev = torch.device("cuda", 0)
 n = 1 << 24

@@ -13,6 +13,8 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import libpnet_amd as lp  # noqa: E402
+import bench  # noqa: E402
+bench.load_library()
 from bench import Shard, HBM_PEAK_GBS, WORKLOADS  # noqa: E402
 
 EXTRA = {"imix": 1 << 22, "udp6_jumbo": 1 << 17}

@@ -8,6 +8,7 @@ import torch
 
 sys.path.insert(0, ".")
 import bench  # noqa: E402
+bench.load_library()
 
 
 def main():
