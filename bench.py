@@ -151,42 +151,115 @@ def host_cpu():
     return {"cpu_model": model, "host_cpus": os.cpu_count(), "usable_cpus": usable}
 
 
-def cpu_baseline(sh, budget_cpu_s=12.0):
-    """The oracle (scalar C restatement, 'port') on this host's cores over a bounded sample."""
+def usable_cpus():
+    try:
+        return len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        return os.cpu_count() or 1
+
+
+def cgroup_cpu_quota():
+    """CPUs' worth of time the cgroup grants (cpu.max), None if unlimited/unknown."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            q, p = fh.read().split()[:2]
+        return None if q == "max" else round(int(q) / int(p), 2)
+    except (OSError, ValueError):
+        return None
+
+
+def _timed_reps(fn, target_s):
+    """Rate of fn(reps): one warm-up pass (page faults, caches), one timed pass to
+    size the sample, then one timed run of about target_s seconds."""
+    fn(1)
+    t = time.perf_counter()
+    fn(1)
+    t1 = max(time.perf_counter() - t, 1e-4)
+    reps = max(1, min(1000, int(target_s / t1)))
+    t = time.perf_counter()
+    fn(reps)
+    return reps, time.perf_counter() - t
+
+
+def cpu_baseline(sh, target_s=3.0):
+    """The oracle (scalar C restatement, 'port') timed on this host: all usable
+    cores (`value`, persistent threads over static shards), 16 threads and one
+    core, over a bounded sample of the same batch."""
     from oracle import coracle  # checker / baseline only
-    nthreads = min(16, os.cpu_count() or 1)
-    n = min(sh.n, 1 << 21)
     w = sh.w
-    frames = 0
-    t0 = time.perf_counter()
-    reps = 0
-    while True:
-        if w.stride:
-            coracle.rx_batch(w.buf, n, stride=w.stride, frame_len=w.frame_len, nthreads=nthreads)
-        else:
-            coracle.rx_batch(w.buf, n, offsets=w.offsets[:n], lengths=w.lengths[:n], nthreads=nthreads)
-        frames += n
-        reps += 1
-        el = time.perf_counter() - t0
-        if el * nthreads >= budget_cpu_s or el > 30:
-            break
-    mpps = frames / el / 1e6
-    # SURVEY.md §8(d)(i): the same restatement on one core, short sample
-    n1, f1, t1 = min(n, 1 << 17), 0, time.perf_counter()
-    while True:
-        if w.stride:
-            coracle.rx_batch(w.buf, n1, stride=w.stride, frame_len=w.frame_len, nthreads=1)
-        else:
-            coracle.rx_batch(w.buf, n1, offsets=w.offsets[:n1], lengths=w.lengths[:n1], nthreads=1)
-        f1 += n1
-        e1 = time.perf_counter() - t1
-        if e1 >= 3.0:
-            break
+    n = min(sh.n, 1 << 22)
+    out = np.zeros(n, dtype=coracle.REC_DTYPE)
+    kw = dict(stride=w.stride, frame_len=w.frame_len) if w.stride else dict(offsets=w.offsets[:n],
+                                                                              lengths=w.lengths[:n])
+    per_frame_bytes = w.expect["bytes"] / sh.n
+    rates = {}
+    for label, nthreads, nn, tgt in (("all", usable_cpus(), n, target_s), ("16", 16, n, target_s / 2),
+                                     ("1", 1, min(n, 1 << 18), target_s / 2)):
+        kwn = kw if w.stride else dict(offsets=w.offsets[:nn], lengths=w.lengths[:nn])
+        reps, el = _timed_reps(lambda r: coracle.rx_batch_reps(w.buf, nn, nthreads=nthreads, reps=r, out=out[:nn],
+                                                               **kwn), tgt)
+        rates[label] = (nn * reps / el / 1e6, nthreads, reps, el, nn)
+    mpps, nthreads, reps, el, _ = rates["all"]
     return {"value": round(mpps, 2), "unit": "Mpkts/s", "cores": nthreads, "kind": "port",
-            "value_1core": round(f1 / e1 / 1e6, 2), **host_cpu(),
-            "gbps": round(frames * (w.expect["bytes"] / sh.n) / el / 1e9, 2),
+            "value_16threads": round(rates["16"][0], 2), "value_1core": round(rates["1"][0], 2),
+            **host_cpu(), "cgroup_cpu_quota": cgroup_cpu_quota(),
+            "gbps": round(mpps * 1e6 * per_frame_bytes / 1e9, 2),
             "sample": f"first {n} frames of the same {sh.name} batch x{reps} passes ({el:.1f} s wall, "
-                      f"{nthreads} threads, oracle/pnet_oracle.c scalar per-frame restatement)"}
+                      f"{nthreads} threads = every usable CPU, persistent threads over static index shards; "
+                      f"oracle/pnet_oracle.c scalar per-frame restatement writing its 120-B record)"}
+
+
+def config0_block(steps, warmup, device):
+    """BASELINE configs[0] (benches/rs_sender.rs + rs_receiver.rs, CPU plumbing):
+    1M rs_sender frames built + checksummed on the CPU (the oracle's restatement
+    of build_udp4_packet, rs_sender.rs:25-72) on one core and on every usable
+    core; their receive + verify on the CPU over an in-memory ring (the
+    dummy.rs:133-153 receiver hands each frame over without a copy); and the GPU
+    legs over the same 1M frames, device-resident: tx_fill_checksums on frames
+    whose checksum fields are zero, then rx_process. The loopback AF_PACKET
+    send/receive needs CAP_NET_RAW, which the GPU box does not grant."""
+    from oracle import coracle  # CPU legs only
+    n = 1 << 20
+    buf = np.zeros(64 * n + 32, dtype=np.uint8)
+    out = {"frames": n, "frame_bytes": 64}
+    for label, nthreads in (("1core", 1), ("all", usable_cpus())):
+        reps, el = _timed_reps(lambda r: coracle.rs_sender_build(n, nthreads=nthreads, reps=r, buf=buf), 2.0)
+        out[f"cpu_build_checksum_{label}_mframes_s"] = round(n * reps / el / 1e6, 2)
+    rec = np.zeros(n, dtype=coracle.REC_DTYPE)
+    for label, nthreads in (("1core", 1), ("all", usable_cpus())):
+        reps, el = _timed_reps(lambda r: coracle.rx_batch_reps(buf, n, stride=64, frame_len=64, nthreads=nthreads,
+                                                               reps=r, out=rec), 2.0)
+        out[f"cpu_receive_verify_{label}_mframes_s"] = round(n * reps / el / 1e6, 2)
+    out["cpu_threads_all"] = usable_cpus()
+    ok = (rec["status"] & 0x0500) == 0x0500
+    out["cpu_frames_verified"] = int(ok.sum())
+    # GPU legs: the same frames with both checksum fields cleared, filled on the GPU
+    blank = buf.reshape(-1)[: 64 * n].reshape(n, 64).copy()
+    blank[:, 24:26] = 0
+    blank[:, 40:42] = 0
+    d = torch.from_numpy(np.concatenate([blank.reshape(-1), np.zeros(32, np.uint8)])).to(device)
+    dcopy = d.clone()
+    st = lp.RxResult(n, device, ("status",), counters=False)
+    stream = torch.cuda.Stream(device)
+    ms_tx = time_launches(lambda s: lp.tx_fill_checksums(d, stride=64, frame_len=64, n_frames=n, out=st, stream=s),
+                          steps, warmup, stream)
+    res = lp.RxResult(n, device, lp.IPV4_COLUMNS, counters=True)
+    ms_rx = time_launches(lambda s: lp.rx_process(d, stride=64, frame_len=64, n_frames=n, out=res, stream=s),
+                          steps, warmup, stream)
+    # the filled frames equal the CPU-built ones byte for byte (every checksum the sender computed)
+    d.copy_(dcopy)
+    lp.tx_fill_checksums(d, stride=64, frame_len=64, n_frames=n, out=st, stream=stream)
+    stream.synchronize()
+    out["gpu_tx_fill_identical_to_cpu_build"] = bool(np.array_equal(d[: 64 * n].cpu().numpy(), buf[: 64 * n]))
+    out["gpu_tx_fill_mframes_s"] = round(n / (ms_tx * 1e-3) / 1e6, 1)
+    out["gpu_tx_fill_kernel_ms"] = round(ms_tx, 4)
+    out["gpu_rx_verify_mframes_s"] = round(n / (ms_rx * 1e-3) / 1e6, 1)
+    out["gpu_rx_verify_kernel_ms"] = round(ms_rx, 4)
+    out["note"] = ("CPU: oracle/pnet_oracle.c (rs_sender_build = rs_sender.rs:25-72 per frame; receive = the "
+                   "packetdump.rs chain per frame, dummy-ring hand-over); GPU: kernel time over 2^20 resident "
+                   "frames (a 64-MiB batch, L2/MALL-resident: not an HBM figure); loopback send/recv not run "
+                   "(no CAP_NET_RAW)")
+    return out
 
 
 def e2e_rate(sh, device, chunks=16, reps=3):
@@ -313,6 +386,7 @@ def tx_fill_rate(sh, steps, warmup, device):
     w = sh.w
     if not w.stride:
         return None
+    small = w.frame_len <= 64
     data = sh.data.clone()
     res = lp.RxResult(sh.n, device, ("status",), counters=False)
     stream = torch.cuda.Stream(device)
@@ -324,14 +398,21 @@ def tx_fill_rate(sh, steps, warmup, device):
     coracle.tx_fill(w.buf[: n1 * w.stride], n1, stride=w.stride, frame_len=w.frame_len)
     cpu = n1 / (time.perf_counter() - t0) / 1e6
     del data
-    return {"mpkts_s": round(sh.n / (ms * 1e-3) / 1e6, 1), "kernel_avg_ms": round(ms, 4),
-            "achieved_gbs": round(alg / (ms * 1e-3) / 1e9, 1), "frac": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-            "cpu_port_1core_mpkts_s": round(cpu, 2),
-            # the kernel writes every patched frame back whole (coalesced 1-KiB stores:
-            # 2-B patches at scattered offsets ran 1.7x slower), so it moves ~2x the frame bytes
-            "rewrite_gbs": round((2 * sh.frame_bytes + 2 * sh.n) / (ms * 1e-3) / 1e9, 1),
-            "note": "device-resident tx_fill_checksums (IPv4 header + L4 checksum patched in place), kernel time; "
-                    f"CPU: oracle_tx_fill, 1 core, first {n1} frames"}
+    out = {"workload": sh.name, "mpkts_s": round(sh.n / (ms * 1e-3) / 1e6, 1), "kernel_avg_ms": round(ms, 4),
+           "alg_bytes_per_launch": alg,
+           "achieved_gbs": round(alg / (ms * 1e-3) / 1e9, 1), "frac": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+           "cpu_port_1core_mpkts_s": round(cpu, 2), "traffic": load_traffic(f"tx_{sh.name}"),
+           "note": "device-resident tx_fill_checksums (IPv4 header + L4 checksum patched in place), kernel time; "
+                   f"CPU: oracle_tx_fill, 1 core, first {n1} frames"}
+    if small:
+        # the small kernel writes every patched frame back whole (coalesced 1-KiB stores:
+        # 2-B patches at scattered offsets ran 1.7x slower), so it moves ~2x the frame bytes
+        out["rewrite_gbs"] = round((2 * sh.frame_bytes + 2 * sh.n) / (ms * 1e-3) / 1e9, 1)
+    else:
+        # the MTU kernel stores the two 2-B checksum fields only (byte stores into the
+        # frame's first line); the traffic key says what HBM saw
+        out["store"] = "2 x 2-B field stores per frame"
+    return out
 
 
 def slices_rate(sh, steps, warmup, device):
@@ -356,6 +437,82 @@ def slices_rate(sh, steps, warmup, device):
     return {"mslices_s": round(n / (ms * 1e-3) / 1e6, 1), "kernel_avg_ms": round(ms, 4),
             "achieved_gbs": round(alg / (ms * 1e-3) / 1e9, 1), "frac": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             "note": f"{n} TCP segments of {w.frame_len - 34} B, util::ipv4_checksum per slice, kernel time"}
+
+
+CAPTURED_TCP_FRAME = bytes.fromhex(   # pnet_packet/benches/packet_benchmarks.rs:63 (bench_ipv4_parsing)
+    "000c291ce319ecf4bbd93e7d08004500002e1b6540008006cd76c0a8c887c0a8c8151a3707d0dd6abb2b1f5fd25150180402120f"
+    "000068656c6c6f0a")
+
+
+def refshapes_block(steps, warmup, device):
+    """The reference's own micro-benchmark shapes, batched on the GPU with the
+    oracle's CPU rate beside them:
+      checksum_small  util::checksum(&[99u8; 20], 5)    checksum_benchmarks.rs:8-12
+      checksum_large  util::checksum(&[123u8; 1024], 5) checksum_benchmarks.rs:14-18
+      ipv4_parsing    the captured 60-B TCP frame through the receive chain
+                      (Ipv4Packet::new over its Ethernet payload, then the rest
+                      of packetdump's chain), packet_benchmarks.rs:63-71
+    Slices are packed back to back, one (u64 offset, u32 length, u32 skipword)
+    descriptor each; algorithmic bytes = slice bytes + 16 B descriptor + 2 B result."""
+    from oracle import coracle  # CPU baseline legs only
+    out = {}
+    stream = torch.cuda.Stream(device)
+    for name, fill, size, n in (("checksum_small", 99, 20, 1 << 24), ("checksum_large", 123, 1024, 1 << 20)):
+        buf = np.full(n * size + 32, fill, dtype=np.uint8)
+        offs = np.arange(n, dtype=np.uint64) * np.uint64(size)
+        lens = np.full(n, size, dtype=np.uint32)
+        skips = np.full(n, 5, dtype=np.uint32)
+        d = torch.from_numpy(buf).to(device)
+        do, dl, ds = (torch.from_numpy(offs.view(np.int64)).to(device), torch.from_numpy(lens.view(np.int32)).to(device),
+                      torch.from_numpy(skips.view(np.int32)).to(device))
+        res = {}
+        ms = time_launches(lambda s: res.__setitem__("o", lp.checksum_slices(d, do, dl, ds, stream=s)), steps, warmup,
+                           stream)
+        got = res["o"].cpu().numpy().view(np.uint16)
+        want = coracle.checksum(bytes([fill] * size), 5)
+        alg = n * (size + 16 + 2)
+        cpu_out = np.zeros(n, np.uint16)
+        k = min(n, 1 << 20)
+        cpu = {}
+        for label, nt in (("1core", 1), ("all", usable_cpus())):
+            reps, el = _timed_reps(lambda r: coracle.checksum_slices_reps(buf, offs[:k], lens[:k], skips[:k],
+                                                                          cpu_out[:k], nthreads=nt, reps=r), 1.0)
+            cpu[label] = round(k * reps / el / 1e6, 1)
+        out[name] = {"slices": n, "slice_bytes": size, "skipword": 5, "kernel_avg_ms": round(ms, 4),
+                     "mslices_s": round(n / (ms * 1e-3) / 1e6, 1),
+                     "achieved_gbs": round(alg / (ms * 1e-3) / 1e9, 1),
+                     "frac": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                     "parity": bool((got == want).all()), "expected": int(want),
+                     "cpu_port_1core_mslices_s": cpu["1core"], "cpu_port_all_mslices_s": cpu["all"]}
+        del d, do, dl, ds
+    # ipv4_parsing: the captured frame replicated at a 64-B stride (the small kernel)
+    n = 1 << 24
+    frame = np.frombuffer(CAPTURED_TCP_FRAME + bytes(64 - len(CAPTURED_TCP_FRAME)), np.uint8)
+    buf = np.concatenate([np.tile(frame, n), np.zeros(32, np.uint8)])
+    d = torch.from_numpy(buf).to(device)
+    res = lp.RxResult(n, device, lp.IPV4_COLUMNS, counters=True)
+    flen = len(CAPTURED_TCP_FRAME)
+    ms = time_launches(lambda s: lp.rx_process(d, stride=64, frame_len=flen, n_frames=n, out=res, stream=s), steps,
+                       warmup, stream)
+    rec = coracle.rx_frame(CAPTURED_TCP_FRAME)
+    got = res.numpy()
+    parity = all(bool((got[c] == rec[c]).all()) for c in lp.IPV4_COLUMNS)
+    alg = n * (flen + lp.column_bytes(lp.IPV4_COLUMNS))
+    recs = np.zeros(1 << 20, dtype=coracle.REC_DTYPE)
+    cpu = {}
+    for label, nt in (("1core", 1), ("all", usable_cpus())):
+        reps, el = _timed_reps(lambda r: coracle.rx_batch_reps(buf, 1 << 20, stride=64, frame_len=flen, nthreads=nt,
+                                                               reps=r, out=recs), 1.0)
+        cpu[label] = round((1 << 20) * reps / el / 1e6, 1)
+    out["ipv4_parsing"] = {"frames": n, "frame_bytes": flen, "stride": 64, "kernel_avg_ms": round(ms, 4),
+                           "mpkts_s": round(n / (ms * 1e-3) / 1e6, 1),
+                           "achieved_gbs": round(alg / (ms * 1e-3) / 1e9, 1),
+                           "frac": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "parity": parity,
+                           "cpu_port_1core_mpkts_s": cpu["1core"], "cpu_port_all_mpkts_s": cpu["all"]}
+    out["note"] = ("GPU kernel time over device-resident batches (IPv4 record columns for ipv4_parsing); frac "
+                   "= algorithmic bytes (slice or frame + descriptor + result) / kernel time / 8 TB/s; CPU: the "
+                   "oracle's scalar restatement over the first 2^20 items")
+    return out
 
 
 def load_traffic(workload):
@@ -543,6 +700,8 @@ def main():
                 "unit": "GB/s",
                 "frac": round(p["achieved_gbs"] / HBM_PEAK_GBS, 4),
                 "traffic": load_traffic(primary),
+                "traffic_source": f"profiles/pmc_{primary}.json: FETCH_SIZE/WRITE_SIZE from separate rocprofv3 --pmc "
+                                  "passes over the same launch (tools/profile_round.sh), not measured in this run",
                 "kernel": WORKLOADS[primary]["kernel"],
                 "kernel_avg_ms": round(p["kernel_avg_ms"], 4),
                 "alg_bytes_per_launch": sh.alg_bytes,
@@ -564,9 +723,14 @@ def main():
             line["cpu_baseline"] = cpu_baseline(sh)
             for name, r in results.items():
                 if name != primary and "synth" not in WORKLOADS[name]:   # not for a re-run of the same frames
-                    line["workloads"][name]["cpu_baseline"] = cpu_baseline(r["sh"], budget_cpu_s=6.0)
+                    line["workloads"][name]["cpu_baseline"] = cpu_baseline(r["sh"], target_s=1.5)
         if world == 1 and not args.no_extra:
+            line["config0"] = config0_block(args.steps, args.warmup, device)
+            line["reference_shapes"] = refshapes_block(args.steps, args.warmup, device)
             line["tx_fill"] = tx_fill_rate(sh, args.steps, args.warmup, device)
+            if "tcp1500" in results:
+                line["workloads"]["tcp1500"]["tx_fill"] = tx_fill_rate(results["tcp1500"]["sh"], args.steps,
+                                                                       args.warmup, device)
             if "tcp1500" in results:
                 line["workloads"]["tcp1500"]["ipv4_checksum_slices"] = slices_rate(results["tcp1500"]["sh"], args.steps,
                                                                                    args.warmup, device)

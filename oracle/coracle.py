@@ -71,6 +71,15 @@ def lib():
         L.oracle_tx_fill.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
                                      ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
                                      ctypes.c_uint32, ctypes.c_void_p]
+        L.oracle_rx_batch_reps.restype = None
+        L.oracle_rx_batch_reps.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
+                                           ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
+                                           ctypes.c_uint32, ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+        L.oracle_rs_sender_build.restype = None
+        L.oracle_rs_sender_build.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_int]
+        L.oracle_checksum_slices_reps.restype = None
+        L.oracle_checksum_slices_reps.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
+                                                  ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
         L.oracle_checksum_slices.restype = None
         L.oracle_checksum_slices.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
                                              ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
@@ -123,6 +132,13 @@ def rx_batch(buf, n, *, stride=0, frame_len=0, first=0, offsets=None, lengths=No
     return out
 
 
+def checksum_slices_reps(buf, offsets, lengths, skipwords, out, nthreads=1, reps=1):
+    """util::checksum per slice, persistent threads, each shard `reps` times (CPU baseline timing)."""
+    lib().oracle_checksum_slices_reps(buf.ctypes.data, len(offsets), offsets.ctypes.data, lengths.ctypes.data,
+                                      skipwords.ctypes.data, out.ctypes.data, nthreads, reps)
+    return out
+
+
 def checksum_slices(buf, offsets, lengths, skipwords):
     buf = np.ascontiguousarray(buf, dtype=np.uint8)
     offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
@@ -146,3 +162,27 @@ def tx_fill(buf, n, *, stride=0, frame_len=0, first=0, offsets=None, lengths=Non
     lib().oracle_tx_fill(out_buf.ctypes.data, out_buf.size, n, first, stride, frame_len, offp, lenp,
                          flags, recs.ctypes.data)
     return out_buf, recs
+
+
+def rx_batch_reps(buf, n, *, stride=0, frame_len=0, first=0, offsets=None, lengths=None, nthreads=1, reps=1,
+                  flags=0, out=None):
+    """rx_batch with persistent threads, each shard processed `reps` times (CPU baseline timing)."""
+    buf = np.ascontiguousarray(buf, dtype=np.uint8)
+    if out is None:
+        out = np.zeros(n, dtype=REC_DTYPE)
+    offp = lenp = None
+    if stride == 0:
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        lengths = np.ascontiguousarray(lengths, dtype=np.uint32)
+        offp, lenp = offsets.ctypes.data, lengths.ctypes.data
+    lib().oracle_rx_batch_reps(buf.ctypes.data, buf.size, n, first, stride, frame_len, offp, lenp, flags,
+                               out.ctypes.data, nthreads, reps)
+    return out
+
+
+def rs_sender_build(n, nthreads=1, reps=1, buf=None):
+    """n frames built as benches/rs_sender.rs:25-72 does (64-B stride); returns the uint8 buffer."""
+    if buf is None:
+        buf = np.zeros(64 * n + 32, dtype=np.uint8)
+    lib().oracle_rs_sender_build(buf.ctypes.data, n, nthreads, reps)
+    return buf

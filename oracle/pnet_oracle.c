@@ -419,3 +419,109 @@ void oracle_tx_fill(uint8_t* buf, uint64_t buf_len, uint64_t n, uint64_t first, 
         }
     }
 }
+
+/* ---- CPU baselines (bench.py's cpu_baseline / config0 legs) ---------------
+ * Persistent threads: each of nthreads static index shards is processed `reps`
+ * times by one thread, so short passes are not dominated by thread start-up. */
+
+typedef struct {
+    void (*fn)(void* arg, uint64_t lo, uint64_t hi);
+    void* arg;
+    uint64_t lo, hi;
+    int reps;
+} rep_job_t;
+
+static void* rep_worker(void* p) {
+    rep_job_t* j = (rep_job_t*)p;
+    for (int r = 0; r < j->reps; ++r) j->fn(j->arg, j->lo, j->hi);
+    return NULL;
+}
+
+static void run_sharded(void (*fn)(void*, uint64_t, uint64_t), void* arg, uint64_t n, int nthreads, int reps) {
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 1024) nthreads = 1024;
+    static rep_job_t jobs[1024];
+    static pthread_t th[1024];
+    for (int t = 0; t < nthreads; ++t) {
+        rep_job_t j = { fn, arg, n * (uint64_t)t / nthreads, n * (uint64_t)(t + 1) / nthreads, reps };
+        jobs[t] = j;
+    }
+    if (nthreads == 1) { rep_worker(&jobs[0]); return; }
+    int started = 0;
+    for (int t = 0; t < nthreads; ++t)
+        if (pthread_create(&th[t], NULL, rep_worker, &jobs[t]) == 0) ++started;
+        else { rep_worker(&jobs[t]); th[t] = 0; }
+    for (int t = 0; t < nthreads; ++t)
+        if (th[t]) pthread_join(th[t], NULL);
+    (void)started;
+}
+
+static void rx_range(void* arg, uint64_t lo, uint64_t hi) {
+    shard_t s = *(shard_t*)arg;
+    s.lo = lo;
+    s.hi = hi;
+    rx_shard(&s);
+}
+
+void oracle_rx_batch_reps(const uint8_t* buf, uint64_t buf_len, uint64_t n, uint64_t first, uint32_t stride,
+                          uint32_t frame_len, const uint64_t* offsets, const uint32_t* lengths, uint32_t flags,
+                          oracle_rec* out, int nthreads, int reps) {
+    shard_t s = { buf, buf_len, 0, n, first, stride, frame_len, offsets, lengths, out, flags };
+    run_sharded(rx_range, &s, n, nthreads, reps);
+}
+
+/* benches/rs_sender.rs:25-72: build_udp4_packet behind an Ethernet header
+ * (rs_sender.rs:94-100), the IPv4 checksum after the IPv4 setters and the UDP
+ * checksum after the payload, written big-endian by the setters. Frame i
+ * carries identification i and UDP source port 1234 + i (16-bit) so that every
+ * frame's checksums differ; frame 0 is rs_sender's own (0xB8CA / 0xB94C). */
+static void rs_sender_frame(uint8_t* f, uint64_t i) {
+    static const uint8_t dst[6] = {0x02, 0x00, 0x00, 0x00, 0x00, 0x01};
+    static const uint8_t src[6] = {0x02, 0x00, 0x00, 0x00, 0x00, 0x02};
+    memset(f, 0, 64);
+    memcpy(f, dst, 6);                                   /* set_destination */
+    memcpy(f + 6, src, 6);                               /* set_source */
+    f[12] = 0x08; f[13] = 0x00;                          /* set_ethertype(EtherTypes::Ipv4) */
+    uint8_t* ip = f + 14;
+    ip[0] = (uint8_t)((4 << 4) | 5);                     /* set_version(4), set_header_length(5) */
+    ip[2] = 0; ip[3] = 20 + 8 + 5;                       /* set_total_length(33) */
+    ip[4] = (uint8_t)(i >> 8); ip[5] = (uint8_t)i;       /* identification */
+    ip[8] = 4;                                           /* set_ttl(4) */
+    ip[9] = 17;                                          /* IpNextHeaderProtocols::Udp */
+    ip[12] = 127; ip[15] = 1;                            /* set_source(127.0.0.1) */
+    ip[16] = 127; ip[19] = 1;                            /* set_destination(127.0.0.1) */
+    const uint16_t ipc = oracle_checksum(ip, 20, 5);     /* ipv4::checksum (ipv4.rs:165-178) */
+    ip[10] = (uint8_t)(ipc >> 8); ip[11] = (uint8_t)ipc;
+    uint8_t* udp = ip + 20;
+    const uint16_t sport = (uint16_t)(1234 + i);
+    udp[0] = (uint8_t)(sport >> 8); udp[1] = (uint8_t)sport;   /* set_source */
+    udp[2] = 1234 >> 8; udp[3] = 1234 & 0xFF;            /* set_destination(1234) */
+    udp[4] = 0; udp[5] = 8 + 5;                          /* set_length(13) */
+    memcpy(udp + 8, "rmesg", 5);
+    const uint16_t uc = oracle_ipv4_checksum(udp, 13, 3, NULL, 0, ip + 12, ip + 16, 17);   /* udp.rs:34-56 */
+    udp[6] = (uint8_t)(uc >> 8); udp[7] = (uint8_t)uc;
+}
+
+static void build_range(void* arg, uint64_t lo, uint64_t hi) {
+    uint8_t* buf = (uint8_t*)arg;
+    for (uint64_t i = lo; i < hi; ++i) rs_sender_frame(buf + 64 * i, i);
+}
+
+void oracle_rs_sender_build(uint8_t* buf, uint64_t n, int nthreads, int reps) {
+    run_sharded(build_range, buf, n, nthreads, reps);
+}
+
+typedef struct {
+    const uint8_t* buf; const uint64_t* offsets; const uint32_t* lengths; const uint32_t* skipwords; uint16_t* out;
+} slices_t;
+
+static void slices_range(void* arg, uint64_t lo, uint64_t hi) {
+    const slices_t* s = (const slices_t*)arg;
+    for (uint64_t i = lo; i < hi; ++i) s->out[i] = oracle_checksum(s->buf + s->offsets[i], s->lengths[i], s->skipwords[i]);
+}
+
+void oracle_checksum_slices_reps(const uint8_t* buf, uint64_t n, const uint64_t* offsets, const uint32_t* lengths,
+                                 const uint32_t* skipwords, uint16_t* out, int nthreads, int reps) {
+    slices_t s = { buf, offsets, lengths, skipwords, out };
+    run_sharded(slices_range, &s, n, nthreads, reps);
+}

@@ -150,6 +150,17 @@ void oracle_tx_fill(uint8_t* buf, uint64_t buf_len, uint64_t n, uint64_t first, 
                     uint32_t frame_len, const uint64_t* offsets, const uint32_t* lengths, uint32_t flags,
                     oracle_rec* out);
 
+/* CPU baselines: the batch receive with persistent threads (each static shard
+ * processed `reps` times by one of nthreads threads), and rs_sender.rs's
+ * build_udp4_packet (benches/rs_sender.rs:25-72) for n 64-B frames at stride 64
+ * (frame i: identification i, UDP source port 1234 + i). */
+void oracle_rx_batch_reps(const uint8_t* buf, uint64_t buf_len, uint64_t n, uint64_t first, uint32_t stride,
+                          uint32_t frame_len, const uint64_t* offsets, const uint32_t* lengths, uint32_t flags,
+                          oracle_rec* out, int nthreads, int reps);
+void oracle_rs_sender_build(uint8_t* buf, uint64_t n, int nthreads, int reps);
+void oracle_checksum_slices_reps(const uint8_t* buf, uint64_t n, const uint64_t* offsets, const uint32_t* lengths,
+                                 const uint32_t* skipwords, uint16_t* out, int nthreads, int reps);
+
 /* Batched util::checksum over (offset, length, skipword) slices. */
 void oracle_checksum_slices(const uint8_t* buf, uint64_t n, const uint64_t* offsets,
                             const uint32_t* lengths, const uint32_t* skipwords,

@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--env", default="")
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--tx", action="store_true", help="time tx_fill_checksums instead of rx_process")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     key, vals = (a.env.split("=") + [""])[:2] if a.env else ("", "")
@@ -34,6 +35,13 @@ def main():
     for name in a.workloads.split(","):
         n = WORKLOADS[name]["n"] if name in WORKLOADS else EXTRA[name]
         sh = Shard(name, n, 1, dev)
+        if a.tx:
+            st = lp.RxResult(sh.n, dev, ("status",), counters=False)
+
+            def tx_step(stream, sh=sh, st=st):
+                lp.tx_fill_checksums(sh.data, stride=sh.w.stride, frame_len=sh.w.frame_len, n_frames=sh.n, out=st,
+                                     stream=stream)
+            sh.step = tx_step
         times = {v: [] for v in vals}
         for _ in range(a.rounds):
             for v in vals:
