@@ -192,21 +192,34 @@ def cpu_baseline(sh, target_s=3.0):
     kw = dict(stride=w.stride, frame_len=w.frame_len) if w.stride else dict(offsets=w.offsets[:n],
                                                                               lengths=w.lengths[:n])
     per_frame_bytes = w.expect["bytes"] / sh.n
+    quota = cgroup_cpu_quota()
+    counts = [("all", usable_cpus())]
+    if quota and int(quota) < usable_cpus():
+        counts.append(("quota", max(1, int(quota))))     # the cgroup's share of the CPUs
+    counts += [("16", 16), ("1", 1)]
     rates = {}
-    for label, nthreads, nn, tgt in (("all", usable_cpus(), n, target_s), ("16", 16, n, target_s / 2),
-                                     ("1", 1, min(n, 1 << 18), target_s / 2)):
+    for label, nthreads in counts:
+        nn = n if nthreads > 1 else min(n, 1 << 18)
         kwn = kw if w.stride else dict(offsets=w.offsets[:nn], lengths=w.lengths[:nn])
         reps, el = _timed_reps(lambda r: coracle.rx_batch_reps(w.buf, nn, nthreads=nthreads, reps=r, out=out[:nn],
-                                                               **kwn), tgt)
+                                                               **kwn), target_s if label == "all" else target_s / 2)
         rates[label] = (nn * reps / el / 1e6, nthreads, reps, el, nn)
-    mpps, nthreads, reps, el, _ = rates["all"]
+    # `value` = the best of the thread counts (every usable CPU by affinity, the
+    # cgroup quota, 16, 1): with a CPU quota below the affinity mask, one thread
+    # per affinity CPU oversubscribes the quota and runs slower than the quota's
+    # worth of threads; every count's rate is kept beside it
+    best = max(rates, key=lambda k: rates[k][0])
+    mpps, nthreads, reps, el, nn = rates[best]
     return {"value": round(mpps, 2), "unit": "Mpkts/s", "cores": nthreads, "kind": "port",
+            "value_all_usable_cpus": round(rates["all"][0], 2), "threads_all_usable_cpus": rates["all"][1],
+            **({"value_quota_threads": round(rates["quota"][0], 2)} if "quota" in rates else {}),
             "value_16threads": round(rates["16"][0], 2), "value_1core": round(rates["1"][0], 2),
-            **host_cpu(), "cgroup_cpu_quota": cgroup_cpu_quota(),
+            **host_cpu(), "cgroup_cpu_quota": quota,
             "gbps": round(mpps * 1e6 * per_frame_bytes / 1e9, 2),
-            "sample": f"first {n} frames of the same {sh.name} batch x{reps} passes ({el:.1f} s wall, "
-                      f"{nthreads} threads = every usable CPU, persistent threads over static index shards; "
-                      f"oracle/pnet_oracle.c scalar per-frame restatement writing its 120-B record)"}
+            "sample": f"first {nn} frames of the same {sh.name} batch x{reps} passes ({el:.1f} s wall, "
+                      f"{nthreads} threads (best of {', '.join(str(c) for _, c in counts)}), persistent threads "
+                      f"over static index shards; oracle/pnet_oracle.c scalar per-frame restatement writing its "
+                      f"120-B record)"}
 
 
 def config0_block(steps, warmup, device):
@@ -248,6 +261,7 @@ def config0_block(steps, warmup, device):
                           steps, warmup, stream)
     # the filled frames equal the CPU-built ones byte for byte (every checksum the sender computed)
     d.copy_(dcopy)
+    torch.cuda.synchronize()          # the restore (current stream) before the fill (`stream`)
     lp.tx_fill_checksums(d, stride=64, frame_len=64, n_frames=n, out=st, stream=stream)
     stream.synchronize()
     out["gpu_tx_fill_identical_to_cpu_build"] = bool(np.array_equal(d[: 64 * n].cpu().numpy(), buf[: 64 * n]))
