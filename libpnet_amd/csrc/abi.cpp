@@ -140,7 +140,8 @@ static int rx_common(pnetgpu_ctx* ctx, const pnetgpu_batch* b, const pnetgpu_rx_
     // Kernel choice. Small: fixed stride, every frame 16-B aligned, at most 64 B,
     // inside the buffer (the 64-B configs). Otherwise rx_kernel with the tail
     // shape of the batch's frame sizes: MTU or jumbo for fixed stride, mixed for
-    // descriptor batches (their lengths are device-resident).
+    // descriptor batches (their lengths are device-resident). rx_flat_kernel
+    // (compact descriptors only) is opt-in: PNETGPU_RX_KIND=5.
     int kind = pnetgpu::kKindMixed;
     bool stream_ok = false;
     if (b->stride) {
@@ -165,7 +166,7 @@ static int rx_common(pnetgpu_ctx* ctx, const pnetgpu_batch* b, const pnetgpu_rx_
     if (kind_env) {
         const int v = std::atoi(kind_env);
         if ((v == pnetgpu::kKindMixed || v == pnetgpu::kKindMtu || v == pnetgpu::kKindJumbo ||
-             (v == pnetgpu::kKindStream && stream_ok)) &&
+             (v == pnetgpu::kKindStream && stream_ok) || (v == pnetgpu::kKindFlat && a.desc_compact)) &&
             kind != pnetgpu::kKindSmall)
             kind = v;
     }

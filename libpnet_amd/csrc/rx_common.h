@@ -43,6 +43,18 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Inclusive scan over the wave: DPP row_shr 1/2/4/8 inside each 16-lane row,
+// then row_bcast:15 and row_bcast:31 carry the row totals forward.
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, true);   // row_shr:1
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, true);   // row_shr:2
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, true);   // row_shr:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, true);   // row_shr:8
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
+    return v;
+}
+
 // ---- LDS access --------------------------------------------------------------
 
 // 16 bytes of a run [p, p+16) of an LDS slot at any alignment, as 4 LE dwords.
@@ -395,24 +407,36 @@ __device__ __forceinline__ void put(T* col, uint64_t i, T v) {
 
 // Column stores for the frames of one run: the base is wave-uniform (SGPR) and
 // the lane adds its index, so each store is one coalesced wave instruction.
+// An opaque per-run copy of a frame index: without it the compiler hoists
+// column + lane * size for every column out of the run loop, holding ~2 VGPRs
+// per column for the whole kernel (16 columns: 32 VGPRs, spills in the flat
+// kernel); with it each store recomputes its address (one VALU op).
+__device__ __forceinline__ uint64_t opaque_index(uint64_t i) {
+#ifndef PNET_HOIST_COLUMNS   // A/B: let the compiler hoist the column addresses
+    asm volatile("" : "+v"(i));
+#endif
+    return i;
+}
+
 __device__ __forceinline__ void store_columns(const pnetgpu_rx_columns& C, uint64_t f0, int lane, bool in_batch,
                                               const Parsed& P, uint32_t ipc, uint32_t l4c, const uint8_t* slot,
                                               int sh) {
     if (!in_batch) return;
-    if (C.status) put<uint16_t>(C.status, f0 + lane, (uint16_t)P.st);
-    if (C.ip_csum) put<uint16_t>(C.ip_csum, f0 + lane, (uint16_t)ipc);
-    if (C.l4_csum) put<uint16_t>(C.l4_csum, f0 + lane, (uint16_t)l4c);
-    if (C.ethertype) put<uint16_t>(C.ethertype, f0 + lane, (uint16_t)P.et);
-    if (C.ip_proto) put<uint8_t>(C.ip_proto, f0 + lane, (uint8_t)P.proto);
-    if (C.ttl) put<uint8_t>(C.ttl, f0 + lane, (uint8_t)P.ttl);
-    if (C.l4_offset) put<uint16_t>(C.l4_offset, f0 + lane, (uint16_t)P.l4off);
-    if (C.l4_length) put<uint16_t>(C.l4_length, f0 + lane, (uint16_t)P.l4len);
-    if (C.src_port) put<uint16_t>(C.src_port, f0 + lane, (uint16_t)P.sp);
-    if (C.dst_port) put<uint16_t>(C.dst_port, f0 + lane, (uint16_t)P.dp);
-    if (C.src_ipv4) put<uint32_t>(C.src_ipv4, f0 + lane, P.s4);
-    if (C.dst_ipv4) put<uint32_t>(C.dst_ipv4, f0 + lane, P.d4);
-    if (C.vlan_tci) put<uint16_t>(C.vlan_tci, f0 + lane, (uint16_t)P.vlan_tci);
-    if (C.l3_offset) put<uint8_t>(C.l3_offset, f0 + lane, (uint8_t)P.l3);
+    const uint64_t i = opaque_index(f0 + (uint64_t)lane);
+    if (C.status) put<uint16_t>(C.status, i, (uint16_t)P.st);
+    if (C.ip_csum) put<uint16_t>(C.ip_csum, i, (uint16_t)ipc);
+    if (C.l4_csum) put<uint16_t>(C.l4_csum, i, (uint16_t)l4c);
+    if (C.ethertype) put<uint16_t>(C.ethertype, i, (uint16_t)P.et);
+    if (C.ip_proto) put<uint8_t>(C.ip_proto, i, (uint8_t)P.proto);
+    if (C.ttl) put<uint8_t>(C.ttl, i, (uint8_t)P.ttl);
+    if (C.l4_offset) put<uint16_t>(C.l4_offset, i, (uint16_t)P.l4off);
+    if (C.l4_length) put<uint16_t>(C.l4_length, i, (uint16_t)P.l4len);
+    if (C.src_port) put<uint16_t>(C.src_port, i, (uint16_t)P.sp);
+    if (C.dst_port) put<uint16_t>(C.dst_port, i, (uint16_t)P.dp);
+    if (C.src_ipv4) put<uint32_t>(C.src_ipv4, i, P.s4);
+    if (C.dst_ipv4) put<uint32_t>(C.dst_ipv4, i, P.d4);
+    if (C.vlan_tci) put<uint16_t>(C.vlan_tci, i, (uint16_t)P.vlan_tci);
+    if (C.l3_offset) put<uint8_t>(C.l3_offset, i, (uint8_t)P.l3);
     if (C.src_ipv6 || C.dst_ipv6) {
         const bool v6ok = (P.st & (PNET_ST_L3_MASK | PNET_ST_L3_MALFORMED)) == PNET_ST_L3_IPV6;
         uint4 sv = make_uint4(0, 0, 0, 0), dv = make_uint4(0, 0, 0, 0);
@@ -420,8 +444,8 @@ __device__ __forceinline__ void store_columns(const pnetgpu_rx_columns& C, uint6
             sv = lds_read16_unaligned(slot, sh + (int)P.l3 + 8);
             dv = lds_read16_unaligned(slot, sh + (int)P.l3 + 24);
         }
-        if (C.src_ipv6) reinterpret_cast<uint4*>(C.src_ipv6)[f0 + lane] = sv;
-        if (C.dst_ipv6) reinterpret_cast<uint4*>(C.dst_ipv6)[f0 + lane] = dv;
+        if (C.src_ipv6) reinterpret_cast<uint4*>(C.src_ipv6)[i] = sv;
+        if (C.dst_ipv6) reinterpret_cast<uint4*>(C.dst_ipv6)[i] = dv;
     }
 }
 
@@ -432,8 +456,9 @@ __device__ __forceinline__ void store_columns(const pnetgpu_rx_columns& C, uint6
 // tcp.rs:55-71, icmp.rs:221-232,303-314 (getter bit extraction:
 // pnet_macros/src/decorator.rs:1563-1670). Mirrors oracle_rx_frame_ex.
 // `l3mode`: PNETGPU_RX_L3 batch (no Ethernet view).
-__device__ __forceinline__ void store_field_columns(const pnetgpu_rx_columns& C, uint64_t i, const Parsed& P,
+__device__ __forceinline__ void store_field_columns(const pnetgpu_rx_columns& C, uint64_t fi, const Parsed& P,
                                                  const FrameBytes& F, bool l3mode) {
+    const uint64_t i = opaque_index(fi);
     const uint32_t st = P.st;
     const bool eth = !l3mode && !(st & (PNET_ST_ETH_MALFORMED | PNET_ST_DESC_INVALID));
     const bool v4 = (st & (PNET_ST_L3_MASK | PNET_ST_L3_MALFORMED)) == PNET_ST_L3_IPV4;

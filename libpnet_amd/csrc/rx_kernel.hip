@@ -65,6 +65,7 @@
 #include "rx_small.h"
 #include "rx_generic.h"
 #include "rx_stream.h"
+#include "rx_flat.h"
 #include "rx_slices.h"
 
 namespace pnetgpu {
@@ -105,6 +106,13 @@ static int resident_blocks(const void* fn, int block_threads) {
 #ifndef PNET_JUMBO_CFG
 #define PNET_JUMBO_CFG 64, 9, true, 0, false
 #endif
+#define PNET_MIXED_FN(EXT, TX) rx_kernel<8, PNET_MIXED_CFG, EXT, TX>
+#define PNET_JUMBO_FN(EXT, TX) rx_kernel<8, PNET_JUMBO_CFG, EXT, TX>
+
+// loads in flight per lane per round of the flat kernel
+#ifndef PNET_FLAT_U
+#define PNET_FLAT_U 4
+#endif
 
 // LDS ring steps (4 KiB each) per wave of the stream kernel
 #ifndef PNET_STREAM_SLOTS
@@ -116,9 +124,10 @@ const void* pick_fn(int kind) {
     switch (kind) {
     case kKindSmall: return reinterpret_cast<const void*>(rx_small_kernel<TX, EXT>);
     case kKindMtu: return reinterpret_cast<const void*>(rx_kernel<8, PNET_MTU_CFG, EXT, TX>);
-    case kKindJumbo: return reinterpret_cast<const void*>(rx_kernel<8, PNET_JUMBO_CFG, EXT, TX>);
+    case kKindJumbo: return reinterpret_cast<const void*>(PNET_JUMBO_FN(EXT, TX));
     case kKindStream: return reinterpret_cast<const void*>(rx_stream_kernel<PNET_STREAM_SLOTS, EXT>);
-    default: return reinterpret_cast<const void*>(rx_kernel<8, PNET_MIXED_CFG, EXT, TX>);
+    case kKindFlat: return reinterpret_cast<const void*>(rx_flat_kernel<PNET_FLAT_U, EXT, TX>);
+    default: return reinterpret_cast<const void*>(PNET_MIXED_FN(EXT, TX));
     }
 }
 
@@ -132,14 +141,17 @@ void launch_t(const RxArgs& args, int kind, int blocks, hipStream_t stream) {
         hipLaunchKernelGGL((rx_kernel<8, PNET_MTU_CFG, EXT, TX>), dim3(blocks), dim3(kBlock), 0, stream, args);
         break;
     case kKindJumbo:
-        hipLaunchKernelGGL((rx_kernel<8, PNET_JUMBO_CFG, EXT, TX>), dim3(blocks), dim3(kBlock), 0, stream, args);
+        hipLaunchKernelGGL((PNET_JUMBO_FN(EXT, TX)), dim3(blocks), dim3(kBlock), 0, stream, args);
+        break;
+    case kKindFlat:
+        hipLaunchKernelGGL((rx_flat_kernel<PNET_FLAT_U, EXT, TX>), dim3(blocks), dim3(kBlock), 0, stream, args);
         break;
     case kKindStream:   // receive only: the host never picks it for TX
         if (!TX)
             hipLaunchKernelGGL((rx_stream_kernel<PNET_STREAM_SLOTS, EXT>), dim3(blocks), dim3(kWave), 0, stream, args);
         break;
     default:
-        hipLaunchKernelGGL((rx_kernel<8, PNET_MIXED_CFG, EXT, TX>), dim3(blocks), dim3(kBlock), 0, stream, args);
+        hipLaunchKernelGGL((PNET_MIXED_FN(EXT, TX)), dim3(blocks), dim3(kBlock), 0, stream, args);
     }
 }
 

@@ -95,18 +95,6 @@ __device__ __forceinline__ int column_stores(const pnetgpu_rx_columns& C) {
            (C.vlan_tci != nullptr) + (C.l3_offset != nullptr) + (C.src_ipv6 != nullptr) + (C.dst_ipv6 != nullptr);
 }
 
-// Inclusive scan over the wave: DPP row_shr 1/2/4/8 inside each 16-lane row,
-// then row_bcast:15 and row_bcast:31 carry the row totals forward.
-__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, true);   // row_shr:1
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, true);   // row_shr:2
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, true);   // row_shr:4
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, true);   // row_shr:8
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
-    return v;
-}
-
 constexpr int kStreamStep = 4096;   // bytes per step: 64 lanes x 64 B
 
 template <int S>

@@ -89,3 +89,69 @@ def test_ring_ships_compact_descriptors_and_full_ones_for_long_frames():
     assert sum(b.n for b in got) == len(offs)
     for c in ALL_COLUMNS:
         assert np.array_equal(np.concatenate([b.records[c] for b in got]), rec[c]), c
+
+
+@pytest.mark.parametrize("kind", ["5", "0"])
+def test_compact_any_order_overlaps_empty_and_max_length(kind, monkeypatch):
+    """Descriptor batches the flat kernel (kind 5, the compact default) and the
+    mixed kernel (kind 0) must both take: frames in shuffled order, frames that
+    overlap other frames, zero-length frames, and 65535-B frames (the compact
+    maximum) at every alignment — every column equal to the oracle."""
+    monkeypatch.setenv("PNETGPU_RX_KIND", kind)
+    rng = np.random.default_rng(404)
+    frames = framegen.random_frames(rng, 3000, max_len=3000) + framegen.edge_frames(rng)
+    buf, offs, lens = framegen.pack(frames, gap=7, rng=rng)
+    offs, lens = offs.astype(np.uint64), lens.astype(np.uint32)
+    big = rng.integers(0, 256, 70000, dtype=np.uint8)
+    big[12:14] = (8, 0)
+    big[14] = 0x45
+    base = buf.size
+    buf = np.concatenate([buf, big, np.zeros(32, np.uint8)])
+    extra_o = [base + a for a in (0, 1, 7, 15, 16, 4000)] + [int(o) + 3 for o in offs[:200:7]] + [5, 9, base]
+    extra_l = [65535, 65535, 65535, 65535, 60000, 65535 - 4000] + [max(0, int(l) - 5) for l in lens[:200:7]] + [0, 0, 0]
+    offs = np.concatenate([offs, np.array(extra_o, np.uint64)])
+    lens = np.concatenate([lens, np.array(extra_l, np.uint32)])
+    perm = rng.permutation(len(offs))
+    offs, lens = offs[perm], lens[perm]
+    rec = coracle.rx_batch(buf, len(offs), offsets=offs, lengths=lens)
+    res = run_compact(to_dev(buf), offs, lens)
+    compare(res, rec)
+    assert res.counter_dict() == oracle_counters(rec, lens)
+
+
+def test_compact_tx_fill_equals_oracle():
+    """tx_fill_checksums over compact descriptors (the flat kernel's TX
+    instantiation): patched bytes and pre-patch records equal oracle_tx_fill."""
+    rng = np.random.default_rng(405)
+    frames = framegen.random_frames(rng, 4000, max_len=1600)
+    buf, offs, lens = framegen.pack(frames, gap=3, rng=rng)
+    want_buf, want_rec = coracle.tx_fill(buf, len(offs), offsets=offs, lengths=lens)
+    d = to_dev(buf)
+    res = lp.tx_fill_checksums(d, offsets=to_dev(np.asarray(offs, np.uint32).view(np.int32)),
+                               lengths=to_dev(np.asarray(lens, np.uint16).view(np.int16)), columns=ALL_COLUMNS,
+                               flags=lp.DESC_COMPACT)
+    torch.cuda.synchronize()
+    assert np.array_equal(d.cpu().numpy(), want_buf)
+    compare(res, want_rec)
+
+
+@pytest.mark.parametrize("flags", [0, 3])
+def test_flat_kernel_random_frames_and_tx(flags, monkeypatch):
+    """The opt-in flat kernel (PNETGPU_RX_KIND=5) on random and extension frames
+    with every column, and its TX instantiation, against the oracle."""
+    monkeypatch.setenv("PNETGPU_RX_KIND", "5")
+    rng = np.random.default_rng(406 + flags)
+    frames = framegen.extension_frames(rng) + framegen.random_frames(rng, 3000, max_len=9100)
+    buf, offs, lens = framegen.pack(frames, gap=11, rng=rng)
+    rec = coracle.rx_batch(buf, len(frames), offsets=offs, lengths=lens, flags=flags)
+    res = run_compact(to_dev(buf), offs, lens, flags=flags)
+    compare(res, rec)
+    assert res.counter_dict() == oracle_counters(rec, lens)
+    want_buf, want_rec = coracle.tx_fill(buf, len(offs), offsets=offs, lengths=lens, flags=flags)
+    d = to_dev(buf)
+    res = lp.tx_fill_checksums(d, offsets=to_dev(np.asarray(offs, np.uint32).view(np.int32)),
+                               lengths=to_dev(np.asarray(lens, np.uint16).view(np.int16)), columns=ALL_COLUMNS,
+                               flags=flags | lp.DESC_COMPACT)
+    torch.cuda.synchronize()
+    assert np.array_equal(d.cpu().numpy(), want_buf)
+    compare(res, want_rec)
