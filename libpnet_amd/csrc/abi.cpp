@@ -226,10 +226,20 @@ static int slices_common(pnetgpu_ctx* ctx, const uint8_t* data, uint64_t data_by
     a.extra_offsets = extra_offsets;
     a.extra_lengths = extra_lengths;
     a.out = out;
-    const uint64_t groups_per_block = kBlock / 16;
-    const uint64_t want = (n + groups_per_block - 1) / groups_per_block;
+    // Kernel choice (slice lengths are device-resident, so by the batch's bytes
+    // per slice): slice_run_kernel, one wave per 64 slices, each slice of at most
+    // 4 granules summed by its own lane, for batches averaging <= 256 B per
+    // slice (9.4x on the reference's 20-B bench shape, same box); slice_kernel,
+    // one 16-lane group per slice in grid-stride order, for longer slices (the
+    // run kernel's per-wave slice ranges ran 1-KiB slices 16 % slower) and for
+    // every *_adv batch. PNETGPU_SLICE_KERNEL=run|group overrides.
+    const char* kenv = std::getenv("PNETGPU_SLICE_KERNEL");
+    bool run = !extra_offsets && data_bytes / n <= 256;
+    if (kenv && !extra_offsets) run = kenv[0] == 'r' ? true : kenv[0] == 'g' ? false : run;
+    const uint64_t per_block = run ? kBlock : kBlock / 16;
+    const uint64_t want = (n + per_block - 1) / per_block;
     const int blocks = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)ctx->cus * 8));
-    if (const int e = pnetgpu::launch_slices(a, pseudo, blocks, static_cast<hipStream_t>(stream))) {
+    if (const int e = pnetgpu::launch_slices(a, pseudo, run, blocks, static_cast<hipStream_t>(stream))) {
         pnetgpu::set_last_hip_error(e);
         return PNETGPU_EHIP;
     }

@@ -61,7 +61,7 @@ int rx_waves_per_block(int kind);
 // both return the hipError_t of the launch (0 = hipSuccess); errors pending
 // from earlier, unrelated HIP calls are cleared first
 int launch_rx(const RxArgs& args, int kind, int blocks, bool tx, hipStream_t stream);
-int launch_slices(const SliceArgs& args, int pseudo, int blocks, hipStream_t stream);
+int launch_slices(const SliceArgs& args, int pseudo, bool run, int blocks, hipStream_t stream);
 // the HIP error code behind the last PNETGPU_EHIP a launch returned on this thread
 int last_hip_error();
 void set_last_hip_error(int e);

@@ -179,14 +179,25 @@ int launch_rx(const RxArgs& args, int kind, int blocks, bool tx, hipStream_t str
     return (int)hipGetLastError();
 }
 
-int launch_slices(const SliceArgs& args, int pseudo, int blocks, hipStream_t stream) {
+int launch_slices(const SliceArgs& args, int pseudo, bool run, int blocks, hipStream_t stream) {
     const bool extra = args.extra_offsets != nullptr;
     (void)hipGetLastError();
-    if (pseudo == 0) hipLaunchKernelGGL((slice_kernel<0, false>), dim3(blocks), dim3(kBlock), 0, stream, args);
-    else if (pseudo == 4 && !extra) hipLaunchKernelGGL((slice_kernel<4, false>), dim3(blocks), dim3(kBlock), 0, stream, args);
-    else if (pseudo == 4) hipLaunchKernelGGL((slice_kernel<4, true>), dim3(blocks), dim3(kBlock), 0, stream, args);
-    else if (!extra) hipLaunchKernelGGL((slice_kernel<16, false>), dim3(blocks), dim3(kBlock), 0, stream, args);
-    else hipLaunchKernelGGL((slice_kernel<16, true>), dim3(blocks), dim3(kBlock), 0, stream, args);
+    if (run && !extra) {
+        if (pseudo == 0) hipLaunchKernelGGL((slice_run_kernel<0>), dim3(blocks), dim3(kBlock), 0, stream, args);
+        else if (pseudo == 4) hipLaunchKernelGGL((slice_run_kernel<4>), dim3(blocks), dim3(kBlock), 0, stream, args);
+        else hipLaunchKernelGGL((slice_run_kernel<16>), dim3(blocks), dim3(kBlock), 0, stream, args);
+    } else if (pseudo == 0) {
+        if (extra) return -1;   // util::checksum has no extra slice
+        hipLaunchKernelGGL((slice_kernel<0, false>), dim3(blocks), dim3(kBlock), 0, stream, args);
+    } else if (pseudo == 4 && !extra) {
+        hipLaunchKernelGGL((slice_kernel<4, false>), dim3(blocks), dim3(kBlock), 0, stream, args);
+    } else if (pseudo == 4) {
+        hipLaunchKernelGGL((slice_kernel<4, true>), dim3(blocks), dim3(kBlock), 0, stream, args);
+    } else if (!extra) {
+        hipLaunchKernelGGL((slice_kernel<16, false>), dim3(blocks), dim3(kBlock), 0, stream, args);
+    } else {
+        hipLaunchKernelGGL((slice_kernel<16, true>), dim3(blocks), dim3(kBlock), 0, stream, args);
+    }
     return (int)hipGetLastError();
 }
 

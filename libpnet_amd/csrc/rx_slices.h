@@ -120,5 +120,120 @@ __global__ __launch_bounds__(kBlock) void slice_kernel(SliceArgs a) {
     }
 }
 
+// slice_run_kernel: the same results without the extra slice (util::checksum,
+// ipv4_checksum, ipv6_checksum), for batches of any slice sizes but built for
+// small ones (the reference's own bench shape is a 20-B slice,
+// checksum_benchmarks.rs:8-12). One wave per run of 64 slices, lane l <-> slice
+// l: coalesced descriptor loads, a slice of at most kSmall granules summed by
+// its own lane (all its loads issued at once, with the two skipped-word bytes),
+// longer slices listed and summed by 16-lane groups as in slice_kernel, and one
+// coalesced 2-B store per lane. slice_kernel gave 16 lanes to every slice: a
+// 20-B slice left 14 of them idle and the results went out as 2-B stores
+// scattered 32 B apart.
+template <int PSEUDO>
+__global__ __launch_bounds__(kBlock) void slice_run_kernel(SliceArgs a) {
+    constexpr int kSmall = 4;    // granules summed by the slice's own lane
+    constexpr int G = 16;
+    __shared__ uint32_t gsum[kWavesPerBlock][kWave];
+    __shared__ uint8_t glist[kWavesPerBlock][kWave];
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wv = threadIdx.x / kWave;
+    const uint64_t nruns = (a.n + kWave - 1) / kWave;
+    const uint64_t wave_stride = (uint64_t)gridDim.x * kWavesPerBlock;
+    for (uint64_t run = (uint64_t)blockIdx.x * kWavesPerBlock + wv; run < nruns; run += wave_stride) {
+        const uint64_t i = run * kWave + lane;
+        const bool in = i < a.n;
+        uint64_t off = 0;
+        uint32_t len = 0, skip = 0;
+        if (in) {
+            off = a.offsets[i] + a.delta;
+            len = a.lengths[i];
+            skip = a.skipwords[i];
+            if (off > a.limit || (uint64_t)len > a.limit - off) {
+                len = 0;
+                off = 0;
+            }
+        }
+        const int sh = (int)(off & 15);
+        const uint8_t* fb = a.data + (off - (uint64_t)sh);
+        const int e = sh + (int)len;
+        const uint32_t nneed = len ? (uint32_t)((e + 15) >> 4) : 0u;
+        const bool small = nneed <= (uint32_t)kSmall;
+        // skipped word: its bytes [2 skip, 2 skip + 2) that lie in the slice (util.rs:166-178)
+        const uint64_t q = 2ull * skip;
+        const bool s0 = q < len, s1 = q + 1 < len;
+        uint32_t b0 = 0, b1 = 0;                 // in flight across the group phase
+        if (s0) b0 = a.data[off + q];
+        if (s1) b1 = a.data[off + q + 1];
+        // slices past kSmall granules: 16-lane groups over the wave's list of them
+        // (before the small slices' loads: no granule registers held across it)
+        const uint64_t bmask = __ballot(in && !small);
+        if (bmask) {
+            if (in && !small) glist[wv][__popcll(bmask & ((1ull << lane) - 1ull))] = (uint8_t)lane;
+            wave_sync();
+            const int nb = __popcll(bmask);
+            const int j = lane % G;
+            for (int k0 = 0; k0 < nb; k0 += kWave / G) {   // wave-uniform; a group's lanes share k
+                const int k = k0 + lane / G;
+                const int sl = k < nb ? glist[wv][k] : 0;
+                // both shuffles unconditional: a shuffle under `k < nb` would read
+                // its source lane with that lane masked off
+                const uint64_t soff = (uint64_t)__shfl((unsigned long long)off, sl);
+                const uint32_t sl_len = (uint32_t)__shfl((int)len, sl);
+                const uint32_t slen = k < nb ? sl_len : 0u;
+                const uint32_t t = group_range_sum(a.data, soff, slen, j);
+                if (k < nb && j == 0) gsum[wv][sl] = t;
+            }
+            wave_sync();
+        }
+        uint4 v[kSmall];
+#pragma unroll
+        for (int c = 0; c < kSmall; ++c)
+            v[c] = small && (uint32_t)c < nneed ? load16(fb + 16 * c) : make_uint4(0, 0, 0, 0);
+        uint32_t acc = 0;
+        if (small) {
+#pragma unroll
+            for (int c = 0; c < kSmall; ++c) {
+                const uint32_t dw[4] = {v[c].x, v[c].y, v[c].z, v[c].w};
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    const int p = 16 * c + 4 * t;
+                    acc = sad(dw[t] & first_bytes(clamp04(e - p)) & ~first_bytes(clamp04(sh - p)), acc);
+                }
+            }
+        } else {
+            acc = gsum[wv][lane];
+        }
+        acc -= s0 ? (((off + q) & 1) ? (b0 << 8) : b0) : 0u;
+        acc -= s1 ? (((off + q + 1) & 1) ? (b1 << 8) : b1) : 0u;
+        uint32_t p = fold16(acc);
+        if (!(off & 1)) p = bswap16(p);
+        uint32_t r;
+        if (PSEUDO == 0) {
+            r = len ? ((~p) & 0xFFFFu) : 0u;                    // util.rs:77-79
+        } else {
+            uint32_t s = 0;
+            if (in) {
+                const uint8_t* ad = a.addrs + i * (2 * PSEUDO);
+                if (!(reinterpret_cast<uintptr_t>(a.addrs) & 3u)) {   // wave-uniform
+#pragma unroll
+                    for (int k = 0; k < 2 * PSEUDO; k += 4) {
+                        const uint32_t w = *reinterpret_cast<const uint32_t*>(ad + k);   // 4 octets, LE load
+                        s += bswap16(w & 0xFFFFu) + bswap16(w >> 16);
+                    }
+                } else {
+#pragma unroll
+                    for (int k = 0; k < 2 * PSEUDO; k += 2) s += ((uint32_t)ad[k] << 8) | ad[k + 1];
+                }
+                s += a.protos[i];
+            }
+            s += len + p;                                        // util.rs:103-113
+            r = (~fold16(s)) & 0xFFFFu;
+        }
+        if (in) a.out[i] = (uint16_t)r;
+        wave_sync();   // glist / gsum are rewritten by the next run
+    }
+}
+
 }  // namespace
 }  // namespace pnetgpu

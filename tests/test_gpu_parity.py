@@ -405,7 +405,9 @@ def test_idempotent_and_stream_ordered():
         assert torch.equal(a.columns[c], b.columns[c])
 
 
-def test_random_slices_vs_oracle():
+@pytest.mark.parametrize("kernel", ["run", "group"])
+def test_random_slices_vs_oracle(kernel, monkeypatch):
+    monkeypatch.setenv("PNETGPU_SLICE_KERNEL", kernel)   # slice_run_kernel / slice_kernel
     rng = np.random.default_rng(21)
     n = 20000
     buf = rng.integers(0, 256, 1 << 22, dtype=np.uint8)
@@ -428,6 +430,48 @@ def test_random_slices_vs_oracle():
             h = alen // 2
             assert got[i] == ofn(bytes(buf[o:o + ln]), int(skips[i]), b"", bytes(a[i, :h]), bytes(a[i, h:]),
                                  int(protos[i])), i
+
+
+@pytest.mark.parametrize("kernel", ["run", "group"])
+@pytest.mark.parametrize("seed", [0, 1])
+def test_small_and_large_slices_mixed_in_runs(seed, kernel, monkeypatch):
+    """slice_run_kernel: tiny slices (0-70 B, summed by their own lane) and long
+    ones (group path) interleaved in the same 64-slice runs, at every alignment,
+    skipwords inside / straddling / past the slice, invalid descriptors, and a
+    batch size that is not a multiple of 64; pseudo-header forms with the
+    address array at a 4-B-aligned and an odd address. Both slice kernels."""
+    monkeypatch.setenv("PNETGPU_SLICE_KERNEL", kernel)
+    rng = np.random.default_rng(600 + seed)
+    n = 64 * 300 + 17
+    buf = rng.integers(0, 256, 1 << 21, dtype=np.uint8)
+    lens = rng.integers(0, 71, n).astype(np.uint32)
+    big = rng.random(n) < 0.2
+    lens[big] = rng.integers(71, 5000, int(big.sum()))
+    offs = rng.integers(0, buf.size - 5100, n).astype(np.uint64)
+    skips = np.where(rng.random(n) < 0.5, rng.integers(0, 40, n), rng.integers(0, 3000, n)).astype(np.uint32)
+    bad = rng.choice(n, 40, replace=False)
+    offs[bad[:20]] = buf.size + rng.integers(0, 1000, 20)
+    lens[bad[20:]] = (buf.size - offs[bad[20:]] + rng.integers(1, 50, 20)).astype(np.uint32)
+    rec_off = np.where(offs > buf.size, 0, offs)
+    rec_len = np.where((offs > buf.size) | (offs + lens > buf.size), 0, lens).astype(np.uint32)
+    want = coracle.checksum_slices(buf, rec_off, rec_len, skips)
+    d = to_dev(buf)
+    do, dl, ds = to_dev(offs.astype(np.int64)), to_dev(lens.astype(np.int32)), to_dev(skips.astype(np.int32))
+    got = lp.checksum_slices(d, do, dl, ds).cpu().numpy().view(np.uint16)
+    assert np.array_equal(got, want)
+    protos = rng.integers(0, 256, n, dtype=np.uint8)
+    for fn, alen, ofn in ((lp.ipv4_checksum_slices, 8, coracle.ipv4_checksum),
+                          (lp.ipv6_checksum_slices, 32, coracle.ipv6_checksum)):
+        raw = rng.integers(0, 256, n * alen + 1, dtype=np.uint8)
+        for shift in (0, 1):                    # the addrs array 4-B aligned, then at an odd address
+            a_dev = to_dev(raw)[shift:shift + n * alen].view(n, alen)
+            a = raw[shift:shift + n * alen].reshape(n, alen)
+            got = fn(d, do, dl, ds, a_dev, to_dev(protos)).cpu().numpy().view(np.uint16)
+            h = alen // 2
+            for i in list(range(0, n, 41)) + [int(x) for x in bad]:
+                o, ln = int(rec_off[i]), int(rec_len[i])
+                assert got[i] == ofn(bytes(buf[o:o + ln]), int(skips[i]), b"", bytes(a[i, :h]), bytes(a[i, h:]),
+                                     int(protos[i])), (alen, shift, i)
 
 
 def test_random_adv_slices_vs_oracle():
