@@ -43,7 +43,7 @@ def main():
     for name, n, size, fn in cases:
         ms = float(np.median(times[name]))
         print(f"{name:12s} {ms * 1e3:8.1f} us  {n / ms / 1e6:9.1f} Mslices/s  "
-              f"{n * (size + 18) / ms / 1e9:7.0f} GB/s alg", flush=True)
+              f"{n * (size + 18) / ms / 1e6:7.0f} GB/s alg", flush=True)
 
 
 if __name__ == "__main__":
