@@ -58,11 +58,12 @@ def log(*a):
 class Shard:
     """One workload resident on this rank's GPU, with its result buffers."""
 
-    def __init__(self, name, n, seed, device):
-        self.name, self.n = name, n
+    def __init__(self, name, n, seed, device, first=0):
+        self.name, self.n, self.first = name, n, first
         cfg = WORKLOADS.get(name, {})
         columns = cfg.get("columns", lp.IPV4_COLUMNS)
-        w = lp.synth.make(cfg.get("synth", name), n, seed=seed, corrupt_ppm=10000)
+        # frames [first, first + n) of the global batch `seed` defines
+        w = lp.synth.make(cfg.get("synth", name), n, seed=seed, corrupt_ppm=10000, first=first)
         self.w = w
         self.data = torch.from_numpy(w.buf).to(device)
         self.offsets = self.lengths = None
@@ -650,7 +651,19 @@ def main():
         cfg = WORKLOADS[name]
         t = time.perf_counter()
         n = max(64, int(cfg["n"] * args.frames_scale))
-        sh = Shard(name, n, args.seed * 1000 + rank, device)
+        # one global batch of world x n frames (the same seed on every rank), each
+        # rank building and processing its shard: by frame index for the
+        # fixed-size workloads, byte-balanced (shard.shard_by_bytes) for IMIX
+        # (the configs[3] partition); weak scaling: n per GPU
+        gname = cfg.get("synth", name)
+        if gname == "imix":
+            lo, hi = shard.shard_by_bytes(lp.synth.lengths(gname, n * world, args.seed * 1000), world, rank)
+            partition = "shard_by_bytes"
+        else:
+            lo, hi = shard.shard_by_index(n * world, world, rank)
+            partition = "shard_by_index"
+        sh = Shard(name, hi - lo, args.seed * 1000, device, first=lo)
+        sh.partition = partition
         if dist_on:
             # the host copy only serves the N=1 extras (CPU baseline, PCIe lines);
             # with 8 ranks on a node it would hold ~50 GB of host memory for nothing
@@ -664,13 +677,15 @@ def main():
         ctr_t = torch.tensor([ctr[k] for k in lp.COUNTER_NAMES] + [int(ok)], dtype=torch.int64, device=device)
         shard.all_reduce_counters(ctr_t)
         wall = shard.all_reduce_max(wall, device)
-        frames_all = sh.n * world * args.steps
+        n_all = torch.tensor([sh.n], dtype=torch.int64, device=device)
+        shard.all_reduce_counters(n_all)              # frames of the whole batch (the shards' sum)
+        frames_all = int(n_all.item()) * args.steps
         achieved = sh.alg_bytes / (avg_ms * 1e-3) / 1e9
         results[name] = {
             "sh": sh, "wall": wall, "ms_per_step": wall / args.steps * 1e3,
             "mpkts_s": frames_all / wall / 1e6,
-            "gb_s": sh.frame_bytes * world * args.steps / wall / 1e9,
-            "kernel_avg_ms": avg_ms,
+            "gb_s": int(ctr_t[lp.COUNTER_NAMES.index("bytes")].item()) * args.steps / wall / 1e9,
+            "kernel_avg_ms": avg_ms, "frames_per_step": frames_all // args.steps,
             "achieved_gbs": achieved, "counters_ok": bool(ctr_t[-1].item() == world),
             "counters": {k: int(v) for k, v in zip(lp.COUNTER_NAMES, ctr_t[:-1].tolist())},
         }
@@ -703,7 +718,8 @@ def main():
                 "batch_bytes_per_gpu": sh.frame_bytes,
                 "mode": "fixed-stride" if sh.w.stride else "descriptor",
                 "result_bytes_per_frame": sh.result_bytes,
-                "parallelism": f"shard-by-index x{world}",
+                "parallelism": f"{getattr(sh, 'partition', 'shard_by_index')} x{world}",
+                "global_batch_frames": results[primary]["frames_per_step"],
                 **({"frames_scale": args.frames_scale} if args.frames_scale != 1.0 else {}),
             },
             "gb_s": round(p["gb_s"], 1),

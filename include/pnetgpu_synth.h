@@ -41,6 +41,17 @@ int pnetgpu_synth_fill(int workload, uint64_t n, uint64_t seed, uint32_t corrupt
                        uint8_t* buf, uint64_t buf_bytes, uint64_t* offsets, uint32_t* lengths,
                        uint64_t expect[PNETGPU_SYNTH_NEXP], int nthreads);
 
+/* The same for frames [first, first + n) of a batch (frame i depends only on
+ * seed and i): one shard of a global batch, byte-identical to those frames of
+ * the whole batch. pnetgpu_synth_lengths writes the frame lengths of that range
+ * without building anything (a byte-balanced split of IMIX, shard_by_bytes). */
+int pnetgpu_synth_layout_range(int workload, uint64_t first, uint64_t n, uint64_t seed, uint64_t* total_bytes,
+                               uint32_t* stride, uint32_t* frame_len);
+int pnetgpu_synth_fill_range(int workload, uint64_t first, uint64_t n, uint64_t seed, uint32_t corrupt_ppm,
+                             uint8_t* buf, uint64_t buf_bytes, uint64_t* offsets, uint32_t* lengths,
+                             uint64_t expect[PNETGPU_SYNTH_NEXP], int nthreads);
+int pnetgpu_synth_lengths(int workload, uint64_t first, uint64_t n, uint64_t seed, uint32_t* lengths);
+
 #ifdef __cplusplus
 }
 #endif

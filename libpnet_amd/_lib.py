@@ -108,6 +108,13 @@ def _load():
                                        ctypes.POINTER(u32)]
     L.pnetgpu_synth_fill.restype = i32
     L.pnetgpu_synth_fill.argtypes = [i32, u64, u64, u32, vp, u64, vp, vp, vp, i32]
+    L.pnetgpu_synth_layout_range.restype = i32
+    L.pnetgpu_synth_layout_range.argtypes = [i32, u64, u64, u64, ctypes.POINTER(u64), ctypes.POINTER(u32),
+                                             ctypes.POINTER(u32)]
+    L.pnetgpu_synth_fill_range.restype = i32
+    L.pnetgpu_synth_fill_range.argtypes = [i32, u64, u64, u64, u32, vp, u64, vp, vp, vp, i32]
+    L.pnetgpu_synth_lengths.restype = i32
+    L.pnetgpu_synth_lengths.argtypes = [i32, u64, u64, u64, vp]
     if L.pnetgpu_abi_version() != DEFS["PNETGPU_ABI_VERSION"]:
         raise ImportError("libpnet_amd: libpnetgpu.so ABI version does not match include/pnetgpu.h")
     return L

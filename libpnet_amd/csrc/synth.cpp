@@ -212,7 +212,8 @@ Built build(int workload, uint64_t seed, uint64_t i, uint32_t corrupt_ppm, uint8
     return b;
 }
 
-bool layout(int workload, uint64_t n, uint64_t seed, uint64_t* total, uint32_t* stride, uint32_t* flen) {
+bool layout(int workload, uint64_t first, uint64_t n, uint64_t seed, uint64_t* total, uint32_t* stride,
+            uint32_t* flen) {
     switch (workload) {
         case PNETGPU_SYNTH_RS_SENDER:
         case PNETGPU_SYNTH_UDP64: *stride = 64; break;
@@ -226,7 +227,7 @@ bool layout(int workload, uint64_t n, uint64_t seed, uint64_t* total, uint32_t* 
     if (*stride) {
         bytes = n * (uint64_t)*stride;
     } else {
-        for (uint64_t i = 0; i < n; ++i) bytes += imix_len(seed, i);
+        for (uint64_t i = first; i < first + n; ++i) bytes += imix_len(seed, i);
     }
     *total = (bytes + 15) / 16 * 16 + 16;
     return true;
@@ -249,23 +250,39 @@ void parallel_for(uint64_t n, int nthreads, F fn) {
 
 extern "C" {
 
-int pnetgpu_synth_layout(int workload, uint64_t n, uint64_t seed, uint64_t* total_bytes, uint32_t* stride,
-                         uint32_t* frame_len) {
-    if (!total_bytes || !stride || !frame_len) return PNETGPU_EINVAL;
-    return layout(workload, n, seed, total_bytes, stride, frame_len) ? PNETGPU_OK : PNETGPU_EINVAL;
+int pnetgpu_synth_layout_range(int workload, uint64_t first, uint64_t n, uint64_t seed, uint64_t* total_bytes,
+                               uint32_t* stride, uint32_t* frame_len) {
+    if (!total_bytes || !stride || !frame_len || n > UINT64_MAX - first) return PNETGPU_EINVAL;
+    return layout(workload, first, n, seed, total_bytes, stride, frame_len) ? PNETGPU_OK : PNETGPU_EINVAL;
 }
 
-int pnetgpu_synth_fill(int workload, uint64_t n, uint64_t seed, uint32_t corrupt_ppm, uint8_t* buf,
-                       uint64_t buf_bytes, uint64_t* offsets, uint32_t* lengths,
-                       uint64_t expect[PNETGPU_SYNTH_NEXP], int nthreads) {
+int pnetgpu_synth_layout(int workload, uint64_t n, uint64_t seed, uint64_t* total_bytes, uint32_t* stride,
+                         uint32_t* frame_len) {
+    return pnetgpu_synth_layout_range(workload, 0, n, seed, total_bytes, stride, frame_len);
+}
+
+int pnetgpu_synth_lengths(int workload, uint64_t first, uint64_t n, uint64_t seed, uint32_t* lengths) {
     uint64_t total = 0;
     uint32_t stride = 0, flen = 0;
-    if (!buf || !layout(workload, n, seed, &total, &stride, &flen) || buf_bytes < total) return PNETGPU_EINVAL;
+    if (!lengths || n > UINT64_MAX - first || !layout(workload, 0, 0, seed, &total, &stride, &flen))
+        return PNETGPU_EINVAL;
+    for (uint64_t i = 0; i < n; ++i) lengths[i] = stride ? stride : imix_len(seed, first + i);
+    return PNETGPU_OK;
+}
+
+int pnetgpu_synth_fill_range(int workload, uint64_t first, uint64_t n, uint64_t seed, uint32_t corrupt_ppm,
+                             uint8_t* buf, uint64_t buf_bytes, uint64_t* offsets, uint32_t* lengths,
+                             uint64_t expect[PNETGPU_SYNTH_NEXP], int nthreads) {
+    uint64_t total = 0;
+    uint32_t stride = 0, flen = 0;
+    if (!buf || n > UINT64_MAX - first || !layout(workload, first, n, seed, &total, &stride, &flen) ||
+        buf_bytes < total)
+        return PNETGPU_EINVAL;
     if (stride == 0 && (!offsets || !lengths)) return PNETGPU_EINVAL;
     if (stride == 0) {
         uint64_t pos = 0;
         for (uint64_t i = 0; i < n; ++i) {
-            const uint32_t l = imix_len(seed, i);
+            const uint32_t l = imix_len(seed, first + i);
             offsets[i] = pos;
             lengths[i] = l;
             pos += l;
@@ -278,7 +295,7 @@ int pnetgpu_synth_fill(int workload, uint64_t n, uint64_t seed, uint32_t corrupt
         for (uint64_t i = lo; i < hi; ++i) {
             const uint64_t off = stride ? i * stride : offsets[i];
             const uint32_t l = stride ? stride : lengths[i];
-            Built r = build(workload, seed, i, corrupt_ppm, buf + off, l);
+            Built r = build(workload, seed, first + i, corrupt_ppm, buf + off, l);   // frame first + i of the batch
             a += r.ip_bad;
             b += r.l4_bad;
             c += l;
@@ -294,6 +311,13 @@ int pnetgpu_synth_fill(int workload, uint64_t n, uint64_t seed, uint32_t corrupt
         }
     }
     return PNETGPU_OK;
+}
+
+int pnetgpu_synth_fill(int workload, uint64_t n, uint64_t seed, uint32_t corrupt_ppm, uint8_t* buf,
+                       uint64_t buf_bytes, uint64_t* offsets, uint32_t* lengths,
+                       uint64_t expect[PNETGPU_SYNTH_NEXP], int nthreads) {
+    return pnetgpu_synth_fill_range(workload, 0, n, seed, corrupt_ppm, buf, buf_bytes, offsets, lengths, expect,
+                                    nthreads);
 }
 
 }  // extern "C"

@@ -25,16 +25,26 @@ class Workload:
         self.expect = {"ip_bad": int(expect[0]), "l4_bad": int(expect[1]), "bytes": int(expect[2])}
 
 
-def layout(name, n, seed=0):
+def layout(name, n, seed=0, first=0):
     tot, st, fl = ctypes.c_uint64(), ctypes.c_uint32(), ctypes.c_uint32()
-    check(lib.pnetgpu_synth_layout(WORKLOADS[name], n, seed, ctypes.byref(tot), ctypes.byref(st),
-                                   ctypes.byref(fl)), "pnetgpu_synth_layout")
+    check(lib.pnetgpu_synth_layout_range(WORKLOADS[name], first, n, seed, ctypes.byref(tot), ctypes.byref(st),
+                                         ctypes.byref(fl)), "pnetgpu_synth_layout_range")
     return tot.value, st.value, fl.value
 
 
-def make(name, n, seed=0, corrupt_ppm=10000, nthreads=None, buf=None):
-    """Build n frames of a workload. `buf` may be a preallocated (e.g. pinned) uint8 array/tensor."""
-    total, stride, flen = layout(name, n, seed)
+def lengths(name, n, seed=0, first=0):
+    """Frame lengths of frames [first, first + n) of a workload's batch (nothing built)."""
+    out = np.empty(n, dtype=np.uint32)
+    check(lib.pnetgpu_synth_lengths(WORKLOADS[name], first, n, seed, ctypes.c_void_p(out.ctypes.data)),
+          "pnetgpu_synth_lengths")
+    return out
+
+
+def make(name, n, seed=0, corrupt_ppm=10000, nthreads=None, buf=None, first=0):
+    """Build n frames of a workload: frames [first, first + n) of the batch `seed`
+    defines (a shard of a global batch, byte-identical to those frames of the
+    whole batch). `buf` may be a preallocated (e.g. pinned) uint8 array/tensor."""
+    total, stride, flen = layout(name, n, seed, first)
     if buf is None:
         buf = np.empty(total, dtype=np.uint8)
     addr = buf.ctypes.data if isinstance(buf, np.ndarray) else buf.data_ptr()
@@ -45,8 +55,8 @@ def make(name, n, seed=0, corrupt_ppm=10000, nthreads=None, buf=None):
         lengths = np.empty(n, dtype=np.uint32)
     exp = (ctypes.c_uint64 * 3)()
     nthreads = nthreads or min(16, os.cpu_count() or 1)
-    check(lib.pnetgpu_synth_fill(WORKLOADS[name], n, seed, corrupt_ppm, ctypes.c_void_p(addr), size,
-                                 ctypes.c_void_p(offsets.ctypes.data if offsets is not None else 0),
-                                 ctypes.c_void_p(lengths.ctypes.data if lengths is not None else 0),
-                                 exp, nthreads), "pnetgpu_synth_fill")
+    check(lib.pnetgpu_synth_fill_range(WORKLOADS[name], first, n, seed, corrupt_ppm, ctypes.c_void_p(addr), size,
+                                       ctypes.c_void_p(offsets.ctypes.data if offsets is not None else 0),
+                                       ctypes.c_void_p(lengths.ctypes.data if lengths is not None else 0),
+                                       exp, nthreads), "pnetgpu_synth_fill_range")
     return Workload(name, n, buf, stride, flen, offsets, lengths, list(exp))

@@ -99,3 +99,7 @@ def test_bench_two_ranks_one_gpu():
     assert line["n_gpus"] == 2 and line["counters_ok"] is True
     assert line["workloads"]["imix"]["counters_ok"] is True
     assert line["config"]["frames_scale"] == 0.01
+    # one global batch, sharded: the two ranks' frames add up to it
+    assert line["config"]["global_batch_frames"] == 2 * int((1 << 24) * 0.01)
+    assert line["config"]["parallelism"] == "shard_by_index x2"
+    assert line["workloads"]["imix"]["counters_ok"] is True

@@ -41,3 +41,22 @@ def test_deterministic_across_threads():
     a = lp.synth.make("imix", 30000, seed=9, nthreads=1)
     b = lp.synth.make("imix", 30000, seed=9, nthreads=7)
     assert (a.buf == b.buf).all() and (a.offsets == b.offsets).all()
+
+
+@pytest.mark.parametrize("name", ["udp64", "imix", "tcp1500"])
+def test_range_is_a_slice_of_the_whole_batch(name):
+    """pnetgpu_synth_fill_range: frames [first, first + n) equal those frames of the
+    whole batch byte for byte (a rank's shard of the bench's global batch), and
+    pnetgpu_synth_lengths gives their lengths without building them."""
+    whole = lp.synth.make(name, 700, seed=9)
+    part = lp.synth.make(name, 250, seed=9, first=333)
+    if whole.stride:
+        s = whole.stride
+        assert np.array_equal(part.buf[:250 * s], whole.buf[333 * s:583 * s])
+    else:
+        lo = int(whole.offsets[333])
+        hi = int(whole.offsets[582] + whole.lengths[582])
+        assert np.array_equal(part.buf[:hi - lo], whole.buf[lo:hi])
+        assert np.array_equal(part.lengths, whole.lengths[333:583])
+    assert np.array_equal(lp.synth.lengths(name, 250, seed=9, first=333),
+                          whole.lengths[333:583] if not whole.stride else np.full(250, whole.stride, np.uint32))
