@@ -157,6 +157,13 @@ void launch_t(const RxArgs& args, int kind, int blocks, hipStream_t stream) {
 
 }  // namespace
 
+// Resident blocks of the small kernel: 4 per CU (4 waves/SIMD) measured best
+// from 3 to 8 in one process (udp64 274 us at 4 vs 285-303 us at 5-8; its 75
+// VGPRs would allow 6), tools/kbench.py --env PNETGPU_BLOCKS_PER_CU.
+#ifndef PNET_SMALL_BLOCKS
+#define PNET_SMALL_BLOCKS 4
+#endif
+
 int rx_blocks_per_cu(int kind, bool ext, int* numregs, int* lds) {
     const void* fn = ext ? pick_fn<true, false>(kind) : pick_fn<false, false>(kind);
     hipFuncAttributes fa;
@@ -164,7 +171,8 @@ int rx_blocks_per_cu(int kind, bool ext, int* numregs, int* lds) {
         if (numregs) *numregs = fa.numRegs;
         if (lds) *lds = (int)fa.sharedSizeBytes;
     }
-    return resident_blocks(fn, kind == kKindStream ? kWave : kBlock);
+    const int nb = resident_blocks(fn, kind == kKindStream ? kWave : kBlock);
+    return kind == kKindSmall && nb > PNET_SMALL_BLOCKS ? PNET_SMALL_BLOCKS : nb;
 }
 
 int rx_waves_per_block(int kind) { return kind == kKindStream ? 1 : kWavesPerBlock; }
