@@ -5,10 +5,10 @@
  * C-ABI. The host only indexes the file (pnetgpu_pcap_scan), ships the records
  * straight from the mapped file (pnetgpu_ring_submit_region) and prints one
  * line per frame from the result columns, in packetdump's formats
- * (packetdump.rs:31-217). Bytes no column carries are read from the frame the
- * way packetdump's zero-copy views read them: UDP get_length (udp.rs),
- * ICMP echo identifier / sequence_number (icmp.rs:222-232, 304-314), MAC
- * addresses and the ARP fields (arp.rs:83-104).
+ * (packetdump.rs:31-217): the record columns plus the header-field columns
+ * packetdump prints — Ethernet source/destination MacAddr, UDP get_length,
+ * ICMP echo sequence_number (its identifier is dst_port). Only the ARP fields
+ * (arp.rs:83-104; ARP is outside the GPU path) are read from the frame bytes.
  *
  * Raw-IP captures (LINKTYPE_RAW / IPV4 / IPV6, e.g. from a tun device) run with
  * PNETGPU_RX_L3: packetdump's tun branch (packetdump.rs:250-283) wraps such
@@ -50,14 +50,19 @@
 #include "pnetgpu_afpacket.h"
 #include "pnetgpu_ring.h"
 
+/* the record columns + the header fields packetdump prints */
+#define DUMP_COLUMNS (PNETGPU_COLS_RECORD | PNETGPU_COL_ETH_DST | PNETGPU_COL_ETH_SRC | PNETGPU_COL_UDP_LENGTH | \
+                      PNETGPU_COL_ICMP_SEQUENCE)
+
 static const char* g_name = "pcap";
 static int g_csum = 0;
 static int g_l3 = 0;   /* raw-IP capture: no Ethernet header */
 
 static unsigned be16(const uint8_t* p) { return ((unsigned)p[0] << 8) | p[1]; }
 
-static void fmt_mac(char* out, const uint8_t* m) {
-    sprintf(out, "%02x:%02x:%02x:%02x:%02x:%02x", m[0], m[1], m[2], m[3], m[4], m[5]);
+static void fmt_mac(char* out, uint64_t m) {   /* column value: MacAddr octets as a BE-valued u48 */
+    sprintf(out, "%02x:%02x:%02x:%02x:%02x:%02x", (unsigned)(m >> 40) & 255u, (unsigned)(m >> 32) & 255u,
+            (unsigned)(m >> 24) & 255u, (unsigned)(m >> 16) & 255u, (unsigned)(m >> 8) & 255u, (unsigned)m & 255u);
 }
 
 static void fmt_v4(char* out, uint32_t be) {   /* column value: octets as a big-endian-valued u32 */
@@ -123,8 +128,8 @@ static void dump_frame(const pnetgpu_ring_batch* b, uint64_t i) {
     if (l3 == 0) {   /* packetdump.rs:202-217: ARP, otherwise unknown */
         const unsigned et = c->ethertype[i];
         char sm[24], dm[24];
-        fmt_mac(dm, f);
-        fmt_mac(sm, f + 6);
+        fmt_mac(dm, c->eth_dst[i]);
+        fmt_mac(sm, c->eth_src[i]);
         if (et == 0x0806) {
             if (len - 14 < 28) {
                 printf("[%s]: Malformed ARP Packet\n", g_name);
@@ -151,13 +156,12 @@ static void dump_frame(const pnetgpu_ring_batch* b, uint64_t i) {
     }
     csum_suffix(sfx, st);
     const unsigned l4len = c->l4_length[i];
-    const uint8_t* l4 = f + c->l4_offset[i];
     const int bad = (st & PNET_ST_L4_MALFORMED) != 0;
     switch (st & PNET_ST_L4_MASK) {
     case PNET_ST_L4_UDP:
         if (bad) printf("[%s]: Malformed UDP Packet\n", g_name);
         else printf("[%s]: UDP Packet: %s:%u > %s:%u; length: %u%s\n", g_name, src, c->src_port[i], dst,
-                    c->dst_port[i], be16(l4 + 4), sfx);
+                    c->dst_port[i], c->udp_length[i], sfx);
         return;
     case PNET_ST_L4_TCP:
         if (bad) printf("[%s]: Malformed TCP Packet\n", g_name);
@@ -170,7 +174,7 @@ static void dump_frame(const pnetgpu_ring_batch* b, uint64_t i) {
             printf("[%s]: Malformed ICMP Packet\n", g_name);
         } else if (type == 0 || type == 8) {
             printf("[%s]: ICMP echo %s %s -> %s (seq=%u, id=%u)%s\n", g_name, type ? "request" : "reply", src, dst,
-                   be16(l4 + 6), be16(l4 + 4), sfx);
+                   c->icmp_sequence[i], c->dst_port[i], sfx);
         } else {
             printf("[%s]: ICMP packet %s -> %s (type=IcmpType(%u))%s\n", g_name, src, dst, type, sfx);
         }
@@ -221,6 +225,7 @@ static int live(const char* ifname, long long count, int idle_ms) {
     pnetgpu_ring* ring = NULL;
     if (!rc) rc = pnetgpu_ctx_create(0, &ctx);
     if (!rc) rc = pnetgpu_ring_create(ctx, 64u << 20, 1u << 18, 0, &ring);
+    if (!rc) rc = pnetgpu_ring_set_columns(ring, DUMP_COLUMNS);
     /* a TPACKET_V3 packet takes at least its 48-B header plus 16-B-aligned data */
     const uint64_t cap = block_bytes / 64u + 1u;
     uint64_t* offs = (uint64_t*)malloc(sizeof(uint64_t) * cap);
@@ -304,6 +309,7 @@ int main(int argc, char** argv) {
     pnetgpu_ring* ring = NULL;
     if (!rc) rc = pnetgpu_ctx_create(0, &ctx);
     if (!rc) rc = pnetgpu_ring_create(ctx, 64u << 20, 1u << 18, flags, &ring);
+    if (!rc) rc = pnetgpu_ring_set_columns(ring, DUMP_COLUMNS);
     enum { kCap = 1 << 16 };
     uint64_t* offs = (uint64_t*)malloc(sizeof(uint64_t) * kCap);
     uint32_t* lens = (uint32_t*)malloc(sizeof(uint32_t) * kCap);

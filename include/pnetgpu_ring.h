@@ -82,6 +82,31 @@ int pnetgpu_ring_submit_region(pnetgpu_ring* ring, const uint8_t* base, const ui
  * the IPv4 set, bits 0-11: 26 B/frame; all 38: 114 B/frame). Growing the record
  * returns PNETGPU_EBUSY while a batch is in flight or held. */
 int pnetgpu_ring_set_columns(pnetgpu_ring* ring, uint64_t column_mask);
+/* column_mask bits: the 16 record columns, then the header-field columns */
+#define PNETGPU_COLS_RECORD            0xFFFFull     /* status ... l3_offset (the default) */
+#define PNETGPU_COLS_IPV4_RECORD       0x0FFFull     /* status ... dst_ipv4: 26 B/frame   */
+#define PNETGPU_COL_ETH_DST            (1ull << 16)
+#define PNETGPU_COL_ETH_SRC            (1ull << 17)
+#define PNETGPU_COL_IP_VERSION         (1ull << 18)
+#define PNETGPU_COL_IP_HEADER_LENGTH   (1ull << 19)
+#define PNETGPU_COL_IP_DSCP            (1ull << 20)
+#define PNETGPU_COL_IP_ECN             (1ull << 21)
+#define PNETGPU_COL_IP_TOTAL_LENGTH    (1ull << 22)
+#define PNETGPU_COL_IP_IDENTIFICATION  (1ull << 23)
+#define PNETGPU_COL_IP_FLAGS           (1ull << 24)
+#define PNETGPU_COL_IP_FRAGMENT_OFFSET (1ull << 25)
+#define PNETGPU_COL_IP6_TRAFFIC_CLASS  (1ull << 26)
+#define PNETGPU_COL_IP6_FLOW_LABEL     (1ull << 27)
+#define PNETGPU_COL_IP6_PAYLOAD_LENGTH (1ull << 28)
+#define PNETGPU_COL_UDP_LENGTH         (1ull << 29)
+#define PNETGPU_COL_TCP_SEQUENCE       (1ull << 30)
+#define PNETGPU_COL_TCP_ACKNOWLEDGEMENT (1ull << 31)
+#define PNETGPU_COL_TCP_DATA_OFFSET    (1ull << 32)
+#define PNETGPU_COL_TCP_RESERVED       (1ull << 33)
+#define PNETGPU_COL_TCP_FLAGS          (1ull << 34)
+#define PNETGPU_COL_TCP_WINDOW         (1ull << 35)
+#define PNETGPU_COL_TCP_URGENT_PTR     (1ull << 36)
+#define PNETGPU_COL_ICMP_SEQUENCE      (1ull << 37)
 /* Page-lock existing host memory for direct DMA (hipHostRegister) and undo it. */
 int pnetgpu_host_register(void* p, uint64_t bytes);
 int pnetgpu_host_unregister(void* p);
