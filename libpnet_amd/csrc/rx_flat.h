@@ -112,68 +112,70 @@ __global__ __launch_bounds__(kBlock, 4) void rx_flat_kernel(RxArgs a) {
         }
 
         // ---- 2. the flat rounds: window entries -> slots, every entry summed ---
-        // Software-pipelined: round r+1's U loads are issued before round r's
-        // entries are processed, so the wave keeps loads in flight while it sums.
-        uint4 v[U], vn[U];           // this round's granules, the next round's
-        uint32_t kc[U], kn[U];       // their entries' compact frame indices
-        auto issue = [&](uint32_t q0, uint4 (&dst)[U], uint32_t (&kq)[U]) {
+        // Lane l takes U consecutive entries of the round, [q0 + U l, q0 + U l + U):
+        // its frame lookups are one mask word per round, its sums a running
+        // prefix in registers, and one wave scan per round (not per entry) turns
+        // the lanes' totals into P. The U loads of an instruction are 16 B per
+        // lane at a 16 U-byte stride; the U instructions together cover the
+        // round's entries whole.
+        uint32_t carry = 0;
+        for (uint32_t q0 = 0; q0 < total; q0 += kRound) {
             if (lane < U) L.mask[lane] = 0;
             wave_sync();
             if (n && cum >= q0 && cum < q0 + kRound)
                 atomicOr(reinterpret_cast<unsigned long long*>(&L.mask[(cum - q0) >> 6]), 1ull << (cum & 63u));
             wave_sync();
-            uint64_t m[U];
+            const uint32_t e0 = (uint32_t)(U * lane);                 // round-relative first entry
+            const uint32_t blk = e0 >> 6;
+            uint32_t pre = 0;                                          // frames starting before my block
 #pragma unroll
-            for (int u = 0; u < U; ++u) m[u] = L.mask[u];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const uint32_t b0 = q0 + 64u * u;
-                const uint32_t before = (uint32_t)__popcll(__ballot(n && cum < b0));
-                const uint32_t k = before + mbcnt64(m[u]) + (uint32_t)((m[u] >> lane) & 1u);
-                kq[u] = k ? min(k - 1u, (uint32_t)kWave - 1u) : 0u;
+            for (int bb = 0; bb < U; ++bb) {
+                const uint32_t c = (uint32_t)__popcll(__ballot(n && cum < q0 + 64u * bb));
+                pre = blk == (uint32_t)bb ? c : pre;
             }
-            uint2 am[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) am[u] = *reinterpret_cast<const uint2*>(&L.info[kq[u]]);
+            const uint64_t m = L.mask[blk];
+            uint4 in[U];
+            uint4 v[U];
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-                const uint32_t q = min(q0 + 64u * u + (uint32_t)lane, total - 1u);   // past the end: reload
-                const uint64_t amin = ((uint64_t)am[u].y << 32) | am[u].x;
-                dst[u] = load16(a.data + amin + 16ull * q);
+                const uint32_t pos = (e0 + u) & 63u;
+                const uint64_t upto = pos == 63u ? ~0ull : ((2ull << pos) - 1ull);
+                const uint32_t k = pre + (uint32_t)__popcll(m & upto);
+                in[u] = L.info[k ? min(k - 1u, (uint32_t)kWave - 1u) : 0u];
             }
-        };
-        uint32_t carry = 0;
-        if (total) issue(0u, v, kc);
-        for (uint32_t q0 = 0; q0 < total; q0 += kRound) {
-            const bool more = q0 + kRound < total;           // wave-uniform
-            if (more) issue(q0 + kRound, vn, kn);
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-                const uint32_t q = q0 + 64u * u + (uint32_t)lane;
+                const uint32_t q = min(q0 + e0 + u, total - 1u);      // past the end: reload
+                const uint64_t amin = ((uint64_t)in[u].y << 32) | in[u].x;
+                v[u] = load16(a.data + amin + 16ull * q);
+            }
+            uint32_t run_sum[U];
+            uint32_t acc = 0;
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t q = q0 + e0 + u;
                 const bool valid = q < total;
-                const uint2 zw = *reinterpret_cast<const uint2*>(&L.info[kc[u]].z);   // cum, fend | lane << 24
-                const uint32_t j = q - zw.x;
-                const uint32_t fe = zw.y & 0xFFFFFFu;
-                const int fl = (int)(zw.y >> 24);
-                const uint32_t nk = (fe + 15u) >> 4;
+                const uint32_t j = q - in[u].z;
+                const int fl = (int)(in[u].w >> 24);
                 if (valid && j < (uint32_t)NW) {                 // window granule -> the frame's slot
                     uint32_t* dst = reinterpret_cast<uint32_t*>(L.win + fl * kSlot + 16 * j);
                     dst[0] = v[u].x; dst[1] = v[u].y; dst[2] = v[u].z; dst[3] = v[u].w;
                 }
-                const uint32_t c = valid ? sad(v[u].w, sad(v[u].z, sad(v[u].y, sad(v[u].x, 0u)))) : 0u;
-                const uint32_t sc = wave_incl_scan(c);
-                const uint32_t p = carry + sc;
-                carry += (uint32_t)__builtin_amdgcn_readlane((int)sc, kWave - 1);
-                if (valid && nk > (uint32_t)NW) {
-                    if (j == (uint32_t)NW - 1u) L.pwin[fl] = p;
-                    if (j == nk - 1u) L.pend[fl] = p;
-                }
+                acc += valid ? sad(v[u].w, sad(v[u].z, sad(v[u].y, sad(v[u].x, 0u)))) : 0u;
+                run_sum[u] = acc;
             }
-            if (more) {
+            const uint32_t incl = wave_incl_scan(acc);
+            const uint32_t base_p = carry + incl - acc;               // P before my first entry
+            carry += (uint32_t)__builtin_amdgcn_readlane((int)incl, kWave - 1);
 #pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    v[u] = vn[u];
-                    kc[u] = kn[u];
+            for (int u = 0; u < U; ++u) {
+                const uint32_t q = q0 + e0 + u;
+                const uint32_t j = q - in[u].z;
+                const uint32_t nk = ((in[u].w & 0xFFFFFFu) + 15u) >> 4;
+                const int fl = (int)(in[u].w >> 24);
+                if (q < total && nk > (uint32_t)NW) {
+                    if (j == (uint32_t)NW - 1u) L.pwin[fl] = base_p + run_sum[u];
+                    if (j == nk - 1u) L.pend[fl] = base_p + run_sum[u];
                 }
             }
         }
