@@ -41,7 +41,7 @@ template <int NW, int U>
 struct FlatLds {
     static constexpr int kSlot = NW * 16 + 4;   // +4 B pad: conflict-free parse reads
     uint8_t win[kWave * kSlot];
-    uint4 info[kWave];         // compact frame index -> {amin lo, amin hi, cum, fend | lane << 24}
+    uint4 info[kWave];         // compact frame index -> {amin lo, amin hi, cum, granules | lane << 24}
     uint32_t pwin[kWave];      // by lane: P at the frame's last window entry
     uint32_t pend[kWave];      // by lane: P at the frame's last entry
     uint64_t mask[U];          // this round's blocks: entries where a frame starts
@@ -108,7 +108,7 @@ __global__ __launch_bounds__(kBlock, 4) void rx_flat_kernel(RxArgs a) {
         if (n) {
             const uint32_t k = mbcnt64(nz);
             const uint64_t amin = base - 16ull * cum;        // entry q of this frame is at amin + 16 q
-            L.info[k] = make_uint4((uint32_t)amin, (uint32_t)(amin >> 32), cum, fend | ((uint32_t)lane << 24));
+            L.info[k] = make_uint4((uint32_t)amin, (uint32_t)(amin >> 32), cum, n | ((uint32_t)lane << 24));
         }
 
         // ---- 2. the flat rounds: window entries -> slots, every entry summed ---
@@ -118,15 +118,15 @@ __global__ __launch_bounds__(kBlock, 4) void rx_flat_kernel(RxArgs a) {
         // the lanes' totals into P. The U loads of an instruction are 16 B per
         // lane at a 16 U-byte stride; the U instructions together cover the
         // round's entries whole.
-        uint32_t carry = 0;
-        for (uint32_t q0 = 0; q0 < total; q0 += kRound) {
+        const uint32_t e0 = (uint32_t)(U * lane);                     // round-relative first entry
+        const uint32_t blk = e0 >> 6;
+        // issue round q0: its masks, its entries' frames, their U loads
+        auto issue = [&](uint32_t q0, uint4 (&v)[U], uint2 (&zw)[U]) {
             if (lane < U) L.mask[lane] = 0;
             wave_sync();
             if (n && cum >= q0 && cum < q0 + kRound)
                 atomicOr(reinterpret_cast<unsigned long long*>(&L.mask[(cum - q0) >> 6]), 1ull << (cum & 63u));
             wave_sync();
-            const uint32_t e0 = (uint32_t)(U * lane);                 // round-relative first entry
-            const uint32_t blk = e0 >> 6;
             uint32_t pre = 0;                                          // frames starting before my block
 #pragma unroll
             for (int bb = 0; bb < U; ++bb) {
@@ -134,13 +134,15 @@ __global__ __launch_bounds__(kBlock, 4) void rx_flat_kernel(RxArgs a) {
                 pre = blk == (uint32_t)bb ? c : pre;
             }
             const uint64_t m = L.mask[blk];
+            // my first entry's frame from the mask, the next ones by the start bits
+            // (a lane's U entries are consecutive, so they sit in one mask word)
+            const uint32_t pos0 = e0 & 63u;
+            const uint32_t bits = (uint32_t)(m >> pos0);             // start bits of my U entries
+            uint32_t k = pre + (uint32_t)__popcll(pos0 ? (m & ((1ull << pos0) - 1ull)) : 0ull);
             uint4 in[U];
-            uint4 v[U];
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-                const uint32_t pos = (e0 + u) & 63u;
-                const uint64_t upto = pos == 63u ? ~0ull : ((2ull << pos) - 1ull);
-                const uint32_t k = pre + (uint32_t)__popcll(m & upto);
+                k += (bits >> u) & 1u;
                 in[u] = L.info[k ? min(k - 1u, (uint32_t)kWave - 1u) : 0u];
             }
 #pragma unroll
@@ -148,15 +150,24 @@ __global__ __launch_bounds__(kBlock, 4) void rx_flat_kernel(RxArgs a) {
                 const uint32_t q = min(q0 + e0 + u, total - 1u);      // past the end: reload
                 const uint64_t amin = ((uint64_t)in[u].y << 32) | in[u].x;
                 v[u] = load16(a.data + amin + 16ull * q);
+                zw[u] = make_uint2(in[u].z, in[u].w);
             }
+        };
+        uint4 v[U], vn[U];
+        uint2 zw[U], zwn[U];
+        uint32_t carry = 0;
+        if (total) issue(0u, v, zw);
+        for (uint32_t q0 = 0; q0 < total; q0 += kRound) {
+            const bool more = q0 + kRound < total;                     // wave-uniform
+            if (more) issue(q0 + kRound, vn, zwn);                     // in flight while this round is summed
             uint32_t run_sum[U];
             uint32_t acc = 0;
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const uint32_t q = q0 + e0 + u;
                 const bool valid = q < total;
-                const uint32_t j = q - in[u].z;
-                const int fl = (int)(in[u].w >> 24);
+                const uint32_t j = q - zw[u].x;
+                const int fl = (int)(zw[u].y >> 24);
                 if (valid && j < (uint32_t)NW) {                 // window granule -> the frame's slot
                     uint32_t* dst = reinterpret_cast<uint32_t*>(L.win + fl * kSlot + 16 * j);
                     dst[0] = v[u].x; dst[1] = v[u].y; dst[2] = v[u].z; dst[3] = v[u].w;
@@ -170,12 +181,19 @@ __global__ __launch_bounds__(kBlock, 4) void rx_flat_kernel(RxArgs a) {
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const uint32_t q = q0 + e0 + u;
-                const uint32_t j = q - in[u].z;
-                const uint32_t nk = ((in[u].w & 0xFFFFFFu) + 15u) >> 4;
-                const int fl = (int)(in[u].w >> 24);
+                const uint32_t j = q - zw[u].x;
+                const uint32_t nk = zw[u].y & 0xFFFFFFu;
+                const int fl = (int)(zw[u].y >> 24);
                 if (q < total && nk > (uint32_t)NW) {
                     if (j == (uint32_t)NW - 1u) L.pwin[fl] = base_p + run_sum[u];
                     if (j == nk - 1u) L.pend[fl] = base_p + run_sum[u];
+                }
+            }
+            if (more) {
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    v[u] = vn[u];
+                    zw[u] = zwn[u];
                 }
             }
         }
