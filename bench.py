@@ -45,6 +45,9 @@ WORKLOADS = {
     # configs[1]'s frames with the verify-only record (status + both computed
     # checksums, R = 6 B/frame; SURVEY.md §8(d) priced the target with R = 8):
     # the same kernel, a consumer that reads no extracted fields
+    "imix_verify": {"n": 1 << 22, "synth": "imix", "columns": ("status", "ip_csum", "l4_csum"),
+                    "kernel": "rx_kernel<8, 4, 8, false, 0, true, false> (mixed)",
+                    "desc": "configs[3] frames, checksum verify only (status + ip_csum + l4_csum columns)"},
     "udp64_verify": {"n": 1 << 24, "synth": "udp64", "columns": ("status", "ip_csum", "l4_csum"),
                      "kernel": "rx_small_kernel",
                      "desc": "configs[1] frames, checksum verify only (status + ip_csum + l4_csum columns)"},
@@ -603,7 +606,7 @@ def main():
                     help="ranks (one per GPU); without WORLD_SIZE set, N > 1 starts them with torchrun")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workloads", default="udp64,tcp1500,imix,udp6_jumbo,udp64_verify",
+    ap.add_argument("--workloads", default="udp64,tcp1500,imix,udp6_jumbo,udp64_verify,imix_verify",
                     help="first one is the headline `value`; the others are reported under `workloads`")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")

@@ -156,10 +156,9 @@ __global__ __launch_bounds__(kBlock, 4) void rx_flat_kernel(RxArgs a) {
         uint4 v[U], vn[U];
         uint2 zw[U], zwn[U];
         uint32_t carry = 0;
-        if (total) issue(0u, v, zw);
-        for (uint32_t q0 = 0; q0 < total; q0 += kRound) {
-            const bool more = q0 + kRound < total;                     // wave-uniform
-            if (more) issue(q0 + kRound, vn, zwn);                     // in flight while this round is summed
+        // sum round q0 (granules v, frame info zw) into the prefix and record
+        // the frames' P at their last window entry and their last entry
+        auto process = [&](uint32_t q0, const uint4 (&v)[U], const uint2 (&zw)[U]) {
             uint32_t run_sum[U];
             uint32_t acc = 0;
 #pragma unroll
@@ -189,12 +188,23 @@ __global__ __launch_bounds__(kBlock, 4) void rx_flat_kernel(RxArgs a) {
                     if (j == nk - 1u) L.pend[fl] = base_p + run_sum[u];
                 }
             }
-            if (more) {
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    v[u] = vn[u];
-                    zw[u] = zwn[u];
-                }
+        };
+        // Two register sets used in turn (a copy of in-flight load registers
+        // would wait for them), and every path that sums a round either issued
+        // the next round first or issues none, so the compiler's wait counts
+        // let the sums start while the next round's loads are in flight.
+        if (total) {
+            issue(0u, v, zw);
+            uint32_t q0 = 0;
+            while (true) {
+                if (q0 + kRound >= total) { process(q0, v, zw); break; }
+                issue(q0 + kRound, vn, zwn);                           // in flight while this round is summed
+                process(q0, v, zw);
+                q0 += kRound;
+                if (q0 + kRound >= total) { process(q0, vn, zwn); break; }
+                issue(q0 + kRound, v, zw);
+                process(q0, vn, zwn);
+                q0 += kRound;
             }
         }
         wave_sync();
