@@ -138,8 +138,10 @@ __device__ __forceinline__ void tail_sums(const uint8_t* data, WaveLds<NW>& L, i
 // header-field columns may be requested; the plain instantiation compiles the
 // parse without those branches (half the code, SGPR spills 118 -> 14, IMIX -2 %).
 template <int NW, int G, int U, bool NT, int PASS, bool DYN, bool EXT, bool TX>
-__global__ __launch_bounds__(kBlock, 4) void rx_kernel(RxArgs a) {
-    static_assert(NW == 8, "window granules");
+__global__ __launch_bounds__(kBlock, NW < 8 ? 5 : 4) void rx_kernel(RxArgs a) {
+    // the window must hold every field the parse reads near (Ethernet + 2 VLAN
+    // tags + the fixed IPv4 header / IPv6 addresses: 82 B) after a 15-B shift
+    static_assert(NW >= 7 || NW == 6, "window granules");
     static_assert(G == 4 || G == 8 || G == 16 || G == 32 || G == 64, "tail group");
     constexpr int kSlot = WaveLds<NW>::kSlot;
     constexpr int kWin = NW * 16;
@@ -253,10 +255,12 @@ __global__ __launch_bounds__(kBlock, 4) void rx_kernel(RxArgs a) {
         if (desc_bad) P.st = PNET_ST_DESC_INVALID;
         else if (in_batch)
             P = parse_frame(FrameBytes{slot + sh, a.data + off, kWin - sh}, len, EXT ? a.flags : 0u);
-        // A (<= 97 B into the frame) always lies in the window; B may run past it
+        // A (<= 97 B into the frame) lies in the window unless the window is
+        // shorter than 8 granules (IPv4 options past it); B may run past it
         const int p0 = P.a_lo + sh, p1 = P.a_hi + sh, p2 = P.b_lo + sh, p3 = P.b_hi + sh;
         uint32_t tA = 0, tB = 0;
-        window_sums(slot, p0, p1, min(p2, kWin), min(p3, kWin), tA, tB);
+        window_sums(slot, p0, min(p1, kWin), min(p2, kWin), min(p3, kWin), tA, tB);
+        if (NW < 8 && p1 > kWin) tA += lane_range_sum(a.data + base, kWin, p1);
         if (P.l4do && p3 > kWin) {
             // B past the window = the speculative tail minus [kWin, p2) and [p3, fend)
             tB += L.tail[lane];

@@ -106,7 +106,11 @@ static int resident_blocks(const void* fn, int block_threads) {
 #ifndef PNET_JUMBO_CFG
 #define PNET_JUMBO_CFG 64, 9, true, 0, false
 #endif
-#define PNET_MIXED_FN(EXT, TX) rx_kernel<8, PNET_MIXED_CFG, EXT, TX>
+// window granules of the mixed shape (6: 96-B window, 5 blocks/CU by LDS)
+#ifndef PNET_MIXED_NW
+#define PNET_MIXED_NW 8
+#endif
+#define PNET_MIXED_FN(EXT, TX) rx_kernel<PNET_MIXED_NW, PNET_MIXED_CFG, EXT, TX>
 #define PNET_JUMBO_FN(EXT, TX) rx_kernel<8, PNET_JUMBO_CFG, EXT, TX>
 
 // loads in flight per lane per round of the flat kernel
