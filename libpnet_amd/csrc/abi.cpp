@@ -166,7 +166,8 @@ static int rx_common(pnetgpu_ctx* ctx, const pnetgpu_batch* b, const pnetgpu_rx_
     if (kind_env) {
         const int v = std::atoi(kind_env);
         if ((v == pnetgpu::kKindMixed || v == pnetgpu::kKindMtu || v == pnetgpu::kKindJumbo ||
-             (v == pnetgpu::kKindStream && stream_ok) || (v == pnetgpu::kKindFlat && a.desc_compact)) &&
+             (v == pnetgpu::kKindStream && stream_ok) || (v == pnetgpu::kKindFlat && a.desc_compact) ||
+             (v == pnetgpu::kKindSplit && !tx)) &&
             kind != pnetgpu::kKindSmall)
             kind = v;
     }

@@ -66,6 +66,7 @@
 #include "rx_generic.h"
 #include "rx_stream.h"
 #include "rx_flat.h"
+#include "rx_split.h"
 #include "rx_slices.h"
 
 namespace pnetgpu {
@@ -122,6 +123,10 @@ static int resident_blocks(const void* fn, int block_threads) {
 #ifndef PNET_STREAM_SLOTS
 #define PNET_STREAM_SLOTS 3
 #endif
+// LDS ring steps of the split kernel's streaming wave
+#ifndef PNET_SPLIT_SLOTS
+#define PNET_SPLIT_SLOTS 4
+#endif
 
 template <bool EXT, bool TX>
 const void* pick_fn(int kind) {
@@ -131,6 +136,7 @@ const void* pick_fn(int kind) {
     case kKindJumbo: return reinterpret_cast<const void*>(PNET_JUMBO_FN(EXT, TX));
     case kKindStream: return reinterpret_cast<const void*>(rx_stream_kernel<PNET_STREAM_SLOTS, EXT>);
     case kKindFlat: return reinterpret_cast<const void*>(rx_flat_kernel<PNET_FLAT_U, EXT, TX>);
+    case kKindSplit: return reinterpret_cast<const void*>(rx_split_kernel<PNET_SPLIT_SLOTS, EXT>);
     default: return reinterpret_cast<const void*>(PNET_MIXED_FN(EXT, TX));
     }
 }
@@ -154,6 +160,10 @@ void launch_t(const RxArgs& args, int kind, int blocks, hipStream_t stream) {
         if (!TX)
             hipLaunchKernelGGL((rx_stream_kernel<PNET_STREAM_SLOTS, EXT>), dim3(blocks), dim3(kWave), 0, stream, args);
         break;
+    case kKindSplit:    // receive only
+        if (!TX)
+            hipLaunchKernelGGL((rx_split_kernel<PNET_SPLIT_SLOTS, EXT>), dim3(blocks), dim3(2 * kWave), 0, stream, args);
+        break;
     default:
         hipLaunchKernelGGL((PNET_MIXED_FN(EXT, TX)), dim3(blocks), dim3(kBlock), 0, stream, args);
     }
@@ -175,11 +185,12 @@ int rx_blocks_per_cu(int kind, bool ext, int* numregs, int* lds) {
         if (numregs) *numregs = fa.numRegs;
         if (lds) *lds = (int)fa.sharedSizeBytes;
     }
-    const int nb = resident_blocks(fn, kind == kKindStream ? kWave : kBlock);
+    const int nb = resident_blocks(fn, kind == kKindStream ? kWave : kind == kKindSplit ? 2 * kWave : kBlock);
     return kind == kKindSmall && nb > PNET_SMALL_BLOCKS ? PNET_SMALL_BLOCKS : nb;
 }
 
-int rx_waves_per_block(int kind) { return kind == kKindStream ? 1 : kWavesPerBlock; }
+// runs per block per pass: the split kernel's block (two waves) takes one run at a time
+int rx_waves_per_block(int kind) { return kind == kKindStream || kind == kKindSplit ? 1 : kWavesPerBlock; }
 
 int launch_rx(const RxArgs& args, int kind, int blocks, bool tx, hipStream_t stream) {
     // EXT instantiations: dispatch extensions (flags; never with the small kernel)
