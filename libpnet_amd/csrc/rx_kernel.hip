@@ -162,7 +162,7 @@ void launch_t(const RxArgs& args, int kind, int blocks, hipStream_t stream) {
         break;
     case kKindSplit:    // receive only
         if (!TX)
-            hipLaunchKernelGGL((rx_split_kernel<PNET_SPLIT_SLOTS, EXT>), dim3(blocks), dim3(2 * kWave), 0, stream, args);
+            hipLaunchKernelGGL((rx_split_kernel<PNET_SPLIT_SLOTS, EXT>), dim3(blocks), dim3(3 * kWave), 0, stream, args);
         break;
     default:
         hipLaunchKernelGGL((PNET_MIXED_FN(EXT, TX)), dim3(blocks), dim3(kBlock), 0, stream, args);
@@ -185,7 +185,7 @@ int rx_blocks_per_cu(int kind, bool ext, int* numregs, int* lds) {
         if (numregs) *numregs = fa.numRegs;
         if (lds) *lds = (int)fa.sharedSizeBytes;
     }
-    const int nb = resident_blocks(fn, kind == kKindStream ? kWave : kind == kKindSplit ? 2 * kWave : kBlock);
+    const int nb = resident_blocks(fn, kind == kKindStream ? kWave : kind == kKindSplit ? 3 * kWave : kBlock);
     return kind == kKindSmall && nb > PNET_SMALL_BLOCKS ? PNET_SMALL_BLOCKS : nb;
 }
 

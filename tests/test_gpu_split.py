@@ -172,3 +172,24 @@ def test_header_field_columns():
     rec = coracle.rx_batch(buf, len(frames), offsets=offs, lengths=lens)
     res = rx(to_dev(buf), offs, lens, columns=ALL_COLUMNS)
     compare(res, rec)
+
+
+@pytest.mark.parametrize("per_cu", ["1", "2"])
+def test_many_runs_per_block(per_cu, monkeypatch):
+    """Few blocks (PNETGPU_BLOCKS_PER_CU) so every block takes several runs —
+    odd and even counts, the pair schedule's last period with one run — with
+    every fifth run spread out (per-lane path) between streamed ones."""
+    monkeypatch.setenv("PNETGPU_BLOCKS_PER_CU", per_cu)
+    rng = np.random.default_rng(610)
+    n = 64 * 1000 + 33
+    frames = framegen.random_frames(rng, n, max_len=600)
+    buf, offs, lens = framegen.pack(frames, gap=0, rng=rng)
+    offs, lens = offs.astype(np.uint64).copy(), lens.astype(np.uint32).copy()
+    for r in range(3, n // 64, 5):
+        sl = slice(64 * r, 64 * r + 64)
+        p = rng.permutation(n)[:64]
+        offs[sl], lens[sl] = offs[p], lens[p]
+    rec = coracle.rx_batch(buf, n, offsets=offs, lengths=lens)
+    res = rx(to_dev(buf), offs, lens)
+    compare(res, rec)
+    assert res.counter_dict() == oracle_counters(rec, lens)
