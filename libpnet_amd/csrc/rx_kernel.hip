@@ -38,11 +38,18 @@
 //                   tail from prefix sums of the byte stream; bit-exact, 1.00x
 //                   traffic, slower than rx_kernel here.
 //
+//  rx_split_kernel  opt-in (PNETGPU_RX_KIND=6), any batch, receive only: three-
+//                   wave blocks, one wave streams each run's byte range through
+//                   an LDS-DMA ring (prefix sums give every frame's tail), two
+//                   waves parse and store; bit-exact, slower than rx_kernel on
+//                   IMIX and jumbo frames (profiles/r02/split/).
+//
 //  slice_kernel     the batched util::checksum / ipv4_checksum / ipv6_checksum
 //                   (and *_adv) entry points: 16 lanes per slice.
 //
 // Files: rx_common.h (helpers, parse_frame, window sums, finalize, TX write,
-// counters, column stores), rx_small.h, rx_generic.h, rx_stream.h, rx_slices.h
+// counters, column stores), rx_small.h, rx_generic.h, rx_stream.h, rx_flat.h,
+// rx_split.h, rx_slices.h
 // (one kernel family each), and this file: the launch glue and kernel choice.
 // All are one translation unit.
 //

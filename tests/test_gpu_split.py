@@ -1,5 +1,5 @@
-"""GPU parity of the split kernel (PNETGPU_RX_KIND=6: a streaming wave and a
-parsing wave per block, receive only) against the oracle: packed and gapped
+"""GPU parity of the split kernel (PNETGPU_RX_KIND=6: a streaming wave and two
+parsing waves per block, receive only) against the oracle: packed and gapped
 descriptor batches (compact and full, with and without the parse extensions),
 shuffled / overlapping / empty / 65535-B frames (runs that are not packed take
 the per-lane path), dense and spread runs interleaved, runs of minimum-size
