@@ -142,7 +142,7 @@ __global__ __launch_bounds__(kBlock, NW < 8 ? 5 : 4) void rx_kernel(RxArgs a) {
     // the window must hold every field the parse reads near (Ethernet + 2 VLAN
     // tags + the fixed IPv4 header / IPv6 addresses: 82 B) after a 15-B shift
     static_assert(NW >= 7 || NW == 6, "window granules");
-    static_assert(G == 4 || G == 8 || G == 16 || G == 32 || G == 64, "tail group");
+    static_assert(G == 2 || G == 4 || G == 8 || G == 16 || G == 32 || G == 64, "tail group");
     constexpr int kSlot = WaveLds<NW>::kSlot;
     constexpr int kWin = NW * 16;
 
