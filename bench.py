@@ -335,8 +335,8 @@ def e2e_ring_rate(sh, seconds=3.0):
     el = time.perf_counter() - t0
     ring.close()
     return {"mpkts_s": round(frames / el / 1e6, 1), "gb_s": round(nbytes / el / 1e9, 2),
-            "note": "host frames pushed into the pinned ring with pnetgpu_ring_push_many (source-adjacent "
-                    "frames coalesced, up to 8 copy threads), async H2D -> rx kernel -> D2H of all 16 result "
+            "note": "host frames pushed into the pinned ring with pnetgpu_ring_push_many (descriptors and "
+                    "source-adjacent frame copies split over up to 8 host threads), async H2D -> rx kernel -> D2H of all 16 result "
                     "columns, 3 rotating slots of 1 Mi frames"}
 
 

@@ -8,6 +8,7 @@
 #include <cstring>
 #include <deque>
 #include <new>
+#include <atomic>
 #include <thread>
 #include <vector>
 
@@ -223,23 +224,25 @@ int pnetgpu_ring_push_many(pnetgpu_ring* r, const uint8_t* buf, const uint64_t* 
     Slot& s = r->slots[r->filling];
     // descriptors of the frames that fit, in order (the same cut as pushing one by one)
     const uint64_t room_f = r->cap_frames - s.n;
-    uint64_t k = 0, bytes = 0;
-    while (k < n && k < room_f && lengths[k] <= r->cap_bytes - s.bytes - bytes) {
-        s.h_off[s.n + k] = s.bytes + bytes;
-        s.h_len[s.n + k] = lengths[k];
-        s.h_off32[s.n + k] = (uint32_t)(s.bytes + bytes);
-        s.h_len16[s.n + k] = (uint16_t)lengths[k];
-        s.max_len = std::max(s.max_len, lengths[k]);
-        bytes += lengths[k];
-        ++k;
-    }
-    if (k == 0) return PNETGPU_EFULL;
-    // frame bytes: runs of frames adjacent in the source go in one memcpy; large
-    // pushes are split over host threads (one thread's memcpy into pinned memory
-    // tops out far below the PCIe link the batch is headed for)
+    const uint64_t room_b = r->cap_bytes - s.bytes;
+    const uint64_t m = std::min(n, room_f);
     uint8_t* dst = s.h_frames;
-    const uint64_t* doff = s.h_off + s.n;
-    auto copy_range = [&](uint64_t lo, uint64_t hi) {
+    // frames [lo, hi) with their slot byte offsets starting at `at`: descriptors,
+    // then the bytes (runs of frames adjacent in the source go in one memcpy);
+    // returns the chunk's largest length
+    auto fill_range = [&](uint64_t lo, uint64_t hi, uint64_t at) {
+        uint32_t mx = 0;
+        uint64_t o = at;
+        for (uint64_t i = lo; i < hi; ++i) {
+            const uint32_t len = lengths[i];
+            s.h_off[s.n + i] = o;
+            s.h_len[s.n + i] = len;
+            s.h_off32[s.n + i] = (uint32_t)o;
+            s.h_len16[s.n + i] = (uint16_t)len;
+            mx = std::max(mx, len);
+            o += len;
+        }
+        const uint64_t* doff = s.h_off + s.n;
         uint64_t i = lo;
         while (i < hi) {
             uint64_t j = i + 1;
@@ -248,15 +251,57 @@ int pnetgpu_ring_push_many(pnetgpu_ring* r, const uint8_t* buf, const uint64_t* 
             if (run) std::memcpy(dst + doff[i], buf + offsets[i], run);
             i = j;
         }
+        return mx;
     };
+    // Large pushes are split over host threads, descriptors included: one
+    // thread's memcpy into pinned memory tops out far below the PCIe link the
+    // batch is headed for, and a serial descriptor pass capped 64-B frames at
+    // ~330 Mframes/s end to end. Pass 1 sums each chunk's lengths; when the whole
+    // push fits (every push but the one that fills a slot by bytes), pass 2
+    // fills each chunk at its prefix offset.
+    uint64_t k = 0, bytes = 0;
     unsigned nt = 1;
-    if (bytes >= (8ull << 20)) nt = std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
-    if (nt == 1) {
-        copy_range(0, k);
-    } else {
+    if (m >= (1u << 16)) nt = std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
+    bool done = false;
+    if (nt > 1) {
+        std::vector<uint64_t> csum(nt, 0);
+        std::vector<uint32_t> cmax(nt, 0);
+        std::atomic<unsigned> arrived{0};
+        std::atomic<bool> fits{false};
+        auto work = [&](unsigned t) {
+            const uint64_t lo = m * t / nt, hi = m * (t + 1) / nt;
+            uint64_t sum = 0;
+            for (uint64_t i = lo; i < hi; ++i) sum += lengths[i];
+            csum[t] = sum;
+            if (arrived.fetch_add(1) + 1 == nt) {   // the last to arrive decides
+                uint64_t tot = 0;
+                for (unsigned c = 0; c < nt; ++c) tot += csum[c];
+                fits.store(tot <= room_b, std::memory_order_release);
+                arrived.fetch_add(1);                  // == nt + 1: released
+            }
+            while (arrived.load(std::memory_order_acquire) <= nt) std::this_thread::yield();
+            if (!fits.load(std::memory_order_acquire)) return;
+            uint64_t at = s.bytes;
+            for (unsigned c = 0; c < t; ++c) at += csum[c];
+            cmax[t] = fill_range(lo, hi, at);
+        };
         std::vector<std::thread> th;
-        for (unsigned t = 0; t < nt; ++t) th.emplace_back(copy_range, k * t / nt, k * (t + 1) / nt);
+        for (unsigned t = 1; t < nt; ++t) th.emplace_back(work, t);
+        work(0);
         for (auto& t : th) t.join();
+        if (fits.load()) {
+            k = m;
+            for (unsigned c = 0; c < nt; ++c) {
+                bytes += csum[c];
+                s.max_len = std::max(s.max_len, cmax[c]);
+            }
+            done = true;
+        }
+    }
+    if (!done) {
+        while (k < m && lengths[k] <= room_b - bytes) bytes += lengths[k++];
+        if (k == 0) return PNETGPU_EFULL;
+        s.max_len = std::max(s.max_len, fill_range(0, k, s.bytes));
     }
     s.n += k;
     s.bytes += bytes;

@@ -49,6 +49,36 @@ def test_ring_feed_many_synth():
     assert sum(b.counters["l4_csum_bad"] for b in out) == w.expect["l4_bad"]
 
 
+@pytest.mark.parametrize("batch_bytes", [64 << 20, 8 << 20])
+def test_ring_feed_many_large_pushes(batch_bytes):
+    """Pushes of >= 2^16 frames split their descriptors and copies over host
+    threads; with 8 MiB slots the byte capacity cuts each push (the serial
+    path). Frames are spread with gaps, so copies break at chunk boundaries
+    and inside chunks; batches equal the source frames and the oracle."""
+    w = lp.synth.make("imix", 150000, seed=8)
+    rng = np.random.default_rng(8)
+    gaps = rng.integers(0, 3, w.offsets.size) * rng.integers(0, 40, w.offsets.size)
+    offs = (w.offsets + np.cumsum(gaps)).astype(np.uint64)
+    buf = np.zeros(int(offs[-1] + w.lengths[-1]) + 64, np.uint8)
+    for o, no, n in zip(w.offsets.tolist(), offs.tolist(), w.lengths.tolist()):
+        buf[no:no + n] = w.buf[o:o + n]
+    ring = lp.Ring(batch_bytes=batch_bytes, batch_frames=1 << 18)
+    out = sorted(list(ring.feed_many(buf, offs, w.lengths)) + list(ring.drain()), key=lambda b: b.id)
+    assert [b.id for b in out] == list(range(len(out)))
+    assert sum(b.n for b in out) == offs.size
+    i = 0
+    for b in out:
+        assert np.array_equal(b.lengths, w.lengths[i:i + b.n])
+        assert b.offsets[0] == 0 and np.array_equal(np.diff(b.offsets.astype(np.int64)), b.lengths[:-1])
+        got = np.asarray(b.frames[:int(b.offsets[-1] + b.lengths[-1])])
+        want = np.concatenate([buf[int(o):int(o) + int(l)] for o, l in zip(offs[i:i + b.n], w.lengths[i:i + b.n])])
+        assert np.array_equal(got, want), b.id
+        rec = coracle.rx_batch(b.frames, b.n, offsets=b.offsets, lengths=b.lengths)
+        for c, v in b.records.items():
+            assert np.array_equal(v, rec[c]), (b.id, c)
+        i += b.n
+
+
 @pytest.mark.parametrize("register", [False, True])
 def test_ring_zero_copy_region(register):
     """submit_region ships frames straight from the caller's (pageable or
