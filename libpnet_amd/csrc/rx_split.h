@@ -12,6 +12,11 @@
 #include "rx_generic.h"
 #include "rx_stream.h"
 
+// stream-wave instruction priority (0-3; 0, 1 and 3 measured alike, profiles/r02/split/)
+#ifndef PNET_SPLIT_PRIO
+#define PNET_SPLIT_PRIO 3
+#endif
+
 namespace pnetgpu {
 namespace {
 
@@ -235,9 +240,6 @@ __global__ __launch_bounds__(3 * kWave) void rx_split_kernel(RxArgs a) {
     }
 
     // ================= streaming wave (lane f <-> frame f of the run) =================
-#ifndef PNET_SPLIT_PRIO
-#define PNET_SPLIT_PRIO 3
-#endif
     __builtin_amdgcn_s_setprio(PNET_SPLIT_PRIO);   // its DMA issue comes before the parses' VALU work
     const uint64_t lim16 = a.limit >= 16 ? ((a.limit + 15) & ~15ull) - 16 : 0;   // last readable granule
     const uint32_t src_off = (uint32_t)(lane & ~3) * 16u + ((uint32_t)((lane & 3) - (lane >> 4)) & 3u) * 16u;
