@@ -193,3 +193,18 @@ def test_many_runs_per_block(per_cu, monkeypatch):
     res = rx(to_dev(buf), offs, lens)
     compare(res, rec)
     assert res.counter_dict() == oracle_counters(rec, lens)
+
+
+@pytest.mark.parametrize("flags", [4, 7])
+def test_l3_packets(flags):
+    """PNETGPU_RX_L3 batches (frames begin at the IP header), with and without
+    the other extensions, packed (streamed) at an odd base."""
+    from tests.test_oracle_ext import ip_packets
+    rng = np.random.default_rng(611 + flags)
+    pkts = ip_packets(rng, 3000)
+    buf, offs, lens = framegen.pack(pkts, gap=0, rng=rng)
+    rec = coracle.rx_batch(buf, len(pkts), offsets=offs, lengths=lens, flags=flags)
+    d = to_dev(np.concatenate([np.zeros(16, np.uint8), buf]))[3:]
+    res = rx(d, offs + 13, lens, flags=flags)
+    compare(res, rec)
+    assert res.counter_dict() == oracle_counters(rec, lens)
