@@ -204,9 +204,10 @@ typedef struct pnetgpu_rx_columns {
     uint8_t*  tcp_flags;           /* TcpPacket get_flags (u8)                          (tcp.rs:63)       */
     uint16_t* tcp_window;          /* TcpPacket get_window                              (tcp.rs:64)       */
     uint16_t* tcp_urgent_ptr;      /* TcpPacket get_urgent_ptr                          (tcp.rs:66)       */
-    uint16_t* icmp_sequence;       /* Icmp(v6) echo get_sequence_number: BE16 at +6 when the ICMP(v6)
-                                    * slice holds >= 8 B, the EchoRequest/EchoReply view (icmp.rs:221-232,
-                                    * 303-314); its identifier is dst_port                                */
+    uint16_t* icmp_sequence;       /* Icmp(v6) echo get_sequence_number: BE16 at +6 for the echo types
+                                    * only (ICMP 0/8, ICMPv6 128/129) when the slice holds >= 8 B, the
+                                    * EchoRequest/EchoReply view (icmp.rs:221-232,303-314; icmpv6.rs:837-995);
+                                    * 0 for every other type. Its identifier is dst_port                  */
 } pnetgpu_rx_columns;
 
 int         pnetgpu_abi_version(void);

@@ -28,6 +28,10 @@ int ctx_device(const pnetgpu_ctx* ctx) { return ctx->device; }
 static thread_local int g_last_hip_error = 0;
 int last_hip_error() { return g_last_hip_error; }
 void set_last_hip_error(int e) { g_last_hip_error = e; }
+int hip_fail(hipError_t e) {
+    g_last_hip_error = e != hipSuccess ? (int)e : (int)hipErrorUnknown;
+    return PNETGPU_EHIP;
+}
 }  // namespace pnetgpu
 
 namespace {
@@ -36,7 +40,8 @@ constexpr int kBlock = 256;
 constexpr int kRunFrames = 64;      // frames per wave-run
 
 int set_device(const pnetgpu_ctx* ctx) {
-    return hipSetDevice(ctx->device) == hipSuccess ? PNETGPU_OK : PNETGPU_EHIP;
+    const hipError_t e = hipSetDevice(ctx->device);
+    return e == hipSuccess ? PNETGPU_OK : pnetgpu::hip_fail(e);
 }
 
 // Aligns the frame base down to 16 B; offsets are shifted by the remainder.
@@ -103,6 +108,7 @@ void pnetgpu_ctx_destroy(pnetgpu_ctx* ctx) { delete ctx; }
 
 static int rx_common(pnetgpu_ctx* ctx, const pnetgpu_batch* b, const pnetgpu_rx_columns* cols, void* stream,
                      bool tx) {
+    pnetgpu::set_last_hip_error(0);   // a stale error of an earlier call is not this one's
     if (!ctx || !b || !cols) return PNETGPU_EINVAL;
     if (b->n_frames == 0) return PNETGPU_OK;
     if (!b->data) return PNETGPU_EINVAL;
@@ -180,7 +186,7 @@ static int rx_common(pnetgpu_ctx* ctx, const pnetgpu_batch* b, const pnetgpu_rx_
             std::fprintf(stderr, "[pnetgpu] rx kind=%d regs=%d lds=%d blocks/cu=%d cus=%d\n", kind, numregs, lds,
                          per_cu_cached, ctx->cus);
     }
-    if (per_cu_cached <= 0) return PNETGPU_EHIP;
+    if (per_cu_cached <= 0) return pnetgpu::hip_fail(hipGetLastError());
     const int per_cu_v = per_cu_env ? std::atoi(per_cu_env) : 0;
     const int per_cu = per_cu_v > 0 ? per_cu_v : per_cu_cached;
     const uint64_t wpb = (uint64_t)pnetgpu::rx_waves_per_block(kind);
@@ -210,6 +216,7 @@ static int slices_common(pnetgpu_ctx* ctx, const uint8_t* data, uint64_t data_by
                          const uint8_t* addrs, const uint8_t* protos, uint16_t* out, int pseudo,
                          void* stream, const uint64_t* extra_offsets = nullptr,
                          const uint32_t* extra_lengths = nullptr) {
+    pnetgpu::set_last_hip_error(0);
     if (!ctx) return PNETGPU_EINVAL;
     if (n == 0) return PNETGPU_OK;
     if (!data || !offsets || !lengths || !skipwords || !out) return PNETGPU_EINVAL;

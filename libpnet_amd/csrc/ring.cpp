@@ -119,14 +119,21 @@ static size_t rec_capacity(uint64_t n, uint64_t mask) {
     return b;
 }
 
+// Replaces the slot's record block with one of `bytes`: the new device and host
+// buffers are allocated first and swapped in only when both exist, so a failed
+// allocation leaves the slot (and the ring's column mask) exactly as it was.
 static bool alloc_rec(Slot& s, size_t bytes) {
+    uint8_t* d = nullptr;
+    uint8_t* h = nullptr;
+    if (hipMalloc((void**)&d, bytes) != hipSuccess) return false;
+    if (hipHostMalloc((void**)&h, bytes, hipHostMallocDefault) != hipSuccess) {
+        (void)hipFree(d);
+        return false;
+    }
     if (s.d_rec) (void)hipFree(s.d_rec);
     if (s.h_rec) (void)hipHostFree(s.h_rec);
-    s.d_rec = s.h_rec = nullptr;
-    s.rec_cap = 0;
-    if (hipMalloc((void**)&s.d_rec, bytes) != hipSuccess ||
-        hipHostMalloc((void**)&s.h_rec, bytes, hipHostMallocDefault) != hipSuccess)
-        return false;
+    s.d_rec = d;
+    s.h_rec = h;
     s.rec_cap = bytes;
     return true;
 }
@@ -148,6 +155,7 @@ extern "C" {
 
 int pnetgpu_ring_create(pnetgpu_ctx* ctx, uint64_t batch_bytes, uint32_t batch_frames, uint32_t flags,
                         pnetgpu_ring** out) {
+    pnetgpu::set_last_hip_error(0);
     if (!ctx || !out || batch_bytes == 0 || batch_frames == 0) return PNETGPU_EINVAL;
     if (flags & ~(PNETGPU_RX_VLAN | PNETGPU_RX_IPV6_EXT | PNETGPU_RX_L3)) return PNETGPU_EINVAL;
     *out = nullptr;
@@ -160,7 +168,7 @@ int pnetgpu_ring_create(pnetgpu_ctx* ctx, uint64_t batch_bytes, uint32_t batch_f
     r->flags = flags;
     if (hipSetDevice(r->device) != hipSuccess) {
         delete r;
-        return PNETGPU_EHIP;
+        return pnetgpu::hip_fail(hipGetLastError());
     }
     bool ok = true;
     for (int i = 0; i < kSlots && ok; ++i) {
@@ -268,7 +276,10 @@ int pnetgpu_ring_push_many(pnetgpu_ring* r, const uint8_t* buf, const uint64_t* 
         std::vector<uint32_t> cmax(nt, 0);
         std::atomic<unsigned> arrived{0};
         std::atomic<bool> fits{false};
+        std::atomic<int> start{0};   // 0: wait, 1: go, 2: abandoned (a thread could not be created)
         auto work = [&](unsigned t) {
+            while (start.load(std::memory_order_acquire) == 0) std::this_thread::yield();
+            if (start.load(std::memory_order_acquire) == 2) return;
             const uint64_t lo = m * t / nt, hi = m * (t + 1) / nt;
             uint64_t sum = 0;
             for (uint64_t i = lo; i < hi; ++i) sum += lengths[i];
@@ -285,11 +296,21 @@ int pnetgpu_ring_push_many(pnetgpu_ring* r, const uint8_t* buf, const uint64_t* 
             for (unsigned c = 0; c < t; ++c) at += csum[c];
             cmax[t] = fill_range(lo, hi, at);
         };
+        // no exception may cross the C-ABI: a thread that cannot be created
+        // (process/thread limits) releases the ones already started, which
+        // return at once, and the push falls back to the serial pass below
         std::vector<std::thread> th;
-        for (unsigned t = 1; t < nt; ++t) th.emplace_back(work, t);
-        work(0);
+        bool started = true;
+        try {
+            th.reserve(nt - 1);
+            for (unsigned t = 1; t < nt; ++t) th.emplace_back(work, t);
+        } catch (...) {
+            started = false;
+        }
+        start.store(started ? 1 : 2, std::memory_order_release);
+        if (started) work(0);
         for (auto& t : th) t.join();
-        if (fits.load()) {
+        if (started && fits.load()) {
             k = m;
             for (unsigned c = 0; c < nt; ++c) {
                 bytes += csum[c];
@@ -313,7 +334,7 @@ int pnetgpu_ring_push_many(pnetgpu_ring* r, const uint8_t* buf, const uint64_t* 
 // caller region for submit_region) and of the descriptors, receive kernel, D2H
 // of every record column and the counters, completion event.
 static int ship_slot(pnetgpu_ring* r, Slot& s, const uint8_t* src, uint64_t* id) {
-    if (hipSetDevice(r->device) != hipSuccess) return PNETGPU_EHIP;
+    if (hipSetDevice(r->device) != hipSuccess) return pnetgpu::hip_fail(hipGetLastError());
     const hipStream_t st = s.stream;
     // compact descriptors (6 B/frame over PCIe instead of 12) whenever they can
     // describe the batch; the full ones stay on the host for the waited batch view
@@ -330,7 +351,7 @@ static int ship_slot(pnetgpu_ring* r, Slot& s, const uint8_t* src, uint64_t* id)
         hipMemcpyAsync(s.d_off, h_off, (compact ? 4ull : 8ull) * s.n, hipMemcpyHostToDevice, st) != hipSuccess ||
         hipMemcpyAsync(s.d_len, h_len, (compact ? 2ull : 4ull) * s.n, hipMemcpyHostToDevice, st) != hipSuccess ||
         hipMemsetAsync(s.d_rec, 0, 8ull * PNETGPU_NCOUNTERS, st) != hipSuccess)
-        return PNETGPU_EHIP;
+        return pnetgpu::hip_fail(hipGetLastError());
     pnetgpu_batch b{};
     b.data = s.d_frames;
     b.data_bytes = s.bytes;
@@ -354,7 +375,7 @@ static int ship_slot(pnetgpu_ring* r, Slot& s, const uint8_t* src, uint64_t* id)
     s.col_mask = r->col_mask;
     if (hipMemcpyAsync(s.h_rec, s.d_rec, at, hipMemcpyDeviceToHost, st) != hipSuccess ||   // counters + records
         hipEventRecord(s.done, st) != hipSuccess)
-        return PNETGPU_EHIP;
+        return pnetgpu::hip_fail(hipGetLastError());
     s.state = kInFlight;
     s.id = r->next_id++;
     if (id) *id = s.id;
@@ -364,6 +385,7 @@ static int ship_slot(pnetgpu_ring* r, Slot& s, const uint8_t* src, uint64_t* id)
 }
 
 int pnetgpu_ring_submit(pnetgpu_ring* r, uint64_t* id) {
+    pnetgpu::set_last_hip_error(0);
     if (!r) return PNETGPU_EINVAL;
     if (id) *id = UINT64_MAX;
     if (r->filling < 0) return PNETGPU_OK;
@@ -375,6 +397,7 @@ int pnetgpu_ring_submit(pnetgpu_ring* r, uint64_t* id) {
 
 int pnetgpu_ring_submit_region(pnetgpu_ring* r, const uint8_t* base, const uint64_t* offsets, const uint32_t* lengths,
                                uint64_t n, uint64_t* taken, uint64_t* id) {
+    pnetgpu::set_last_hip_error(0);
     if (!r || !taken || (n && (!base || !offsets || !lengths))) return PNETGPU_EINVAL;
     *taken = 0;
     if (id) *id = UINT64_MAX;
@@ -405,6 +428,7 @@ int pnetgpu_ring_submit_region(pnetgpu_ring* r, const uint8_t* base, const uint6
     return ship_slot(r, s, base + o0, id);
 }
 int pnetgpu_ring_wait(pnetgpu_ring* r, pnetgpu_ring_batch* out) {
+    pnetgpu::set_last_hip_error(0);
     if (!r || !out) return PNETGPU_EINVAL;
     if (r->held >= 0) {                          // the previous batch is released now
         r->slots[r->held].state = kFree;
@@ -415,7 +439,7 @@ int pnetgpu_ring_wait(pnetgpu_ring* r, pnetgpu_ring_batch* out) {
     const int i = r->inflight.front();
     r->inflight.pop_front();
     Slot& s = r->slots[i];
-    if (hipEventSynchronize(s.done) != hipSuccess) return PNETGPU_EHIP;
+    if (const hipError_t e = hipEventSynchronize(s.done)) return pnetgpu::hip_fail(e);
     s.state = kHeld;
     r->held = i;
     out->id = s.id;
@@ -431,6 +455,7 @@ int pnetgpu_ring_wait(pnetgpu_ring* r, pnetgpu_ring_batch* out) {
 }
 
 int pnetgpu_ring_set_columns(pnetgpu_ring* r, uint64_t column_mask) {
+    pnetgpu::set_last_hip_error(0);
     if (!r || (column_mask >> kNumCols)) return PNETGPU_EINVAL;
     const size_t need = rec_capacity(r->cap_frames, column_mask);
     bool grow = false;
@@ -438,7 +463,7 @@ int pnetgpu_ring_set_columns(pnetgpu_ring* r, uint64_t column_mask) {
     if (grow) {   // record blocks are resized only while no batch uses them
         for (const Slot& s : r->slots)
             if (s.state == kInFlight || s.state == kHeld) return PNETGPU_EBUSY;
-        if (hipSetDevice(r->device) != hipSuccess) return PNETGPU_EHIP;
+        if (hipSetDevice(r->device) != hipSuccess) return pnetgpu::hip_fail(hipGetLastError());
         for (Slot& s : r->slots)
             if (s.rec_cap < need && !alloc_rec(s, need)) return PNETGPU_ENOMEM;
     }
@@ -448,12 +473,16 @@ int pnetgpu_ring_set_columns(pnetgpu_ring* r, uint64_t column_mask) {
 
 int pnetgpu_host_register(void* p, uint64_t bytes) {
     if (!p || !bytes) return PNETGPU_EINVAL;
-    return hipHostRegister(p, bytes, hipHostRegisterDefault) == hipSuccess ? PNETGPU_OK : PNETGPU_EHIP;
+    pnetgpu::set_last_hip_error(0);
+    const hipError_t e = hipHostRegister(p, bytes, hipHostRegisterDefault);
+    return e == hipSuccess ? PNETGPU_OK : pnetgpu::hip_fail(e);
 }
 
 int pnetgpu_host_unregister(void* p) {
     if (!p) return PNETGPU_EINVAL;
-    return hipHostUnregister(p) == hipSuccess ? PNETGPU_OK : PNETGPU_EHIP;
+    pnetgpu::set_last_hip_error(0);
+    const hipError_t e = hipHostUnregister(p);
+    return e == hipSuccess ? PNETGPU_OK : pnetgpu::hip_fail(e);
 }
 
 // ---- classic pcap reader -----------------------------------------------------

@@ -465,7 +465,11 @@ __device__ __forceinline__ void store_field_columns(const pnetgpu_rx_columns& C,
     const bool v6 = (st & (PNET_ST_L3_MASK | PNET_ST_L3_MALFORMED)) == PNET_ST_L3_IPV6;
     const uint32_t l4kind = (st & (PNET_ST_L4_MALFORMED | PNET_ST_FRAGMENT)) ? 0u : (st & PNET_ST_L4_MASK);
     const bool udp = l4kind == PNET_ST_L4_UDP, tcp = l4kind == PNET_ST_L4_TCP;
-    const bool echo = (l4kind == PNET_ST_L4_ICMP || l4kind == PNET_ST_L4_ICMPV6) && P.l4len >= 8u;
+    // echo views only for the echo types: ICMP 0/8 (packetdump.rs:52-75), ICMPv6
+    // 128/129 (icmpv6.rs:135-137); P.sp holds type << 8 | code for ICMP(v6)
+    const uint32_t itype = P.sp >> 8;
+    const bool echo = P.l4len >= 8u && ((l4kind == PNET_ST_L4_ICMP && (itype == 0u || itype == 8u)) ||
+                                        (l4kind == PNET_ST_L4_ICMPV6 && (itype == 128u || itype == 129u)));
     const int l3 = (int)P.l3, l4 = (int)P.l4off;
     const uint32_t b0 = (v4 || v6) ? F.near8(l3) : 0u, b1 = (v4 || v6) ? F.near8(l3 + 1) : 0u;
     if (C.eth_dst || C.eth_src) {

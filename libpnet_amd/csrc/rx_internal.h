@@ -66,5 +66,8 @@ int launch_slices(const SliceArgs& args, int pseudo, bool run, int blocks, hipSt
 // the HIP error code behind the last PNETGPU_EHIP a launch returned on this thread
 int last_hip_error();
 void set_last_hip_error(int e);
+// records `e` as the thread's last HIP error and returns PNETGPU_EHIP: every
+// EHIP return site reports its own hipError_t (entry points reset it to 0)
+int hip_fail(hipError_t e);
 
 }  // namespace pnetgpu

@@ -9,6 +9,16 @@ returned None (the record's *_MALFORMED / dispatch bits), whose getters return
 the fields the GPU extracted, and whose payload() is a zero-copy memoryview of
 the frame bytes at the bounds the GPU computed. Nothing here re-parses a frame.
 
+The rest of the trait surface (pnet_macros_support/src/packet.rs:19-89):
+`packet()` / `payload()` (Packet), `packet_mut()` / `payload_mut()` (MutablePacket:
+writable views when the frame buffer is writable — edit, then recompute the
+checksums of the whole batch with tx_fill_checksums), `packet_size()`
+(PacketSize, the generated header + variable-field sizes) and `from_packet()`
+(FromPacket: an owned dict of every field). IPv4 and TCP options are decoded
+from the option bytes between the fixed header and the bounds the record
+gives, by the generated Ipv4OptionIterable / TcpOptionIterable rules
+(`get_options_iter()`, ipv4.rs:156-157,258-290; tcp.rs:68,107-210).
+
     b = next(ring.drain())                      # or RxResult.numpy() + the batch bytes
     v = frame_view(b.records, i, b.frames[b.offsets[i]:b.offsets[i] + b.lengths[i]])
     ip = v.ipv4()                               # Ipv4Packet::new(eth.payload()) or None
@@ -16,6 +26,7 @@ the frame bytes at the bounds the GPU computed. Nothing here re-parses a frame.
         udp.get_source(), udp.payload(), udp.checksum_ok()
 """
 import ipaddress
+from dataclasses import dataclass
 
 from .engine import DEFS
 
@@ -33,6 +44,60 @@ def _field(records, name, i):
     if not _has(records, name):
         raise KeyError(f"the batch was processed without the '{name}' column")
     return records[name][i]
+
+
+def _writable(buf, what):
+    mv = memoryview(buf)
+    if mv.readonly:
+        raise TypeError(f"{what}: the frame buffer is read-only (pass a bytearray / numpy array to mutate)")
+    return mv
+
+
+def _be16(b, at):
+    return (b[at] << 8) | b[at + 1]
+
+
+@dataclass(frozen=True)
+class Ipv4Option:
+    """Ipv4Option (ipv4.rs:258-290): copied u1, class u2, number u5, the optional
+    length byte (empty for EOL 0 / NOP 1) and the data (length - 2 bytes, bounded
+    by the option buffer)."""
+    copied: int
+    class_: int
+    number: int
+    length: bytes
+    data: bytes
+
+
+@dataclass(frozen=True)
+class TcpOption:
+    """TcpOption (tcp.rs:107-116): number u8, the optional length byte (empty for
+    EOL 0 / NOP 1) and the data (length - 2 bytes when length >= 2, bounded by the
+    option buffer, tcp.rs:198-210)."""
+    number: int
+    length: bytes
+    data: bytes
+
+
+def _option_iter(buf, tcp):
+    """The generated {Ipv4Option,TcpOption}Iterable (pnet_macros decorator.rs:772-810):
+    while bytes remain, XxxOptionPacket::new(buf) (1-B minimum), then advance by
+    min(packet_size, remaining), packet_size = 1 + len(length) + len(data)."""
+    buf = bytes(buf)
+    while buf:
+        first = buf[0]
+        number = first if tcp else first & 0x1F
+        ll = 0 if number in (0, 1) else 1                 # ipv4.rs:276-282, tcp.rs:191-198
+        length = buf[1:1 + ll]                            # get_length(): bounded by the buffer
+        if tcp:
+            plen = length[0] - 2 if length and length[0] >= 2 else 0     # tcp.rs:206-210
+        else:
+            plen = max(length[0] - 2, 0) if length else 0                # ipv4.rs:285-290
+        lo = min(1 + ll, len(buf))
+        data = buf[lo:max(min(1 + ll + plen, len(buf)), lo)]
+        yield (TcpOption(number, length, data) if tcp else
+               Ipv4Option(first >> 7, (first >> 5) & 3, number, length, data))
+        buf = buf[min(1 + ll + plen, len(buf)):]
 
 
 class L4View:
@@ -58,6 +123,69 @@ class L4View:
             start = 20 + (do * 4 - 20 if do > 5 else 0)             # tcp.rs:227-236
             return p[start:] if len(p) > start else p[0:0]
         return p[_L4_HEADER[self.kind]:]
+
+    def _tcp_data_offset(self, p):
+        return int(self._rec("tcp_data_offset")) if _has(self._r, "tcp_data_offset") else p[12] >> 4
+
+    def _bounds(self):
+        return int(self._rec("l4_offset")), int(self._rec("l4_length"))
+
+    def packet_mut(self):
+        """MutablePacket::packet_mut: the L4 slice, writable (the frame buffer must be)."""
+        off, n = self._bounds()
+        return _writable(self._f, "packet_mut")[off:off + n]
+
+    def payload_mut(self):
+        """MutablePacket::payload_mut: payload() over the writable frame buffer."""
+        off, n = self._bounds()
+        start = len(self.packet()) - len(self.payload())
+        return _writable(self._f, "payload_mut")[off + start:off + n]
+
+    def packet_size(self):
+        """PacketSize::packet_size: UDP 8, TCP 20 + tcp_options_length (tcp.rs:228-236),
+        ICMP / ICMPv6 4 (their payloads have no length function)."""
+        if self.kind == "tcp":
+            do = self._tcp_data_offset(self.packet())
+            return 20 + (do * 4 - 20 if do > 5 else 0)
+        return _L4_HEADER[self.kind]
+
+    def get_options_raw(self):
+        """TcpPacket::get_options_raw: bytes [20, 20 + options length) of the slice, bounded."""
+        if self.kind != "tcp":
+            raise AttributeError("options are a TCP field")
+        p = self.packet()
+        return p[20:min(self.packet_size(), len(p))]
+
+    def get_options_iter(self):
+        """TcpPacket::get_options_iter (tcp.rs:68): TcpOption items."""
+        return _option_iter(self.get_options_raw(), tcp=True)
+
+    def get_options(self):
+        return list(self.get_options_iter())
+
+    def from_packet(self):
+        """FromPacket::from_packet: the owned Udp / Tcp / Icmp / Icmpv6 struct as a dict."""
+        p = self.packet()
+        out = {}
+        if self.kind in ("udp", "tcp"):
+            out.update(source=self.get_source(), destination=self.get_destination())
+        else:
+            t = self.get_source()
+            out.update({("icmp_type" if self.kind == "icmp" else "icmpv6_type"): t >> 8,
+                        ("icmp_code" if self.kind == "icmp" else "icmpv6_code"): t & 0xFF})
+        if self.kind == "udp":
+            out["length"] = int(self._rec("udp_length")) if _has(self._r, "udp_length") else _be16(p, 4)
+        if self.kind == "tcp":
+            col = lambda c, fb: int(self._rec(c)) if _has(self._r, c) else fb   # noqa: E731
+            do = self._tcp_data_offset(p)
+            out.update(sequence=col("tcp_sequence", int.from_bytes(bytes(p[4:8]), "big")),
+                       acknowledgement=col("tcp_acknowledgement", int.from_bytes(bytes(p[8:12]), "big")),
+                       data_offset=do, reserved=col("tcp_reserved", p[12] & 15), flags=col("tcp_flags", p[13]),
+                       window=col("tcp_window", _be16(p, 14)), urgent_ptr=col("tcp_urgent_ptr", _be16(p, 18)),
+                       options=self.get_options())
+        out["checksum"] = self.get_checksum()
+        out["payload"] = bytes(self.payload())
+        return out
 
     def get_source(self):
         """UDP/TCP source port; for ICMP(v6) the record holds type << 8 | code."""
@@ -204,6 +332,70 @@ class IpView:
         off, n = int(self._rec("l4_offset")), int(self._rec("l4_length"))
         return memoryview(self._f)[off:off + n]
 
+    def _l3(self):
+        return int(self._rec("l3_offset")) if _has(self._r, "l3_offset") else 14
+
+    def packet(self):
+        """Ipv4Packet / Ipv6Packet::packet(): the buffer the view was built over,
+        eth.payload() = the frame from the IP header on."""
+        return memoryview(self._f)[self._l3():]
+
+    def packet_mut(self):
+        return _writable(self._f, "packet_mut")[self._l3():]
+
+    def payload_mut(self):
+        off, n = int(self._rec("l4_offset")), int(self._rec("l4_length"))
+        return _writable(self._f, "payload_mut")[off:off + n]
+
+    def _ihl(self):
+        return int(self._rec("ip_header_length")) if _has(self._r, "ip_header_length") else self.packet()[0] & 15
+
+    def _total_length(self):
+        return int(self._rec("ip_total_length")) if _has(self._r, "ip_total_length") else _be16(self.packet(), 2)
+
+    def packet_size(self):
+        """PacketSize::packet_size: IPv4 20 + ipv4_options_length + ipv4_payload_length
+        (ipv4.rs:226-243; equals total_length for IHL >= 5, ipv4.rs:316); IPv6
+        40 + payload_length (ipv6.rs:34)."""
+        if self.version == 4:
+            ihl4 = self._ihl() * 4
+            return 20 + max(ihl4 - 20, 0) + max(self._total_length() - ihl4, 0)
+        pl = int(self._rec("ip6_payload_length")) if _has(self._r, "ip6_payload_length") else _be16(self.packet(), 4)
+        return 40 + pl
+
+    def get_options_raw(self):
+        """Ipv4Packet::get_options_raw: bytes [20, 20 + options length) of the IP
+        packet, bounded by the buffer (decorator.rs:1128-1140)."""
+        if self.version != 4:
+            raise AttributeError("options are an IPv4 field")
+        p = self.packet()
+        return p[20:min(20 + max(self._ihl() * 4 - 20, 0), len(p))]
+
+    def get_options_iter(self):
+        """Ipv4Packet::get_options_iter (ipv4.rs:156-157): Ipv4Option items."""
+        return _option_iter(self.get_options_raw(), tcp=False)
+
+    def get_options(self):
+        return list(self.get_options_iter())
+
+    def from_packet(self):
+        """FromPacket::from_packet: the owned Ipv4 / Ipv6 struct (every field) as a dict."""
+        p = self.packet()
+        col = lambda c, fb: int(self._rec(c)) if _has(self._r, c) else fb   # noqa: E731
+        if self.version == 4:
+            return dict(version=col("ip_version", p[0] >> 4), header_length=self._ihl(),
+                        dscp=col("ip_dscp", p[1] >> 2), ecn=col("ip_ecn", p[1] & 3),
+                        total_length=self._total_length(), identification=col("ip_identification", _be16(p, 4)),
+                        flags=col("ip_flags", p[6] >> 5), fragment_offset=col("ip_fragment_offset", _be16(p, 6) & 0x1FFF),
+                        ttl=self.get_ttl(), next_level_protocol=self.get_next_level_protocol(),
+                        checksum=_be16(p, 10), source=self.get_source(), destination=self.get_destination(),
+                        options=self.get_options(), payload=bytes(self.payload()))
+        return dict(version=col("ip_version", p[0] >> 4),
+                    traffic_class=col("ip6_traffic_class", ((p[0] & 15) << 4) | (p[1] >> 4)),
+                    flow_label=col("ip6_flow_label", ((p[1] & 15) << 16) | _be16(p, 2)),
+                    payload_length=col("ip6_payload_length", _be16(p, 4)), next_header=p[6], hop_limit=p[7],
+                    source=self.get_source(), destination=self.get_destination(), payload=bytes(self.payload()))
+
     def _l4(self, kind):
         st = int(self._rec("status"))
         if _L4.get(st & ST["L4_MASK"]) != kind or st & (ST["L4_MALFORMED"] | ST["FRAGMENT"]):
@@ -253,6 +445,29 @@ class FrameView:
 
     def get_source(self):
         return self._mac("eth_src", 6)
+
+    def packet(self):
+        """EthernetPacket::packet(): the whole frame."""
+        return memoryview(self._f)
+
+    def payload(self):
+        """EthernetPacket::payload(): bytes 14.. (the payload has no length function)."""
+        return memoryview(self._f)[14:]
+
+    def packet_mut(self):
+        return _writable(self._f, "packet_mut")
+
+    def payload_mut(self):
+        return _writable(self._f, "payload_mut")[14:]
+
+    def packet_size(self):
+        """PacketSize::packet_size: 14 (ethernet.rs:20-30, fixed fields only)."""
+        return 14
+
+    def from_packet(self):
+        """FromPacket::from_packet: the owned Ethernet struct as a dict."""
+        return dict(destination=self.get_destination(), source=self.get_source(),
+                    ethertype=_be16(self._f, 12), payload=bytes(self.payload()))
 
     def _ip(self, bit, version):
         st = int(self._rec("status"))

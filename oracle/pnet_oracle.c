@@ -140,7 +140,9 @@ static void l4_dispatch(oracle_rec* r, int is_v6, uint8_t proto, slice_t l4,
         if (l4.len < 4) { r->status |= ORACLE_ST_L4_MALFORMED; return; }   /* IcmpPacket::new */
         r->src_port = be16(l4.p + 0);                     /* icmp_type << 8 | icmp_code */
         r->dst_port = l4.len >= 8 ? be16(l4.p + 4) : 0;   /* echo identifier, icmp.rs:221-232 */
-        r->icmp_sequence = l4.len >= 8 ? be16(l4.p + 6) : 0;   /* sequence_number, icmp.rs:229/311 */
+        /* EchoReply (type 0) / EchoRequest (type 8) views only: packetdump.rs:52-75,
+         * sequence_number icmp.rs:229/311; any other type builds no echo view */
+        r->icmp_sequence = (l4.len >= 8 && (l4.p[0] == 0 || l4.p[0] == 8)) ? be16(l4.p + 6) : 0;
         r->l4_csum = oracle_checksum(l4.p, l4.len, 1);
         r->status |= ORACLE_ST_L4_CSUM_DONE;
         if (r->l4_csum == be16(l4.p + 2)) r->status |= ORACLE_ST_L4_CSUM_OK;
@@ -150,7 +152,8 @@ static void l4_dispatch(oracle_rec* r, int is_v6, uint8_t proto, slice_t l4,
         if (l4.len < 4) { r->status |= ORACLE_ST_L4_MALFORMED; return; }   /* Icmpv6Packet::new */
         r->src_port = be16(l4.p + 0);
         r->dst_port = l4.len >= 8 ? be16(l4.p + 4) : 0;
-        r->icmp_sequence = l4.len >= 8 ? be16(l4.p + 6) : 0;   /* echo views, icmpv6.rs */
+        /* Icmpv6 EchoRequest (128) / EchoReply (129) views only (icmpv6.rs:135-137,837-995) */
+        r->icmp_sequence = (l4.len >= 8 && (l4.p[0] == 128 || l4.p[0] == 129)) ? be16(l4.p + 6) : 0;
         if (is_v6) { /* icmpv6::checksum needs IPv6 addresses; none exists over IPv4 */
             r->l4_csum = oracle_ipv6_checksum(l4.p, l4.len, 1, NULL, 0, src, dst, 58);
             r->status |= ORACLE_ST_L4_CSUM_DONE;

@@ -94,7 +94,7 @@ typedef struct oracle_rec {
     uint16_t udp_length;          /* udp.rs:27                                  */
     uint16_t tcp_window;          /* tcp.rs:64                                  */
     uint16_t tcp_urgent_ptr;      /* tcp.rs:66                                  */
-    uint16_t icmp_sequence;       /* icmp.rs:229/311 echo views (slice >= 8 B)  */
+    uint16_t icmp_sequence;       /* echo views only: ICMP 0/8, ICMPv6 128/129, slice >= 8 B */
     uint8_t  ip_version;          /* ipv4.rs:140 / ipv6.rs:23 u4                */
     uint8_t  ip_header_length;    /* ipv4.rs:141 u4                             */
     uint8_t  ip_dscp;             /* ipv4.rs:142 u6                             */

@@ -216,7 +216,9 @@ def rx_frame(frame, flags=0):
         r.update(getters(l4, UDP if proto == 17 else TCP))
     else:
         r["dst_port"] = _be16(l4, 4) if len(l4) >= 8 else 0
-        if len(l4) >= 8:                     # EchoRequest/EchoReply view (minimum 8 bytes)
+        # EchoRequest/EchoReply view (minimum 8 bytes) for the echo types only:
+        # ICMP 0/8 (packetdump.rs:52-75), ICMPv6 128/129 (icmpv6.rs:135-137)
+        if len(l4) >= 8 and l4[0] in ((0, 8) if proto == 1 else (128, 129)):
             r.update(getters(l4, ECHO))
     c = None
     if proto == 1:

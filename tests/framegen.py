@@ -262,3 +262,27 @@ def extension_frames(rng):
         h = bytearray(g[:n])
         out.append(bytes(h))
     return out
+
+
+def icmp_type_frames(rng):
+    """ICMP over IPv4 and ICMPv6 over IPv6 frames of every echo / non-echo type the
+    echo-view gate distinguishes (icmp_sequence is the EchoRequest/EchoReply
+    get_sequence_number for ICMP 0/8 and ICMPv6 128/129 only, packetdump.rs:52-75,
+    icmpv6.rs:135-137), with 4-, 7-, 8- and 24-B slices. Returns (frames, echo?)."""
+    frames, echo = [], []
+    for kind, types, ok in (("icmp", (0, 3, 5, 8, 11, 128), (0, 8)), ("icmp6", (0, 1, 8, 128, 129, 135), (128, 129))):
+        for t in types:
+            for l4_len in (4, 7, 8, 24):
+                f = bytearray(build_frame(rng, kind, l4_len))
+                l4 = len(f) - l4_len
+                f[l4] = t
+                f[l4 + 2:l4 + 4] = b"\0\0"
+                seg = bytes(f[l4:])
+                if kind == "icmp":
+                    c = po.checksum(seg, 1)
+                else:
+                    c = po.ipv6_checksum(seg, 1, b"", bytes(f[22:38]), bytes(f[38:54]), 58)
+                _set16(f, l4 + 2, c)
+                frames.append(bytes(f))
+                echo.append(t in ok and l4_len >= 8)
+    return frames, echo

@@ -156,6 +156,20 @@ def test_kat_header_getters():
         compare(res, oracle_desc(buf, offs, lens))
 
 
+def test_icmp_sequence_echo_types_only():
+    """icmp_sequence on the GPU: the echo views' sequence number for ICMP 0/8 and
+    ICMPv6 128/129 with >= 8 B, 0 for every other type, at two alignments."""
+    frames, echo = framegen.icmp_type_frames(np.random.default_rng(9))
+    for gap in (0, 3):
+        buf, offs, lens = framegen.pack(frames, gap=gap, rng=np.random.default_rng(gap))
+        res = run_desc(buf, offs, lens)
+        got = res.numpy()
+        for i, e in enumerate(echo):
+            if not e:
+                assert got["icmp_sequence"][i] == 0, i
+        compare(res, oracle_desc(buf, offs, lens))
+
+
 # ---- edge cases, random frames, alignment ---------------------------------
 
 @pytest.mark.parametrize("gap", [0, 3, 15])

@@ -80,3 +80,30 @@ def test_tx_fill_stride_every_kernel(stride, flen, monkeypatch):
         got = d.cpu().numpy()
         assert np.array_equal(got, want_buf), (kind, int((got != want_buf).sum()))
         compare(res, want_rec)
+
+
+def test_payload_mut_then_gpu_fill():
+    """MutablePacket::payload_mut on host frame buffers (libpnet_amd.views), the
+    payloads edited, then tx_fill_checksums on the GPU: the frames equal the
+    oracle's fill of the same edited bytes and verify on the receive path."""
+    rng = np.random.default_rng(23)
+    frames = [framegen.build_frame(rng, k, 40 + 3 * i) for i, k in enumerate(("udp", "tcp", "icmp", "udp6", "tcp6") * 20)]
+    buf, offs, lens = framegen.pack(frames, gap=3, rng=rng)
+    rec = coracle.rx_batch(buf, len(frames), offsets=offs, lengths=lens)
+    edit = buf.copy()
+    for i in range(len(frames)):
+        fr = edit[int(offs[i]):int(offs[i]) + int(lens[i])]          # a writable numpy view into the batch
+        v = lp.frame_view(rec, i, fr)
+        ip = v.ipv4() or v.ipv6()
+        l4 = ip.udp() or ip.tcp() or ip.icmp()
+        pm = l4.payload_mut()
+        pm[:4] = bytes([i & 0xFF, 0x55, 0xAA, 0x01])
+    assert not np.array_equal(edit, buf)
+    d = to_dev(edit)
+    lp.tx_fill_checksums(d, offsets=to_dev(offs.astype(np.int64)), lengths=to_dev(lens.astype(np.int32)))
+    torch.cuda.synchronize()
+    want_buf, _ = coracle.tx_fill(edit, len(frames), offsets=offs, lengths=lens)
+    got = d.cpu().numpy()
+    assert np.array_equal(got, want_buf)
+    after = coracle.rx_batch(got, len(frames), offsets=offs, lengths=lens)
+    assert ((after["status"] & 0x0400) != 0).all()

@@ -97,3 +97,17 @@ def test_l3_mode_version_dispatch():
     assert r["status"] == pyoracle.ST_L3_IPV4 | pyoracle.ST_L3_MALFORMED and r["ethertype"] == 0x0800
     r = pyoracle.rx_frame(b"\x55" + bytes(40), pyoracle.RX_L3)
     assert r["status"] == pyoracle.ST_UNKNOWN_ETHERTYPE and r["ethertype"] == 0
+
+
+def test_icmp_sequence_only_for_echo_types():
+    """icmp_sequence is the echo views' get_sequence_number: set for ICMP 0/8 and
+    ICMPv6 128/129 with >= 8 B, 0 for every other type (a Destination
+    Unreachable's bytes 6-7 are not a sequence number); both restatements agree."""
+    frames, echo = framegen.icmp_type_frames(np.random.default_rng(9))
+    for f, e in zip(frames, echo):
+        rc = coracle.rx_frame(f)
+        rp = pyoracle.rx_frame(f)
+        l4 = int(rc["l4_offset"])
+        seq = (f[l4 + 6] << 8 | f[l4 + 7]) if e else 0
+        assert int(rc["icmp_sequence"]) == seq == int(rp["icmp_sequence"]), (f[l4], len(f) - l4)
+        assert rc["status"] & pyoracle.ST_L4_CSUM_OK

@@ -11,7 +11,7 @@ import pytest
 import libpnet_amd as lp
 from libpnet_amd.views import ST
 from oracle import coracle, pyoracle
-from tests import framegen
+from tests import framegen, kats
 
 
 def check_views(records, frames, flags=0):
@@ -66,7 +66,9 @@ def check_views(records, frames, flags=0):
                         t[k] for k in ("tcp_sequence", "tcp_acknowledgement", "tcp_data_offset", "tcp_reserved",
                                        "tcp_flags", "tcp_window", "tcp_urgent_ptr"))
                 elif len(p) >= 8:
-                    assert l4.get_identifier() == (p[4] << 8 | p[5]) and l4.get_sequence_number() == (p[6] << 8 | p[7])
+                    echo = p[0] in ((0, 8) if kind == "icmp" else (128, 129))   # the echo views only
+                    assert l4.get_identifier() == (p[4] << 8 | p[5])
+                    assert l4.get_sequence_number() == ((p[6] << 8 | p[7]) if echo else 0)
             else:
                 assert l4.get_icmp_type() == p[0] and l4.get_icmp_code() == p[1]
             assert l4.checksum_ok() == bool(st & ST["L4_CSUM_OK"])
@@ -120,3 +122,140 @@ def test_views_over_ring_batch(tmp_path):
         check_views(b.records, fr)
         i0 += b.n
     assert i0 == len(frames)
+
+
+# ---- the rest of the trait surface: Packet / MutablePacket / PacketSize /
+# FromPacket, IPv4 and TCP options (pnet_macros_support/src/packet.rs:19-89) ----
+
+def _records(frames):
+    buf, offs, lens = framegen.pack(frames)
+    return coracle.rx_batch(buf, len(frames), offsets=offs, lengths=lens)
+
+
+def _eth_ipv4(ip_and_up):
+    return bytes(12) + b"\x08\x00" + ip_and_up
+
+
+def _ipv4_tcp_reference_frame():
+    """tcp.rs:288-356's packet: IPv4 192.168.2.1 -> 192.168.111.51, TCP with
+    options NOP, NOP, Timestamp(743951781, 44056978), payload "test", checksum
+    0xC031 (the reference sets no IPv4 total_length; here it is 20 + 36 so that
+    ip.payload() holds the segment, and the IPv4 header checksum is filled)."""
+    tcp = bytes([0xc1, 0x67, 0x23, 0x28, 0x90, 0x37, 0xd2, 0xb8, 0x94, 0x4b, 0xb2, 0x76, 0x80, 0x18, 0x0f, 0xaf,
+                 0xc0, 0x31, 0x00, 0x00, 0x01, 0x01, 0x08, 0x0a, 0x2c, 0x57, 0xcd, 0xa5, 0x02, 0xa0, 0x41, 0x92,
+                 0x74, 0x65, 0x73, 0x74])
+    ip = bytearray(20)
+    ip[0], ip[2:4], ip[9] = 0x45, (20 + len(tcp)).to_bytes(2, "big"), 6
+    ip[12:16], ip[16:20] = bytes([192, 168, 2, 1]), bytes([192, 168, 111, 51])
+    ip[10:12] = pyoracle.checksum(bytes(ip), 5).to_bytes(2, "big")
+    return _eth_ipv4(bytes(ip) + tcp)
+
+
+def test_tcp_options_reference_packet():
+    f = _ipv4_tcp_reference_frame()
+    rec = _records([f])
+    assert int(rec["l4_csum"][0]) == 0xC031 and rec["status"][0] & ST["L4_CSUM_OK"]
+    tcp = lp.frame_view(rec, 0, f).ipv4().tcp()
+    assert tcp.packet_size() == 32                      # 20 + tcp_options_length (data offset 8)
+    assert bytes(tcp.get_options_raw()) == bytes([1, 1, 8, 10, 0x2c, 0x57, 0xcd, 0xa5, 0x02, 0xa0, 0x41, 0x92])
+    opts = tcp.get_options()
+    assert opts == [lp.views.TcpOption(1, b"", b""), lp.views.TcpOption(1, b"", b""),
+                    lp.views.TcpOption(8, b"\x0a", (743951781).to_bytes(4, "big") + (44056978).to_bytes(4, "big"))]
+    assert bytes(tcp.payload()) == b"test"
+    d = tcp.from_packet()
+    assert (d["source"], d["destination"], d["sequence"], d["acknowledgement"], d["data_offset"], d["flags"],
+            d["window"], d["checksum"], d["urgent_ptr"], d["payload"]) == (
+        49511, 9000, 0x9037d2b8, 0x944bb276, 8, 0x18, 4015, 0xC031, 0, b"test")
+    assert d["options"] == opts
+
+
+def _tcp_frame(tcp_bytes):
+    ip = bytearray(20)
+    ip[0], ip[2:4], ip[9] = 0x45, (20 + len(tcp_bytes)).to_bytes(2, "big"), 6
+    return _eth_ipv4(bytes(ip) + bytes(tcp_bytes))
+
+
+def test_tcp_options_invalid_offset_and_length():
+    """tcp.rs:359-420: a data offset past the segment and an option length past
+    the option bytes iterate without fault, bounded by the buffer."""
+    seg = bytearray(20)
+    seg[12] = 10 << 4                                    # 20 B of options announced, none present
+    tcp = lp.frame_view(_records([_tcp_frame(seg)]), 0, _tcp_frame(seg)).ipv4().tcp()
+    assert tcp.get_options() == [] and bytes(tcp.get_options_raw()) == b""
+    assert tcp.packet_size() == 40
+    seg = bytearray(24)
+    seg[12] = 6 << 4
+    seg[20], seg[21] = 2, 8                              # MSS claiming 8 B with 4 left
+    tcp = lp.frame_view(_records([_tcp_frame(seg)]), 0, _tcp_frame(seg)).ipv4().tcp()
+    assert tcp.get_options() == [lp.views.TcpOption(2, b"\x08", b"\x00\x00")]
+
+
+def test_ipv4_options_reference_option():
+    """ipv4.rs:359-387's option bytes (copied 1, class 0, number 3 = LSR, length 3,
+    data 0x10) in a header with IHL 6, followed by EOL."""
+    ip = bytearray(24 + 8)
+    ip[0], ip[2:4], ip[9] = 0x46, (24 + 8).to_bytes(2, "big"), 17
+    ip[20:24] = bytes([0x83, 0x03, 0x10, 0x00])
+    ip[10:12] = pyoracle.checksum(bytes(ip[:24]), 5).to_bytes(2, "big")
+    f = _eth_ipv4(bytes(ip))
+    ip4 = lp.frame_view(_records([f]), 0, f).ipv4()
+    assert ip4.get_options() == [lp.views.Ipv4Option(1, 0, 3, b"\x03", b"\x10"),
+                                 lp.views.Ipv4Option(0, 0, 0, b"", b"")]
+    assert ip4.packet_size() == 32
+    assert ip4.from_packet()["options"] == ip4.get_options()
+
+
+def test_packet_size_and_from_packet_getters():
+    """ipv4.rs:292-357: packet_size() == total_length (115); from_packet() holds the
+    getters' values; Ethernet 14; UDP 8; ICMP 4; IPv6 40 + payload_length."""
+    v = kats.by_kind("getters")
+    ipk = [x for x in v if x["name"].startswith("ipv4")]
+    assert ipk
+    for k in ipk:
+        f = kats.getter_frame(k)
+        rec = _records([f])
+        ip4 = lp.frame_view(rec, 0, f).ipv4()
+        d = ip4.from_packet()
+        for col, want in k["expected"].items():
+            key = {"ttl": "ttl", "ip_proto": "next_level_protocol"}.get(col, col[3:])
+            assert d[key] == want, col
+        assert ip4.packet_size() == max(20, d["header_length"] * 4) + max(d["total_length"] - d["header_length"] * 4, 0)
+    rng = np.random.default_rng(21)
+    frames = [framegen.build_frame(rng, k, 30) for k in ("udp", "icmp", "udp6", "tcp")]
+    rec = _records(frames)
+    sizes = []
+    for i, f in enumerate(frames):
+        fv = lp.frame_view(rec, i, f)
+        assert fv.packet_size() == 14
+        assert fv.from_packet()["ethertype"] == (f[12] << 8 | f[13])
+        ip = fv.ipv4() or fv.ipv6()
+        l4 = ip.udp() or ip.icmp() or ip.tcp()
+        sizes.append((ip.packet_size(), l4.packet_size()))
+    assert sizes == [(20 + 30, 8), (20 + 30, 4), (40 + 30, 8), (20 + 30, 20)]
+
+
+def test_packet_mut_and_payload_mut():
+    """MutablePacket: writable views of a writable frame buffer; edit the UDP
+    payload, and the checksum fill (oracle TX restatement here, the GPU's
+    tx_fill_checksums in test_gpu_packet_api) makes the frame verify again."""
+    rng = np.random.default_rng(22)
+    f = framegen.build_frame(rng, "udp", 40)
+    rec = _records([f])
+    ro = lp.frame_view(rec, 0, f).ipv4().udp()
+    with pytest.raises(TypeError):
+        ro.payload_mut()
+    buf = bytearray(f)
+    udp = lp.frame_view(rec, 0, buf).ipv4().udp()
+    pm = udp.payload_mut()
+    assert bytes(pm) == bytes(udp.payload()) and len(pm) == 32
+    pm[:5] = b"hello"
+    assert bytes(buf[14 + 20 + 8:14 + 20 + 13]) == b"hello"
+    assert not coracle.rx_frame(bytes(buf))["status"] & ST["L4_CSUM_OK"]
+    arr = np.frombuffer(bytes(buf) + bytes(32), np.uint8).copy()
+    arr, _ = coracle.tx_fill(arr, 1, offsets=np.array([0], np.uint64), lengths=np.array([len(buf)], np.uint32))
+    assert coracle.rx_frame(bytes(arr[:len(buf)]))["status"] & ST["L4_CSUM_OK"]
+    fv = lp.frame_view(rec, 0, buf)
+    fv.packet_mut()[0] = 0xAA
+    assert buf[0] == 0xAA and len(fv.payload_mut()) == len(buf) - 14
+    ip = fv.ipv4()
+    assert len(ip.packet_mut()) == len(buf) - 14 and len(ip.payload_mut()) == 40
