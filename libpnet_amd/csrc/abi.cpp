@@ -146,19 +146,13 @@ static int rx_common(pnetgpu_ctx* ctx, const pnetgpu_batch* b, const pnetgpu_rx_
     // Kernel choice. Small: fixed stride, every frame 16-B aligned, at most 64 B,
     // inside the buffer (the 64-B configs). Otherwise rx_kernel with the tail
     // shape of the batch's frame sizes: MTU or jumbo for fixed stride, mixed for
-    // descriptor batches (their lengths are device-resident). rx_flat_kernel
-    // (compact descriptors only) is opt-in: PNETGPU_RX_KIND=5.
+    // descriptor batches (their lengths are device-resident).
     int kind = pnetgpu::kKindMixed;
-    bool stream_ok = false;
     if (b->stride) {
         const uint64_t base_sh = (a.delta + b->first_offset) & 15u;
         const uint64_t last_end = a.delta + b->first_offset + (b->n_frames - 1) * (uint64_t)b->stride + b->frame_len;
         const bool fits = b->n_frames <= (UINT64_MAX - a.delta - b->first_offset - b->frame_len) / b->stride &&
                           last_end <= a.limit;
-        // stream kernel (opt-in through PNETGPU_RX_KIND=4 until it beats the per-frame
-        // kernels): contiguous frames >= 1 KiB apart with at most 1/8 of the span in gaps
-        stream_ok = !tx && !a.field_cols && fits && b->stride >= 1024 && b->stride <= (1u << 20) && b->frame_len <= b->stride &&
-                    b->frame_len >= 256 && (uint64_t)b->frame_len * 8 >= (uint64_t)b->stride * 7;
         if (base_sh == 0 && b->stride % 16 == 0 && b->frame_len <= 64 && fits && rxf == 0)
             kind = pnetgpu::kKindSmall;
         else
@@ -171,9 +165,7 @@ static int rx_common(pnetgpu_ctx* ctx, const pnetgpu_batch* b, const pnetgpu_rx_
     const bool debug = debug_env && *debug_env == '1';
     if (kind_env) {
         const int v = std::atoi(kind_env);
-        if ((v == pnetgpu::kKindMixed || v == pnetgpu::kKindMtu || v == pnetgpu::kKindJumbo ||
-             (v == pnetgpu::kKindStream && stream_ok) || (v == pnetgpu::kKindFlat && a.desc_compact) ||
-             (v == pnetgpu::kKindSplit && !tx)) &&
+        if ((v == pnetgpu::kKindMixed || v == pnetgpu::kKindMtu || v == pnetgpu::kKindJumbo) &&
             kind != pnetgpu::kKindSmall)
             kind = v;
     }

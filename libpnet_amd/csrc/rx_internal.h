@@ -50,9 +50,6 @@ constexpr int kKindMixed = 0;
 constexpr int kKindSmall = 1;
 constexpr int kKindMtu = 2;
 constexpr int kKindJumbo = 3;
-constexpr int kKindStream = 4;   // rx_stream_kernel: fixed stride >= 1 KiB, LDS-DMA byte stream (receive only)
-constexpr int kKindFlat = 5;     // rx_flat_kernel: compact-descriptor batches, one flat granule list per run
-constexpr int kKindSplit = 6;    // rx_split_kernel: a streaming and a parsing wave per block (receive only)
 
 // device index a context is bound to (abi.cpp)
 int ctx_device(const pnetgpu_ctx* ctx);

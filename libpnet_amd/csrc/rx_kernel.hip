@@ -32,24 +32,16 @@
 //                   (mixed / MTU / jumbo) and the unified pass, where the group
 //                   loop also fills the window, are at the end of this file.
 //
-//  rx_stream_kernel opt-in (PNETGPU_RX_KIND=4) for fixed strides >= 1 KiB: each
-//                   wave streams its contiguous frame range through an LDS-DMA
-//                   ring (global_load_lds_dwordx4) and derives every frame's
-//                   tail from prefix sums of the byte stream; bit-exact, 1.00x
-//                   traffic, slower than rx_kernel here.
-//
-//  rx_split_kernel  opt-in (PNETGPU_RX_KIND=6), any batch, receive only: three-
-//                   wave blocks, one wave streams each run's byte range through
-//                   an LDS-DMA ring (prefix sums give every frame's tail), two
-//                   waves parse and store; bit-exact, slower than rx_kernel on
-//                   IMIX and jumbo frames (profiles/r02/split/).
+//  (Three opt-in kernels built in rounds 1-2 — an LDS-DMA stream kernel, a
+//  flat granule-list kernel and a stream+parse split kernel — were bit-exact
+//  but slower than these on every batch shape and were removed in round 3;
+//  their measurements stay in DESIGN.md §3/§8 and profiles/r02/.)
 //
 //  slice_kernel     the batched util::checksum / ipv4_checksum / ipv6_checksum
 //                   (and *_adv) entry points: 16 lanes per slice.
 //
 // Files: rx_common.h (helpers, parse_frame, window sums, finalize, TX write,
-// counters, column stores), rx_small.h, rx_generic.h, rx_stream.h, rx_flat.h,
-// rx_split.h, rx_slices.h
+// counters, column stores), rx_small.h, rx_generic.h, rx_slices.h
 // (one kernel family each), and this file: the launch glue and kernel choice.
 // All are one translation unit.
 //
@@ -71,9 +63,6 @@
 #include "rx_common.h"
 #include "rx_small.h"
 #include "rx_generic.h"
-#include "rx_stream.h"
-#include "rx_flat.h"
-#include "rx_split.h"
 #include "rx_slices.h"
 
 namespace pnetgpu {
@@ -121,29 +110,12 @@ static int resident_blocks(const void* fn, int block_threads) {
 #define PNET_MIXED_FN(EXT, TX) rx_kernel<PNET_MIXED_NW, PNET_MIXED_CFG, EXT, TX>
 #define PNET_JUMBO_FN(EXT, TX) rx_kernel<8, PNET_JUMBO_CFG, EXT, TX>
 
-// loads in flight per lane per round of the flat kernel
-#ifndef PNET_FLAT_U
-#define PNET_FLAT_U 4
-#endif
-
-// LDS ring steps (4 KiB each) per wave of the stream kernel
-#ifndef PNET_STREAM_SLOTS
-#define PNET_STREAM_SLOTS 3
-#endif
-// LDS ring steps of the split kernel's streaming wave
-#ifndef PNET_SPLIT_SLOTS
-#define PNET_SPLIT_SLOTS 4
-#endif
-
 template <bool EXT, bool TX>
 const void* pick_fn(int kind) {
     switch (kind) {
     case kKindSmall: return reinterpret_cast<const void*>(rx_small_kernel<TX, EXT>);
     case kKindMtu: return reinterpret_cast<const void*>(rx_kernel<8, PNET_MTU_CFG, EXT, TX>);
     case kKindJumbo: return reinterpret_cast<const void*>(PNET_JUMBO_FN(EXT, TX));
-    case kKindStream: return reinterpret_cast<const void*>(rx_stream_kernel<PNET_STREAM_SLOTS, EXT>);
-    case kKindFlat: return reinterpret_cast<const void*>(rx_flat_kernel<PNET_FLAT_U, EXT, TX>);
-    case kKindSplit: return reinterpret_cast<const void*>(rx_split_kernel<PNET_SPLIT_SLOTS, EXT>);
     default: return reinterpret_cast<const void*>(PNET_MIXED_FN(EXT, TX));
     }
 }
@@ -159,17 +131,6 @@ void launch_t(const RxArgs& args, int kind, int blocks, hipStream_t stream) {
         break;
     case kKindJumbo:
         hipLaunchKernelGGL((PNET_JUMBO_FN(EXT, TX)), dim3(blocks), dim3(kBlock), 0, stream, args);
-        break;
-    case kKindFlat:
-        hipLaunchKernelGGL((rx_flat_kernel<PNET_FLAT_U, EXT, TX>), dim3(blocks), dim3(kBlock), 0, stream, args);
-        break;
-    case kKindStream:   // receive only: the host never picks it for TX
-        if (!TX)
-            hipLaunchKernelGGL((rx_stream_kernel<PNET_STREAM_SLOTS, EXT>), dim3(blocks), dim3(kWave), 0, stream, args);
-        break;
-    case kKindSplit:    // receive only
-        if (!TX)
-            hipLaunchKernelGGL((rx_split_kernel<PNET_SPLIT_SLOTS, EXT>), dim3(blocks), dim3(3 * kWave), 0, stream, args);
         break;
     default:
         hipLaunchKernelGGL((PNET_MIXED_FN(EXT, TX)), dim3(blocks), dim3(kBlock), 0, stream, args);
@@ -192,12 +153,12 @@ int rx_blocks_per_cu(int kind, bool ext, int* numregs, int* lds) {
         if (numregs) *numregs = fa.numRegs;
         if (lds) *lds = (int)fa.sharedSizeBytes;
     }
-    const int nb = resident_blocks(fn, kind == kKindStream ? kWave : kind == kKindSplit ? 3 * kWave : kBlock);
+    const int nb = resident_blocks(fn, kBlock);
     return kind == kKindSmall && nb > PNET_SMALL_BLOCKS ? PNET_SMALL_BLOCKS : nb;
 }
 
-// runs per block per pass: the split kernel's block (two waves) takes one run at a time
-int rx_waves_per_block(int kind) { return kind == kKindStream || kind == kKindSplit ? 1 : kWavesPerBlock; }
+// runs per block per pass (one per wave)
+int rx_waves_per_block(int) { return kWavesPerBlock; }
 
 int launch_rx(const RxArgs& args, int kind, int blocks, bool tx, hipStream_t stream) {
     // EXT instantiations: dispatch extensions (flags; never with the small kernel)

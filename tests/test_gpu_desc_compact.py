@@ -91,13 +91,11 @@ def test_ring_ships_compact_descriptors_and_full_ones_for_long_frames():
         assert np.array_equal(np.concatenate([b.records[c] for b in got]), rec[c]), c
 
 
-@pytest.mark.parametrize("kind", ["5", "0"])
-def test_compact_any_order_overlaps_empty_and_max_length(kind, monkeypatch):
-    """Descriptor batches the flat kernel (kind 5, the compact default) and the
-    mixed kernel (kind 0) must both take: frames in shuffled order, frames that
-    overlap other frames, zero-length frames, and 65535-B frames (the compact
-    maximum) at every alignment — every column equal to the oracle."""
-    monkeypatch.setenv("PNETGPU_RX_KIND", kind)
+def test_compact_any_order_overlaps_empty_and_max_length():
+    """Compact descriptor batches the mixed kernel must take: frames in shuffled
+    order, frames that overlap other frames, zero-length frames, and 65535-B
+    frames (the compact maximum) at every alignment — every column equal to the
+    oracle."""
     rng = np.random.default_rng(404)
     frames = framegen.random_frames(rng, 3000, max_len=3000) + framegen.edge_frames(rng)
     buf, offs, lens = framegen.pack(frames, gap=7, rng=rng)
@@ -120,8 +118,8 @@ def test_compact_any_order_overlaps_empty_and_max_length(kind, monkeypatch):
 
 
 def test_compact_tx_fill_equals_oracle():
-    """tx_fill_checksums over compact descriptors (the flat kernel's TX
-    instantiation): patched bytes and pre-patch records equal oracle_tx_fill."""
+    """tx_fill_checksums over compact descriptors: patched bytes and pre-patch
+    records equal oracle_tx_fill."""
     rng = np.random.default_rng(405)
     frames = framegen.random_frames(rng, 4000, max_len=1600)
     buf, offs, lens = framegen.pack(frames, gap=3, rng=rng)
@@ -130,28 +128,6 @@ def test_compact_tx_fill_equals_oracle():
     res = lp.tx_fill_checksums(d, offsets=to_dev(np.asarray(offs, np.uint32).view(np.int32)),
                                lengths=to_dev(np.asarray(lens, np.uint16).view(np.int16)), columns=ALL_COLUMNS,
                                flags=lp.DESC_COMPACT)
-    torch.cuda.synchronize()
-    assert np.array_equal(d.cpu().numpy(), want_buf)
-    compare(res, want_rec)
-
-
-@pytest.mark.parametrize("flags", [0, 3])
-def test_flat_kernel_random_frames_and_tx(flags, monkeypatch):
-    """The opt-in flat kernel (PNETGPU_RX_KIND=5) on random and extension frames
-    with every column, and its TX instantiation, against the oracle."""
-    monkeypatch.setenv("PNETGPU_RX_KIND", "5")
-    rng = np.random.default_rng(406 + flags)
-    frames = framegen.extension_frames(rng) + framegen.random_frames(rng, 3000, max_len=9100)
-    buf, offs, lens = framegen.pack(frames, gap=11, rng=rng)
-    rec = coracle.rx_batch(buf, len(frames), offsets=offs, lengths=lens, flags=flags)
-    res = run_compact(to_dev(buf), offs, lens, flags=flags)
-    compare(res, rec)
-    assert res.counter_dict() == oracle_counters(rec, lens)
-    want_buf, want_rec = coracle.tx_fill(buf, len(offs), offsets=offs, lengths=lens, flags=flags)
-    d = to_dev(buf)
-    res = lp.tx_fill_checksums(d, offsets=to_dev(np.asarray(offs, np.uint32).view(np.int32)),
-                               lengths=to_dev(np.asarray(lens, np.uint16).view(np.int16)), columns=ALL_COLUMNS,
-                               flags=flags | lp.DESC_COMPACT)
     torch.cuda.synchronize()
     assert np.array_equal(d.cpu().numpy(), want_buf)
     compare(res, want_rec)
