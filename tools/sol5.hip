@@ -256,6 +256,17 @@ int main(int argc, char** argv) {
                (rbytes + wb) / ms / 1e6, wb / 1e6);
         return 0;
     };
+    if (argc > 1 && argv[1][0] == 'r') {   // the 64-B verify-only record (R = 6) against the full one (R = 26)
+        for (int k = 0; k < 3; ++k) {
+            rw("read only", rw_kernel<2, 0, true, 1>, 0);
+            rw("r + 3x 128B nt every step (R=6)", rw_kernel<2, 3, true, 1, false, 0>, 384);
+            rw("r + 13x 128B nt every step (R=26)", rw_kernel<2, 13, true, 1, false, 0>, 1664);
+            rwr("reg read only", rw_reg_kernel<2, 0, 1, 4>, 4, 0);
+            rwr("reg r + 3x 128B nt every step (R=6)", rw_reg_kernel<2, 3, 1, 4>, 4, 384);
+            rwr("reg r + 13x 128B nt every step (R=26)", rw_reg_kernel<2, 13, 1, 4>, 4, 1664);
+        }
+        return 0;
+    }
     if (argc > 1) {   // dense writes (the 64-B workload's 26 B/frame) in bursts of M steps
         rw("read only", rw_kernel<2, 0, true, 1>, 0);
         rw("r + 13x 128B nt every step", rw_kernel<2, 13, true, 1, false, 0>, 1664);
