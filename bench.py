@@ -33,23 +33,21 @@ lp = shard = None
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (/opt/skills/guides/MI355X_MICROARCH.md:36)
 METRIC = "device-resident Mpkts/s & GB/s, checksum+parse, 64B & 1500B, 1/2/4/8 GPU"
 WORKLOADS = {
-    "udp64": {"n": 1 << 24, "kernel": "rx_small_kernel", "desc": "configs[1]: 64B UDP/IPv4/Ethernet, checksum verify + header extract, "
+    "udp64": {"n": 1 << 24, "desc": "configs[1]: 64B UDP/IPv4/Ethernet, checksum verify + header extract, "
                                     "device-resident batch"},
-    "tcp1500": {"n": 1 << 20, "kernel": "rx_kernel<8, 8, 4, false, 1, false, false> (MTU, unified pass)", "desc": "configs[2]: 1500B TCP/IPv4/Ethernet, full-MTU ones-complement sum over "
+    "tcp1500": {"n": 1 << 20, "desc": "configs[2]: 1500B TCP/IPv4/Ethernet, full-MTU ones-complement sum over "
                                       "pseudo-header+payload"},
     # BASELINE's 8-GPU configs, per-GPU shard sizes (weak scaling); secondary lines
-    "imix": {"n": 1 << 22, "kernel": "rx_kernel<8, 4, 8, false, 0, true, false> (mixed, dynamic tail queue)",
+    "imix": {"n": 1 << 22,
              "desc": "configs[3]: IMIX 64/576/1500B 7:4:1 Eth/IPv4/{UDP,TCP,ICMP}, descriptor mode, per-GPU shard"},
-    "udp6_jumbo": {"n": 1 << 17, "kernel": "rx_kernel<8, 64, 9, true, 0, false, false> (jumbo)",
+    "udp6_jumbo": {"n": 1 << 17,
                    "desc": "configs[4]: 9000B IPv6/UDP jumbo frames, IPv6 pseudo-header checksum, per-GPU shard"},
     # configs[1]'s frames with the verify-only record (status + both computed
     # checksums, R = 6 B/frame; SURVEY.md §8(d) priced the target with R = 8):
     # the same kernel, a consumer that reads no extracted fields
     "imix_verify": {"n": 1 << 22, "synth": "imix", "columns": ("status", "ip_csum", "l4_csum"),
-                    "kernel": "rx_kernel<8, 4, 8, false, 0, true, false> (mixed)",
                     "desc": "configs[3] frames, checksum verify only (status + ip_csum + l4_csum columns)"},
     "udp64_verify": {"n": 1 << 24, "synth": "udp64", "columns": ("status", "ip_csum", "l4_csum"),
-                     "kernel": "rx_small_kernel",
                      "desc": "configs[1] frames, checksum verify only (status + ip_csum + l4_csum columns)"},
 }
 
@@ -410,13 +408,15 @@ def tx_fill_rate(sh, steps, warmup, device):
     stream = torch.cuda.Stream(device)
     ms = time_launches(lambda s: lp.tx_fill_checksums(data, stride=w.stride, frame_len=w.frame_len, n_frames=sh.n,
                                                       out=res, stream=s), steps, warmup, stream)
+    kernel = lp.last_rx_kernel()
     alg = sh.frame_bytes + sh.n * (4 + 2)   # frames read, two checksum fields + status written
     n1 = min(sh.n, 1 << 20)
     t0 = time.perf_counter()
     coracle.tx_fill(w.buf[: n1 * w.stride], n1, stride=w.stride, frame_len=w.frame_len)
     cpu = n1 / (time.perf_counter() - t0) / 1e6
     del data
-    out = {"workload": sh.name, "mpkts_s": round(sh.n / (ms * 1e-3) / 1e6, 1), "kernel_avg_ms": round(ms, 4),
+    out = {"workload": sh.name, "kernel": kernel, "mpkts_s": round(sh.n / (ms * 1e-3) / 1e6, 1),
+           "kernel_avg_ms": round(ms, 4),
            "alg_bytes_per_launch": alg,
            "achieved_gbs": round(alg / (ms * 1e-3) / 1e9, 1), "frac": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
            "cpu_port_1core_mpkts_s": round(cpu, 2), "traffic": load_traffic(f"tx_{sh.name}"),
@@ -471,7 +471,9 @@ def refshapes_block(steps, warmup, device):
                       (Ipv4Packet::new over its Ethernet payload, then the rest
                       of packetdump's chain), packet_benchmarks.rs:63-71
     Slices are packed back to back, one (u64 offset, u32 length, u32 skipword)
-    descriptor each; algorithmic bytes = slice bytes + 16 B descriptor + 2 B result."""
+    descriptor each; algorithmic bytes = slice bytes + 16 B descriptor + 2 B result.
+    `strided`: the same slices through pnetgpu_checksum_slices_strided (no
+    descriptor arrays; algorithmic bytes = slice + 2 B result)."""
     from oracle import coracle  # CPU baseline legs only
     out = {}
     stream = torch.cuda.Stream(device)
@@ -496,12 +498,22 @@ def refshapes_block(steps, warmup, device):
             reps, el = _timed_reps(lambda r: coracle.checksum_slices_reps(buf, offs[:k], lens[:k], skips[:k],
                                                                           cpu_out[:k], nthreads=nt, reps=r), 1.0)
             cpu[label] = round(k * reps / el / 1e6, 1)
+        # the same slices without descriptor arrays (pnetgpu_checksum_slices_strided)
+        ms_st = time_launches(lambda s: res.__setitem__("s", lp.checksum_slices_strided(d, n, size, size, 5, stream=s)),
+                              steps, warmup, stream)
+        got_st = res["s"].cpu().numpy().view(np.uint16)
+        alg_st = n * (size + 2)
+        strided = {"kernel_avg_ms": round(ms_st, 4), "mslices_s": round(n / (ms_st * 1e-3) / 1e6, 1),
+                   "achieved_gbs": round(alg_st / (ms_st * 1e-3) / 1e9, 1),
+                   "frac": round(alg_st / (ms_st * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                   "parity": bool((got_st == want).all()), "alg_bytes_per_slice": size + 2}
         out[name] = {"slices": n, "slice_bytes": size, "skipword": 5, "kernel_avg_ms": round(ms, 4),
                      "mslices_s": round(n / (ms * 1e-3) / 1e6, 1),
                      "achieved_gbs": round(alg / (ms * 1e-3) / 1e9, 1),
                      "frac": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                      "parity": bool((got == want).all()), "expected": int(want),
-                     "cpu_port_1core_mslices_s": cpu["1core"], "cpu_port_all_mslices_s": cpu["all"]}
+                     "cpu_port_1core_mslices_s": cpu["1core"], "cpu_port_all_mslices_s": cpu["all"],
+                     "strided": strided}
         del d, do, dl, ds
     # ipv4_parsing: the captured frame replicated at a 64-B stride (the small kernel)
     n = 1 << 24
@@ -588,14 +600,18 @@ def launch_check(args, world, rank):
     n = 100003
     lengths = rng.choice(np.array([64, 576, 1500], dtype=np.uint32), size=n, p=[7 / 12, 4 / 12, 1 / 12])
     t0 = time.perf_counter()
-    lo, hi = shard_mod.shard_by_bytes(lengths, world, rank)
+    # as in a GPU run: rank 0 cuts the global vector, every rank receives the cuts
+    lo, hi = shard_mod.broadcast_byte_cuts(lambda: lengths, world, rank)
+    assert (lo, hi) == shard_mod.shard_by_bytes(lengths, world, rank)
     ctr = torch.tensor([hi - lo, int(lengths[lo:hi].sum()), rank], dtype=torch.int64)
     shard_mod.all_reduce_counters(ctr)
     wall = shard_mod.all_reduce_max(time.perf_counter() - t0, "cpu")
+    bmin, bmax = shard_mod.all_reduce_min_max(float(lengths[lo:hi].sum()), "cpu")
     ok = int(ctr[0]) == n and int(ctr[1]) == int(lengths.sum()) and int(ctr[2]) == world * (world - 1) // 2
     if rank == 0:
         print(json.dumps({"metric": METRIC, "launch_check": True, "n_gpus": world, "world_size": world,
-                          "frames": int(ctr[0]), "bytes": int(ctr[1]), "wall_s": wall, "counters_ok": ok}),
+                          "frames": int(ctr[0]), "bytes": int(ctr[1]), "wall_s": wall, "counters_ok": ok,
+                          "shard_bytes_min": int(bmin), "shard_bytes_max": int(bmax)}),
               flush=True)
     return 0 if ok else 1
 
@@ -660,7 +676,10 @@ def main():
         # (the configs[3] partition); weak scaling: n per GPU
         gname = cfg.get("synth", name)
         if gname == "imix":
-            lo, hi = shard.shard_by_bytes(lp.synth.lengths(gname, n * world, args.seed * 1000), world, rank)
+            # the global length vector lives on rank 0 only; the cuts are broadcast
+            lo, hi = shard.broadcast_byte_cuts(lambda: lp.synth.lengths(gname, n * world, args.seed * 1000), world,
+                                               rank, device if dist_on and torch.distributed.get_backend() == "nccl"
+                                               else None)
             partition = "shard_by_bytes"
         else:
             lo, hi = shard.shard_by_index(n * world, world, rank)
@@ -674,6 +693,7 @@ def main():
         if rank == 0:
             log(f"[bench] {name}: built {sh.n} frames ({sh.frame_bytes / 2**30:.2f} GiB) in {time.perf_counter() - t:.1f}s")
         ok, ctr = check_counters(sh)
+        sh.kernel = lp.last_rx_kernel()      # the instantiation the launches use (rocprofv3's name)
         stream = torch.cuda.Stream(device)
         wall, avg_ms = time_shard(sh, args.steps, args.warmup, stream, dist_on)
         # counters: one RCCL all-reduce at the end (the "final throughput reduction")
@@ -684,11 +704,14 @@ def main():
         shard.all_reduce_counters(n_all)              # frames of the whole batch (the shards' sum)
         frames_all = int(n_all.item()) * args.steps
         achieved = sh.alg_bytes / (avg_ms * 1e-3) / 1e9
+        # every rank's kernel time: the spread shows shard imbalance (byte-balanced IMIX cuts)
+        kmin, kmax = shard.all_reduce_min_max(avg_ms, device)
         results[name] = {
             "sh": sh, "wall": wall, "ms_per_step": wall / args.steps * 1e3,
             "mpkts_s": frames_all / wall / 1e6,
             "gb_s": int(ctr_t[lp.COUNTER_NAMES.index("bytes")].item()) * args.steps / wall / 1e9,
-            "kernel_avg_ms": avg_ms, "frames_per_step": frames_all // args.steps,
+            "kernel_avg_ms": avg_ms, "kernel_ms_min": kmin, "kernel_ms_max": kmax,
+            "frames_per_step": frames_all // args.steps,
             "achieved_gbs": achieved, "counters_ok": bool(ctr_t[-1].item() == world),
             "counters": {k: int(v) for k, v in zip(lp.COUNTER_NAMES, ctr_t[:-1].tolist())},
         }
@@ -735,7 +758,7 @@ def main():
                 "traffic": load_traffic(primary),
                 "traffic_source": f"profiles/pmc_{primary}.json: FETCH_SIZE/WRITE_SIZE from separate rocprofv3 --pmc "
                                   "passes over the same launch (tools/profile_round.sh), not measured in this run",
-                "kernel": WORKLOADS[primary]["kernel"],
+                "kernel": p["sh"].kernel,
                 "kernel_avg_ms": round(p["kernel_avg_ms"], 4),
                 "alg_bytes_per_launch": sh.alg_bytes,
             },
@@ -746,9 +769,11 @@ def main():
             line["workloads"][name] = {
                 "mpkts_s": round(r["mpkts_s"], 1), "gb_s": round(r["gb_s"], 1),
                 "kernel_avg_ms": round(r["kernel_avg_ms"], 4),
+                "kernel_ms_min": round(r["kernel_ms_min"], 4), "kernel_ms_max": round(r["kernel_ms_max"], 4),
+                "frames_per_step": r["frames_per_step"],
                 "roofline_frac": round(r["achieved_gbs"] / HBM_PEAK_GBS, 4),
                 "achieved_gbs": round(r["achieved_gbs"], 1), "counters_ok": r["counters_ok"],
-                "traffic": load_traffic(name), "kernel": WORKLOADS[name]["kernel"],
+                "traffic": load_traffic(name), "kernel": r["sh"].kernel,
                 "alg_bytes_per_launch": r["sh"].alg_bytes, "result_bytes_per_frame": r["sh"].result_bytes,
                 "desc_bytes_per_frame": r["sh"].desc_bytes,
             }

@@ -24,7 +24,8 @@
  *                             benches/rs_sender.rs:38-39,70-71 does per frame.
  *   pnetgpu_checksum_slices   pnet_packet::util::checksum (pnet_packet/src/util.rs:76-82),
  *                             re-exported as pnet::util::checksum (src/util.rs:11-12),
- *                             over a batch of slices.
+ *                             over a batch of slices; _strided: uniform slices
+ *                             without descriptor arrays.
  *   pnetgpu_ipv4_checksum_slices  pnet_packet::util::ipv4_checksum with empty
  *                             extra_data (util.rs:92-117), batched.
  *   pnetgpu_ipv6_checksum_slices  pnet_packet::util::ipv6_checksum with empty
@@ -215,6 +216,11 @@ const char* pnetgpu_strerror(int code);
 /* The hipError_t behind the last PNETGPU_EHIP a kernel launch returned on the
  * calling thread (0 if none); PNETGPU_DEBUG=1 also prints it to stderr. */
 int         pnetgpu_last_hip_error(void);
+/* The receive kernel the last pnetgpu_rx_process / pnetgpu_tx_fill_checksums
+ * launch on the calling thread used, named as rocprofv3 names it (e.g.
+ * "rx_kernel<8, 4, 8, false, 0, true, false, false>"; "" before any launch):
+ * what a profile's kernel row is, for measurement records. Static storage. */
+const char* pnetgpu_last_rx_kernel(void);
 int         pnetgpu_device_count(int* count);
 
 int  pnetgpu_ctx_create(int device, pnetgpu_ctx** out);
@@ -239,6 +245,15 @@ int pnetgpu_tx_fill_checksums(pnetgpu_ctx* ctx, const pnetgpu_batch* batch,
 int pnetgpu_checksum_slices(pnetgpu_ctx* ctx, const uint8_t* data, uint64_t data_bytes,
                             uint64_t n, const uint64_t* offsets, const uint32_t* lengths,
                             const uint32_t* skipwords, uint16_t* out, void* stream);
+
+/* out[i] = util::checksum(data[first_offset + i*stride, +slice_len), skipword) for
+ * i < n: uniform slices with no descriptor arrays (the reference's own bench
+ * shape, pnet_packet/benches/checksum_benchmarks.rs:8-18, batched). Every
+ * slice must lie inside [0, data_bytes) (else PNETGPU_EINVAL); slices may
+ * overlap (stride < slice_len) and stride 0 repeats one slice. */
+int pnetgpu_checksum_slices_strided(pnetgpu_ctx* ctx, const uint8_t* data, uint64_t data_bytes,
+                                    uint64_t n, uint64_t first_offset, uint32_t stride,
+                                    uint32_t slice_len, uint32_t skipword, uint16_t* out, void* stream);
 
 /* out[i] = util::ipv4_checksum(slice_i, skipwords[i], &[], src_i, dst_i, protos[i]);
  * addrs: [n][8] = src octets || dst octets. */

@@ -86,6 +86,8 @@ def _load():
     L.pnetgpu_strerror.argtypes = [i32]
     L.pnetgpu_last_hip_error.restype = i32
     L.pnetgpu_last_hip_error.argtypes = []
+    L.pnetgpu_last_rx_kernel.restype = ctypes.c_char_p
+    L.pnetgpu_last_rx_kernel.argtypes = []
     L.pnetgpu_device_count.restype = i32
     L.pnetgpu_device_count.argtypes = [ctypes.POINTER(i32)]
     L.pnetgpu_ctx_create.restype = i32
@@ -97,6 +99,8 @@ def _load():
         f.argtypes = [vp, ctypes.POINTER(Batch), ctypes.POINTER(RxColumns), vp]
     L.pnetgpu_checksum_slices.restype = i32
     L.pnetgpu_checksum_slices.argtypes = [vp, vp, u64, u64, vp, vp, vp, vp, vp]
+    L.pnetgpu_checksum_slices_strided.restype = i32
+    L.pnetgpu_checksum_slices_strided.argtypes = [vp, vp, u64, u64, u64, u32, u32, u32, vp, vp]
     for f in (L.pnetgpu_ipv4_checksum_slices, L.pnetgpu_ipv6_checksum_slices):
         f.restype = i32
         f.argtypes = [vp, vp, u64, u64, vp, vp, vp, vp, vp, vp, vp]

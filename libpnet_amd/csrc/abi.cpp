@@ -28,6 +28,9 @@ int ctx_device(const pnetgpu_ctx* ctx) { return ctx->device; }
 static thread_local int g_last_hip_error = 0;
 int last_hip_error() { return g_last_hip_error; }
 void set_last_hip_error(int e) { g_last_hip_error = e; }
+static thread_local const char* g_last_rx_kernel = "";
+void set_last_rx_kernel(const char* name) { g_last_rx_kernel = name; }
+const char* last_rx_kernel() { return g_last_rx_kernel; }
 int hip_fail(hipError_t e) {
     g_last_hip_error = e != hipSuccess ? (int)e : (int)hipErrorUnknown;
     return PNETGPU_EHIP;
@@ -76,6 +79,8 @@ const char* pnetgpu_strerror(int code) {
 }
 
 int pnetgpu_last_hip_error(void) { return pnetgpu::last_hip_error(); }
+
+const char* pnetgpu_last_rx_kernel(void) { return pnetgpu::last_rx_kernel(); }
 
 int pnetgpu_device_count(int* count) {
     if (!count) return PNETGPU_EINVAL;
@@ -243,6 +248,41 @@ static int slices_common(pnetgpu_ctx* ctx, const uint8_t* data, uint64_t data_by
         pnetgpu::set_last_hip_error(e);
         return PNETGPU_EHIP;
     }
+    return PNETGPU_OK;
+}
+
+int pnetgpu_checksum_slices_strided(pnetgpu_ctx* ctx, const uint8_t* data, uint64_t data_bytes, uint64_t n,
+                                    uint64_t first_offset, uint32_t stride, uint32_t slice_len, uint32_t skipword,
+                                    uint16_t* out, void* stream) {
+    pnetgpu::set_last_hip_error(0);
+    if (!ctx) return PNETGPU_EINVAL;
+    if (n == 0) return PNETGPU_OK;
+    if (!data || !out) return PNETGPU_EINVAL;
+    // every slice inside [0, data_bytes): first + (n - 1) * stride + slice_len, overflow-safe
+    if (first_offset > data_bytes || slice_len > data_bytes - first_offset) return PNETGPU_EINVAL;
+    if (stride && n - 1 > (data_bytes - first_offset - slice_len) / stride) return PNETGPU_EINVAL;
+    int rc = set_device(ctx);
+    if (rc) return rc;
+    pnetgpu::SliceArgs a{};
+    align_base(data, data_bytes, &a.data, &a.delta, &a.limit);
+    a.n = n;
+    a.out = out;
+    a.strided = 1;
+    a.first = first_offset;
+    a.stride = stride;
+    a.slice_len = slice_len;
+    a.skipword = skipword;
+    // small uniform slices (<= 64 B at <= 64 B apart): runs staged through LDS;
+    // otherwise the descriptor kernels with computed offsets (the same choice
+    // as pnetgpu_checksum_slices, by the slice length the caller gave)
+    const bool small = stride <= 64 && slice_len <= 64;
+    const bool run = !small && slice_len <= 256;
+    const uint64_t per_block = small || run ? kBlock : kBlock / 16;
+    const uint64_t want = (n + per_block - 1) / per_block;
+    const int blocks = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)ctx->cus * 8));
+    const int e = small ? pnetgpu::launch_slices_strided_small(a, blocks, static_cast<hipStream_t>(stream))
+                        : pnetgpu::launch_slices(a, 0, run, blocks, static_cast<hipStream_t>(stream));
+    if (e) return pnetgpu::hip_fail((hipError_t)e);
     return PNETGPU_OK;
 }
 

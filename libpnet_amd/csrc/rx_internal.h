@@ -40,6 +40,13 @@ struct SliceArgs {
     const uint64_t* extra_offsets;   // *_adv: extra_data slices (nullptr otherwise)
     const uint32_t* extra_lengths;
     uint16_t* out;
+    // strided form (pnetgpu_checksum_slices_strided): slice i = [first + i * stride,
+    // +slice_len), one skipword for all; offsets/lengths/skipwords are unused
+    uint32_t strided;
+    uint32_t stride;
+    uint32_t slice_len;
+    uint32_t skipword;
+    uint64_t first;
 };
 
 // Kernel kinds: the register-resident small-frame kernel (fixed stride, frames
@@ -60,9 +67,14 @@ int rx_waves_per_block(int kind);
 // from earlier, unrelated HIP calls are cleared first
 int launch_rx(const RxArgs& args, int kind, int blocks, bool tx, hipStream_t stream);
 int launch_slices(const SliceArgs& args, int pseudo, bool run, int blocks, hipStream_t stream);
+// uniform slices of at most 64 B at a stride of at most 64 B (util::checksum)
+int launch_slices_strided_small(const SliceArgs& args, int blocks, hipStream_t stream);
 // the HIP error code behind the last PNETGPU_EHIP a launch returned on this thread
 int last_hip_error();
 void set_last_hip_error(int e);
+// the instantiation name of a receive kernel kind, and the thread's last launch
+const char* rx_kernel_name(int kind, bool ext, bool tx);
+void set_last_rx_kernel(const char* name);
 // records `e` as the thread's last HIP error and returns PNETGPU_EHIP: every
 // EHIP return site reports its own hipError_t (entry points reset it to 0)
 int hip_fail(hipError_t e);

@@ -160,13 +160,43 @@ int rx_blocks_per_cu(int kind, bool ext, int* numregs, int* lds) {
 // runs per block per pass (one per wave)
 int rx_waves_per_block(int) { return kWavesPerBlock; }
 
+#define PNET_STR2(...) #__VA_ARGS__
+#define PNET_STR(...) PNET_STR2(__VA_ARGS__)
+// The launched instantiation as rocprofv3 prints it (template arguments in
+// declaration order: rx_small_kernel<TX, FIELDS>, rx_kernel<NW, G, U, NT, PASS,
+// DYN, EXT, TX>), from the same macros the launches use.
+const char* rx_kernel_name(int kind, bool ext, bool tx) {
+#define PNET_NAMES(HEAD)                                                                       \
+    {HEAD ", false, false>", HEAD ", false, true>", HEAD ", true, false>", HEAD ", true, true>"}
+    static const char* const mixed[4] = PNET_NAMES("rx_kernel<" PNET_STR(PNET_MIXED_NW) ", " PNET_STR(PNET_MIXED_CFG));
+    static const char* const mtu[4] = PNET_NAMES("rx_kernel<8, " PNET_STR(PNET_MTU_CFG));
+    static const char* const jumbo[4] = PNET_NAMES("rx_kernel<8, " PNET_STR(PNET_JUMBO_CFG));
+    static const char* const small[4] = {"rx_small_kernel<false, false>", "rx_small_kernel<true, false>",
+                                         "rx_small_kernel<false, true>", "rx_small_kernel<true, true>"};
+#undef PNET_NAMES
+    const int i = (ext ? 2 : 0) + (tx ? 1 : 0);
+    switch (kind) {
+    case kKindSmall: return small[i];
+    case kKindMtu: return mtu[i];
+    case kKindJumbo: return jumbo[i];
+    default: return mixed[i];
+    }
+}
+
 int launch_rx(const RxArgs& args, int kind, int blocks, bool tx, hipStream_t stream) {
     // EXT instantiations: dispatch extensions (flags; never with the small kernel)
     // or header-field columns
     const bool ext = args.flags != 0 || args.field_cols != 0;
     (void)hipGetLastError();   // a stale error of an unrelated earlier call is not this launch's
+    set_last_rx_kernel(rx_kernel_name(kind, ext, tx));
     if (tx) ext ? launch_t<true, true>(args, kind, blocks, stream) : launch_t<false, true>(args, kind, blocks, stream);
     else ext ? launch_t<true, false>(args, kind, blocks, stream) : launch_t<false, false>(args, kind, blocks, stream);
+    return (int)hipGetLastError();
+}
+
+int launch_slices_strided_small(const SliceArgs& args, int blocks, hipStream_t stream) {
+    (void)hipGetLastError();
+    hipLaunchKernelGGL(slice_strided_kernel, dim3(blocks), dim3(kBlock), 0, stream, args);
     return (int)hipGetLastError();
 }
 

@@ -73,9 +73,9 @@ __global__ __launch_bounds__(kBlock) void slice_kernel(SliceArgs a) {
     // groups are 16-lane aligned, so every shuffle stays inside one group, whose
     // lanes share i (and therefore control flow)
     for (uint64_t i = gid; i < a.n; i += ngroups) {
-        const uint64_t off = a.offsets[i] + a.delta;
-        uint32_t len = a.lengths[i];
-        const uint32_t skip = a.skipwords[i];
+        const uint64_t off = (a.strided ? a.first + i * a.stride : a.offsets[i]) + a.delta;   // wave-uniform branch
+        uint32_t len = a.strided ? a.slice_len : a.lengths[i];
+        const uint32_t skip = a.strided ? a.skipword : a.skipwords[i];
         if (off > a.limit || (uint64_t)len > a.limit - off) len = 0;
         uint32_t acc = group_range_sum(a.data, off, len, j);
         uint32_t pe = 0, elen = 0;
@@ -146,9 +146,9 @@ __global__ __launch_bounds__(kBlock) void slice_run_kernel(SliceArgs a) {
         uint64_t off = 0;
         uint32_t len = 0, skip = 0;
         if (in) {
-            off = a.offsets[i] + a.delta;
-            len = a.lengths[i];
-            skip = a.skipwords[i];
+            off = (a.strided ? a.first + i * a.stride : a.offsets[i]) + a.delta;   // wave-uniform branch
+            len = a.strided ? a.slice_len : a.lengths[i];
+            skip = a.strided ? a.skipword : a.skipwords[i];
             if (off > a.limit || (uint64_t)len > a.limit - off) {
                 len = 0;
                 off = 0;
@@ -232,6 +232,66 @@ __global__ __launch_bounds__(kBlock) void slice_run_kernel(SliceArgs a) {
         }
         if (in) a.out[i] = (uint16_t)r;
         wave_sync();   // glist / gsum are rewritten by the next run
+    }
+}
+
+// slice_strided_kernel: util::checksum over uniform slices, slice i = [first +
+// i * stride, +slice_len) with stride and slice_len at most 64 B (the
+// reference's own bench shape: 20-B slices, checksum_benchmarks.rs:8-12, here
+// back to back). No descriptors: one wave per run of 64 slices, the run's span
+// (<= 4 KiB + 15 B) arrives as coalesced 1-KiB wave loads into an LDS stage
+// (aligned like memory, so the byte weights are the absolute ones), lane l sums
+// slice l's dwords from the stage with masks on the first and last, removes the
+// skipped word, and the 64 results go out as one coalesced 2-B store per lane.
+constexpr int kStageGranules = 264;   // >= ceil((63 * 64 + 64 + 15) / 16) + 1
+
+__global__ __launch_bounds__(kBlock) void slice_strided_kernel(SliceArgs a) {
+    __shared__ __attribute__((aligned(16))) uint32_t stage[kWavesPerBlock][kStageGranules * 4];
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wv = threadIdx.x / kWave;
+    uint32_t* st = stage[wv];
+    const uint8_t* sb = reinterpret_cast<const uint8_t*>(st);
+    const uint64_t nruns = (a.n + kWave - 1) / kWave;
+    const uint64_t wave_stride = (uint64_t)gridDim.x * kWavesPerBlock;
+    const uint32_t s = a.stride, L = a.slice_len;
+    for (uint64_t run = (uint64_t)blockIdx.x * kWavesPerBlock + wv; run < nruns; run += wave_stride) {
+        const uint64_t i0 = run * kWave;
+        const uint32_t nr = (uint32_t)min((uint64_t)kWave, a.n - i0);
+        const uint64_t b0 = a.first + a.delta + i0 * s;         // first slice of the run (a.data is 16-B aligned)
+        const uint64_t g0 = b0 & ~15ull;
+        const uint32_t ng = (uint32_t)((b0 + (uint64_t)(nr - 1) * s + L - g0 + 15) >> 4);   // <= 258
+        uint4 v[5];
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            const uint32_t g = 64u * k + lane;
+            v[k] = g < ng ? load16_nt(a.data + g0 + 16u * g) : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            const uint32_t g = 64u * k + lane;
+            if (g < ng) *reinterpret_cast<uint4*>(st + 4 * g) = v[k];
+        }
+        wave_sync();
+        uint32_t r = 0;
+        if ((uint32_t)lane < nr && L) {
+            const int p = (int)(b0 - g0) + lane * (int)s, q = p + (int)L;   // stage bytes [p, q)
+            uint32_t acc = 0;
+#pragma unroll 1
+            for (int k = p >> 2; 4 * k < q; ++k)
+                acc = sad(st[k] & first_bytes(clamp04(q - 4 * k)) & ~first_bytes(clamp04(p - 4 * k)), acc);
+            // skipped word: its bytes [2 skip, 2 skip + 2) that lie in the slice (util.rs:166-178)
+            const uint64_t qq = 2ull * a.skipword;
+            if (qq < L) {
+                const int x = p + (int)qq;
+                acc -= (x & 1) ? ((uint32_t)sb[x] << 8) : (uint32_t)sb[x];
+                if (qq + 1 < L) acc -= ((x + 1) & 1) ? ((uint32_t)sb[x + 1] << 8) : (uint32_t)sb[x + 1];
+            }
+            uint32_t f = fold16(acc);
+            if (!(p & 1)) f = bswap16(f);
+            r = (~f) & 0xFFFFu;                                     // util.rs:76-82 (non-empty)
+        }
+        if ((uint32_t)lane < nr) a.out[i0 + lane] = (uint16_t)r;
+        wave_sync();   // the stage is rewritten by the next run
     }
 }
 

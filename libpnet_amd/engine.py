@@ -194,6 +194,12 @@ def _check_u8_cuda(t, what):
         raise TypeError(f"{what} must be a contiguous torch.uint8 CUDA tensor")
 
 
+def last_rx_kernel():
+    """The receive kernel instantiation the calling thread's last rx_process /
+    tx_fill_checksums launched, named as rocprofv3 names it (pnetgpu_last_rx_kernel)."""
+    return lib.pnetgpu_last_rx_kernel().decode()
+
+
 def rx_process(data, *, n_frames=None, stride=0, frame_len=None, first_offset=0, offsets=None, lengths=None,
                columns=IPV4_COLUMNS, counters=True, out=None, stream=None, data_bytes=None, flags=0, ctx=None):
     """Parse + verify every frame of a device-resident batch.
@@ -275,6 +281,18 @@ def _slices(fn_name, data, offsets, lengths, skipwords, addrs=None, protos=None,
 def checksum_slices(data, offsets, lengths, skipwords, stream=None):
     """out[i] = util::checksum(data[off_i, +len_i), skipwords[i]) (uint16 in an int16 tensor)."""
     return _slices("pnetgpu_checksum_slices", data, offsets, lengths, skipwords, stream=stream)
+
+
+def checksum_slices_strided(data, n, stride, slice_len, skipword, first_offset=0, stream=None):
+    """out[i] = util::checksum(data[first_offset + i*stride, +slice_len), skipword), i < n:
+    uniform slices without descriptor arrays (pnetgpu_checksum_slices_strided)."""
+    _check_u8_cuda(data, "data")
+    out = torch.empty(n, dtype=torch.int16, device=data.device)
+    ctx = context(data.device.index)
+    check(lib.pnetgpu_checksum_slices_strided(ctx.handle, _ptr(data), data.numel(), n, first_offset, stride,
+                                              slice_len, skipword, _ptr(out), _stream_handle(stream, data.device)),
+          "pnetgpu_checksum_slices_strided")
+    return out
 
 
 def ipv4_checksum_slices(data, offsets, lengths, skipwords, addrs, protos, stream=None):

@@ -25,8 +25,9 @@ def _json_lines(out):
     return [json.loads(ln) for ln in out.splitlines() if ln.startswith("{")]
 
 
-@pytest.mark.parametrize("n", [1, 2, 3])
+@pytest.mark.parametrize("n", [1, 2, 3, 8])
 def test_bench_gpus_n_starts_n_ranks(n):
+    """N = 8 is the driver's scaling run: 8 ranks, byte cuts broadcast from rank 0."""
     p = _run(["--gpus", str(n), "--launch-check"])
     assert p.returncode == 0, p.stderr[-3000:]
     lines = _json_lines(p.stdout)
@@ -35,6 +36,9 @@ def test_bench_gpus_n_starts_n_ranks(n):
     assert line["n_gpus"] == n and line["world_size"] == n
     assert line["counters_ok"] is True
     assert line["frames"] == 100003
+    # byte-balanced: no rank's shard is more than one 1500-B frame off the mean
+    mean = line["bytes"] / n
+    assert line["shard_bytes_max"] - mean <= 1500 and mean - line["shard_bytes_min"] <= 1500
 
 
 def test_bench_world_size_must_match_gpus():

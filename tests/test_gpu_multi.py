@@ -103,3 +103,32 @@ def test_bench_two_ranks_one_gpu():
     assert line["config"]["global_batch_frames"] == 2 * int((1 << 24) * 0.01)
     assert line["config"]["parallelism"] == "shard_by_index x2"
     assert line["workloads"]["imix"]["counters_ok"] is True
+
+
+def test_bench_four_ranks_one_gpu():
+    """A rehearsal of the driver's scaling run on the 1-GPU box: `bench.py --gpus 4`
+    (gloo standing in for RCCL) over udp64 and IMIX at a small frame scale. The
+    IMIX cuts come from rank 0's prefix sum (broadcast), the four shards add up
+    to the global batch, every planted corruption is counted, and the line
+    carries each workload's per-rank kernel-time spread."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["PNETGPU_BENCH_BACKEND"] = "gloo"
+    p = subprocess.run([sys.executable, "-u", os.path.join(root, "bench.py"), "--gpus", "4", "--steps", "3",
+                        "--warmup", "1", "--frames-scale", "0.002", "--workloads", "udp64,imix", "--no-cpu",
+                        "--no-e2e", "--no-extra"], cwd=root, env=env, capture_output=True, text=True, timeout=110)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [json.loads(ln) for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    line = lines[0]
+    assert line["n_gpus"] == 4 and line["counters_ok"] is True
+    assert line["config"]["global_batch_frames"] == 4 * int((1 << 24) * 0.002)
+    im = line["workloads"]["imix"]
+    assert im["counters_ok"] is True
+    assert im["frames_per_step"] == 4 * int((1 << 22) * 0.002)
+    for w in ("udp64", "imix"):
+        r = line["workloads"][w]
+        assert 0 < r["kernel_ms_min"] <= r["kernel_avg_ms"] <= r["kernel_ms_max"]

@@ -683,3 +683,65 @@ def test_empty_batches():
     torch.cuda.synchronize()
     assert res.counter_dict()["frames"] == 0 and res2.counter_dict()["frames"] == 0
     assert int(d.sum()) == 0
+
+
+def test_last_rx_kernel_names_the_launched_instantiation():
+    """pnetgpu_last_rx_kernel: the instantiation rocprofv3 reports for each batch shape."""
+    w = lp.synth.make("udp64", 4096, seed=3)
+    lp.rx_process(to_dev(w.buf), stride=64, frame_len=64, n_frames=4096)
+    assert lp.last_rx_kernel() == "rx_small_kernel<false, false>"
+    lp.rx_process(to_dev(w.buf), stride=64, frame_len=64, n_frames=4096, columns=("status", "tcp_flags"))
+    assert lp.last_rx_kernel() == "rx_small_kernel<false, true>"
+    w = lp.synth.make("imix", 2048, seed=3)
+    d = to_dev(w.buf)
+    lp.rx_process(d, offsets=to_dev(w.offsets.astype(np.int64)), lengths=to_dev(w.lengths.astype(np.int32)))
+    assert lp.last_rx_kernel() == "rx_kernel<8, 4, 8, false, 0, true, false, false>"
+    lp.tx_fill_checksums(d, offsets=to_dev(w.offsets.astype(np.int64)), lengths=to_dev(w.lengths.astype(np.int32)))
+    assert lp.last_rx_kernel() == "rx_kernel<8, 4, 8, false, 0, true, false, true>"
+    w = lp.synth.make("tcp1500", 256, seed=3)
+    lp.rx_process(to_dev(w.buf), stride=1500, frame_len=1500, n_frames=256)
+    assert lp.last_rx_kernel() == "rx_kernel<8, 8, 4, false, 1, false, false, false>"
+    torch.cuda.synchronize()
+
+
+# ---- util::checksum over uniform slices (pnetgpu_checksum_slices_strided) ----
+
+def _strided_want(buf, n, first, stride, slen, skip):
+    offs = first + np.arange(n, dtype=np.uint64) * np.uint64(stride)
+    return coracle.checksum_slices(buf, offs, np.full(n, slen, np.uint32), np.full(n, skip, np.uint32))
+
+
+def test_strided_slices_reference_bench_shapes():
+    """checksum_benchmarks.rs:8-18: util::checksum(&[99u8; 20], 5) and
+    util::checksum(&[123u8; 1024], 5), batched back to back without descriptors."""
+    for fill, size, n in ((99, 20, 100003), (123, 1024, 2049)):
+        buf = np.full(n * size + 32, fill, np.uint8)
+        got = lp.checksum_slices_strided(to_dev(buf), n, size, size, 5).cpu().numpy().view(np.uint16)
+        want = coracle.checksum(bytes([fill] * size), 5)
+        assert (got == want).all(), (size, want)
+
+
+@pytest.mark.parametrize("stride,slen", [(20, 20), (0, 7), (1, 64), (7, 20), (16, 16), (63, 64), (64, 64),
+                                         (64, 1), (65, 20), (100, 256), (300, 257), (1024, 1000), (40, 0)])
+def test_strided_slices_random_vs_oracle(stride, slen):
+    rng = np.random.default_rng(stride * 1000 + slen)
+    n = 5000
+    for first, data_off, skip in ((0, 0, 5), (13, 3, 0), (7, 6, 40), (2, 1, 1 << 20)):
+        total = first + (n - 1) * stride + slen
+        buf = rng.integers(0, 256, total, dtype=np.uint8)
+        full = to_dev(np.concatenate([np.zeros(16, np.uint8), buf, np.zeros(64, np.uint8)]))
+        d = full[16 + data_off:16 + total]                    # buf[data_off:] at a misaligned device pointer
+        got = lp.checksum_slices_strided(d, n, stride, slen, skip, first_offset=first - data_off)
+        want = _strided_want(buf[data_off:], n, first - data_off, stride, slen, skip)
+        assert np.array_equal(got.cpu().numpy().view(np.uint16), want), (first, data_off, skip)
+
+
+def test_strided_slices_bounds_are_checked():
+    d = to_dev(np.zeros(1000, np.uint8))
+    with pytest.raises(lp.PnetGpuError):
+        lp.checksum_slices_strided(d, 11, 100, 1, 0)        # slice 10 starts at byte 1000
+    with pytest.raises(lp.PnetGpuError):
+        lp.checksum_slices_strided(d, 1, 0, 1001, 0)
+    out = lp.checksum_slices_strided(d, 10, 100, 100, 0)      # exactly fits
+    assert (out.cpu().numpy() == 0).all()
+    assert lp.checksum_slices_strided(d, 0, 100, 100, 0).numel() == 0

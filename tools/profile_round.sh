@@ -19,7 +19,13 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/sta
     python3 $R/bench.py --workloads tcp1500,imix,udp6_jumbo --no-cpu --no-e2e --no-extra \
     > $O/bench_rest_under_rocprof.json 2> $O/bench_rest_under_rocprof.err
 cp $(find $O/stats_rest -name "*kernel_stats.csv" | head -1) $O/kernel_stats_tcp1500_imix_jumbo.csv
-declare -A KN=([udp64]="rx_small_kernel<false, false>" [tcp1500]="rx_kernel<8, 8, 4, false, 1, false, false, false>" [imix]="rx_kernel<8, 4, 8, false, 0, true, false, false>" [udp6_jumbo]="rx_kernel<8, 64, 9, true, 0, false, false, false>" [tx_tcp1500]="rx_kernel<8, 8, 4, false, 1, false, false, true>")
+# kernel names as the library reports them (pnetgpu_last_rx_kernel, the bench line's "kernel")
+declare -A KN
+for W in udp64 tcp1500 imix udp6_jumbo; do
+  F=$O/bench_rest_under_rocprof.json; [ $W = udp64 ] && F=$O/bench_udp64_under_rocprof.json
+  KN[$W]=$(python3 -c "import json; print(json.load(open('$F'))['workloads']['$W']['kernel'])")
+done
+KN[tx_tcp1500]="${KN[tcp1500]%, false>}, true>"
 for W in udp64 tcp1500 imix udp6_jumbo tx_tcp1500; do
   WL=${W#tx_}; TX=""; [ "$W" != "$WL" ] && TX="--tx"
   for C in FETCH_SIZE WRITE_SIZE; do
