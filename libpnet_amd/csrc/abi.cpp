@@ -21,6 +21,8 @@ struct pnetgpu_ctx {
     int cus;
     // resident blocks per CU of each receive kernel (kind x EXT), queried once
     int per_cu[8][2] = {};
+    // of each slice kernel: [strided, run, group] x pseudo {0, 4, 16} x extra
+    int slice_per_cu[3][3][2] = {};
 };
 
 namespace pnetgpu {
@@ -40,6 +42,16 @@ int hip_fail(hipError_t e) {
 namespace {
 
 constexpr int kBlock = 256;
+
+// persistent slice grid: one resident wave of blocks (at most `want`)
+int slice_grid(pnetgpu_ctx* ctx, int which, int pseudo, bool extra, uint64_t want) {
+    int& c = ctx->slice_per_cu[which][pseudo == 0 ? 0 : pseudo == 4 ? 1 : 2][extra ? 1 : 0];
+    if (c <= 0) c = pnetgpu::slice_blocks_per_cu(which, pseudo, extra);
+    const char* env = std::getenv("PNETGPU_SLICE_BLOCKS_PER_CU");   // tuning override (tools/)
+    const int v = env ? std::atoi(env) : 0;
+    const uint64_t cap = (uint64_t)ctx->cus * (uint64_t)(v > 0 ? v : c > 0 ? c : 1);
+    return (int)std::max<uint64_t>(1, std::min<uint64_t>(want, cap));
+}
 constexpr int kRunFrames = 64;      // frames per wave-run
 
 int set_device(const pnetgpu_ctx* ctx) {
@@ -242,8 +254,7 @@ static int slices_common(pnetgpu_ctx* ctx, const uint8_t* data, uint64_t data_by
     bool run = !extra_offsets && data_bytes / n <= 256;
     if (kenv && !extra_offsets) run = kenv[0] == 'r' ? true : kenv[0] == 'g' ? false : run;
     const uint64_t per_block = run ? kBlock : kBlock / 16;
-    const uint64_t want = (n + per_block - 1) / per_block;
-    const int blocks = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)ctx->cus * 8));
+    const int blocks = slice_grid(ctx, run ? 1 : 2, pseudo, extra_offsets != nullptr, (n + per_block - 1) / per_block);
     if (const int e = pnetgpu::launch_slices(a, pseudo, run, blocks, static_cast<hipStream_t>(stream))) {
         pnetgpu::set_last_hip_error(e);
         return PNETGPU_EHIP;
@@ -278,8 +289,7 @@ int pnetgpu_checksum_slices_strided(pnetgpu_ctx* ctx, const uint8_t* data, uint6
     const bool small = stride <= 64 && slice_len <= 64;
     const bool run = !small && slice_len <= 256;
     const uint64_t per_block = small || run ? kBlock : kBlock / 16;
-    const uint64_t want = (n + per_block - 1) / per_block;
-    const int blocks = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)ctx->cus * 8));
+    const int blocks = slice_grid(ctx, small ? 0 : run ? 1 : 2, 0, false, (n + per_block - 1) / per_block);
     const int e = small ? pnetgpu::launch_slices_strided_small(a, blocks, static_cast<hipStream_t>(stream))
                         : pnetgpu::launch_slices(a, 0, run, blocks, static_cast<hipStream_t>(stream));
     if (e) return pnetgpu::hip_fail((hipError_t)e);

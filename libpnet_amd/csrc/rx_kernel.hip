@@ -194,9 +194,30 @@ int launch_rx(const RxArgs& args, int kind, int blocks, bool tx, hipStream_t str
     return (int)hipGetLastError();
 }
 
+// Resident 256-thread blocks per CU of a slice kernel (0 strided, 1 run, 2 group),
+// so that the persistent grid is exactly one resident wave of blocks (a grid
+// larger than what fits runs its last blocks after the first ones finish).
+int slice_blocks_per_cu(int which, int pseudo, bool extra) {
+    const void* fn = which == 0 ? reinterpret_cast<const void*>(slice_strided_kernel<17>)
+                   : which == 1 ? (pseudo == 0 ? reinterpret_cast<const void*>(slice_run_kernel<0>)
+                                  : pseudo == 4 ? reinterpret_cast<const void*>(slice_run_kernel<4>)
+                                                : reinterpret_cast<const void*>(slice_run_kernel<16>))
+                   : (pseudo == 0 ? reinterpret_cast<const void*>(slice_kernel<0, false>)
+                      : pseudo == 4 ? (extra ? reinterpret_cast<const void*>(slice_kernel<4, true>)
+                                             : reinterpret_cast<const void*>(slice_kernel<4, false>))
+                                    : (extra ? reinterpret_cast<const void*>(slice_kernel<16, true>)
+                                             : reinterpret_cast<const void*>(slice_kernel<16, false>)));
+    return resident_blocks(fn, kBlock);
+}
+
 int launch_slices_strided_small(const SliceArgs& args, int blocks, hipStream_t stream) {
     (void)hipGetLastError();
-    hipLaunchKernelGGL(slice_strided_kernel, dim3(blocks), dim3(kBlock), 0, stream, args);
+    // dwords a slice may touch at any alignment: ceil((len + 3) / 4)
+    const uint32_t nd = (args.slice_len + 6) / 4;
+    if (nd <= 2) hipLaunchKernelGGL(slice_strided_kernel<2>, dim3(blocks), dim3(kBlock), 0, stream, args);
+    else if (nd <= 6) hipLaunchKernelGGL(slice_strided_kernel<6>, dim3(blocks), dim3(kBlock), 0, stream, args);
+    else if (nd <= 10) hipLaunchKernelGGL(slice_strided_kernel<10>, dim3(blocks), dim3(kBlock), 0, stream, args);
+    else hipLaunchKernelGGL(slice_strided_kernel<17>, dim3(blocks), dim3(kBlock), 0, stream, args);
     return (int)hipGetLastError();
 }
 

@@ -238,60 +238,110 @@ __global__ __launch_bounds__(kBlock) void slice_run_kernel(SliceArgs a) {
 // slice_strided_kernel: util::checksum over uniform slices, slice i = [first +
 // i * stride, +slice_len) with stride and slice_len at most 64 B (the
 // reference's own bench shape: 20-B slices, checksum_benchmarks.rs:8-12, here
-// back to back). No descriptors: one wave per run of 64 slices, the run's span
-// (<= 4 KiB + 15 B) arrives as coalesced 1-KiB wave loads into an LDS stage
-// (aligned like memory, so the byte weights are the absolute ones), lane l sums
-// slice l's dwords from the stage with masks on the first and last, removes the
-// skipped word, and the 64 results go out as one coalesced 2-B store per lane.
-constexpr int kStageGranules = 264;   // >= ceil((63 * 64 + 64 + 15) / 16) + 1
+// back to back). No descriptors. One wave per "block" of R runs of 64 slices,
+// R = the most runs whose span fits 4 KiB (3 for 20-B slices, 16 for <= 4-B
+// strides): the block's span arrives as (at most) five coalesced 1-KiB wave
+// loads, the NEXT block's loads are issued before this one is summed (two
+// register sets), and the span goes through an LDS stage that keeps memory's
+// dword alignment (so the byte weights are the absolute ones) with one pad
+// dword after every 64 B: lane l reads slice 64 r + l as ND dwords (all issued
+// at once, masks past its ends), and lanes 16, 32 or 64 B apart hit distinct
+// banks (17 l instead of 16 l). Then the skipped word is removed and each run's
+// 64 results go out as one coalesced 2-B store per lane.
+// ND = dwords read per slice (>= ceil((slice_len + 3) / 4)): 6 for the 20-B shape.
+constexpr int kStageDwords = 1152;   // padded (4175 + 4 * 17) / 4 * 17 / 16, rounded up
+__device__ __forceinline__ int stage_index(int d) { return d + (d >> 4); }
 
+template <int ND>
 __global__ __launch_bounds__(kBlock) void slice_strided_kernel(SliceArgs a) {
-    __shared__ __attribute__((aligned(16))) uint32_t stage[kWavesPerBlock][kStageGranules * 4];
+    __shared__ uint32_t stage[kWavesPerBlock][kStageDwords];
     const int lane = threadIdx.x & (kWave - 1);
     const int wv = threadIdx.x / kWave;
     uint32_t* st = stage[wv];
     const uint8_t* sb = reinterpret_cast<const uint8_t*>(st);
-    const uint64_t nruns = (a.n + kWave - 1) / kWave;
-    const uint64_t wave_stride = (uint64_t)gridDim.x * kWavesPerBlock;
     const uint32_t s = a.stride, L = a.slice_len;
-    for (uint64_t run = (uint64_t)blockIdx.x * kWavesPerBlock + wv; run < nruns; run += wave_stride) {
-        const uint64_t i0 = run * kWave;
-        const uint32_t nr = (uint32_t)min((uint64_t)kWave, a.n - i0);
-        const uint64_t b0 = a.first + a.delta + i0 * s;         // first slice of the run (a.data is 16-B aligned)
-        const uint64_t g0 = b0 & ~15ull;
-        const uint32_t ng = (uint32_t)((b0 + (uint64_t)(nr - 1) * s + L - g0 + 15) >> 4);   // <= 258
-        uint4 v[5];
-#pragma unroll
-        for (int k = 0; k < 5; ++k) {
-            const uint32_t g = 64u * k + lane;
-            v[k] = g < ng ? load16_nt(a.data + g0 + 16u * g) : make_uint4(0, 0, 0, 0);
+    // runs per block: span (R * 64 - 1) * s + L + 15 <= 4096 + 64 + 15
+    const uint32_t R = s ? max(1u, min(16u, 4096u / (64u * s))) : 16u;
+    const uint64_t per = (uint64_t)kWave * R;
+    const uint64_t nblk = (a.n + per - 1) / per;
+    const uint64_t wave_stride = (uint64_t)gridDim.x * kWavesPerBlock;
+    struct Blk {
+        uint64_t i0, g0;
+        uint32_t nsl, ng;
+    };
+    auto locate = [&](uint64_t b) {
+        Blk k{};
+        if (b < nblk) {
+            k.i0 = b * per;
+            k.nsl = (uint32_t)min(per, a.n - k.i0);
+            const uint64_t b0 = a.first + a.delta + k.i0 * s;   // a.data is 16-B aligned
+            k.g0 = b0 & ~15ull;
+            k.ng = (uint32_t)((b0 + (uint64_t)(k.nsl - 1) * s + L - k.g0 + 15) >> 4);
         }
+        return k;
+    };
+    auto load = [&](const Blk& k, uint4 (&v)[5]) {
 #pragma unroll
-        for (int k = 0; k < 5; ++k) {
-            const uint32_t g = 64u * k + lane;
-            if (g < ng) *reinterpret_cast<uint4*>(st + 4 * g) = v[k];
+        for (int c = 0; c < 5; ++c) {
+            const uint32_t g = 64u * c + lane;
+            v[c] = g < k.ng ? load16_nt(a.data + k.g0 + 16u * g) : make_uint4(0, 0, 0, 0);
+        }
+    };
+    uint64_t b = (uint64_t)blockIdx.x * kWavesPerBlock + wv;
+    Blk cur = locate(b);
+    uint4 v[5], w[5];
+    load(cur, v);
+    for (; b < nblk; b += wave_stride) {
+        const Blk nxt = locate(b + wave_stride);
+        load(nxt, w);                                 // in flight while this block is summed
+#pragma unroll
+        for (int c = 0; c < 5; ++c) {
+            const int g = 64 * c + lane;
+            if ((uint32_t)g < cur.ng) {
+                uint32_t* dst = st + stage_index(4 * g);   // a granule never straddles a pad
+                dst[0] = v[c].x; dst[1] = v[c].y; dst[2] = v[c].z; dst[3] = v[c].w;
+            }
         }
         wave_sync();
-        uint32_t r = 0;
-        if ((uint32_t)lane < nr && L) {
-            const int p = (int)(b0 - g0) + lane * (int)s, q = p + (int)L;   // stage bytes [p, q)
-            uint32_t acc = 0;
+        const int pb = (int)(a.first + a.delta + cur.i0 * s - cur.g0);   // stage byte of the block's slice 0
 #pragma unroll 1
-            for (int k = p >> 2; 4 * k < q; ++k)
-                acc = sad(st[k] & first_bytes(clamp04(q - 4 * k)) & ~first_bytes(clamp04(p - 4 * k)), acc);
-            // skipped word: its bytes [2 skip, 2 skip + 2) that lie in the slice (util.rs:166-178)
-            const uint64_t qq = 2ull * a.skipword;
-            if (qq < L) {
-                const int x = p + (int)qq;
-                acc -= (x & 1) ? ((uint32_t)sb[x] << 8) : (uint32_t)sb[x];
-                if (qq + 1 < L) acc -= ((x + 1) & 1) ? ((uint32_t)sb[x + 1] << 8) : (uint32_t)sb[x + 1];
+        for (uint32_t r = 0; r < R; ++r) {
+            const uint32_t k = 64u * r + lane;
+            uint32_t res = 0;
+            if (k < cur.nsl && L) {
+                const int p = pb + (int)(k * s), q = p + (int)L;   // unpadded stage bytes [p, q)
+                const int d0 = p >> 2;
+                uint32_t x[ND];
+#pragma unroll
+                for (int t = 0; t < ND; ++t) x[t] = st[stage_index(d0 + t)];
+                uint32_t acc = 0;
+#pragma unroll
+                for (int t = 0; t < ND; ++t) {
+                    const int pos = 4 * (d0 + t);
+                    acc = sad(x[t] & first_bytes(clamp04(q - pos)) & ~first_bytes(clamp04(p - pos)), acc);
+                }
+                // skipped word: its bytes [2 skip, 2 skip + 2) that lie in the slice (util.rs:166-178)
+                const uint64_t qq = 2ull * a.skipword;
+                if (qq < L) {
+                    const int y = p + (int)qq;
+                    const uint32_t b0 = sb[4 * stage_index(y >> 2) + (y & 3)];
+                    acc -= (y & 1) ? (b0 << 8) : b0;
+                    if (qq + 1 < L) {
+                        const int z = y + 1;
+                        const uint32_t b1 = sb[4 * stage_index(z >> 2) + (z & 3)];
+                        acc -= (z & 1) ? (b1 << 8) : b1;
+                    }
+                }
+                uint32_t f = fold16(acc);
+                if (!(p & 1)) f = bswap16(f);
+                res = (~f) & 0xFFFFu;                           // util.rs:76-82 (non-empty)
             }
-            uint32_t f = fold16(acc);
-            if (!(p & 1)) f = bswap16(f);
-            r = (~f) & 0xFFFFu;                                     // util.rs:76-82 (non-empty)
+            if (k < cur.nsl) a.out[cur.i0 + k] = (uint16_t)res;
         }
-        if ((uint32_t)lane < nr) a.out[i0 + lane] = (uint16_t)r;
-        wave_sync();   // the stage is rewritten by the next run
+        wave_sync();   // the stage is rewritten by the next block
+        cur = nxt;
+#pragma unroll
+        for (int c = 0; c < 5; ++c) v[c] = w[c];
     }
 }
 

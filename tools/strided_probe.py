@@ -1,0 +1,42 @@
+#!/usr/bin/env python3
+"""Times pnetgpu_checksum_slices_strided on the reference's bench shapes (20-B and
+1024-B slices back to back, skipword 5) against the descriptor form, one process."""
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import libpnet_amd as lp  # noqa: E402
+
+dev = torch.device("cuda", 0)
+s = torch.cuda.Stream(dev)
+
+
+def timeit(fn, steps=20):
+    for _ in range(3):
+        fn()
+    s.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record(s)
+    for _ in range(steps):
+        fn()
+    b.record(s)
+    s.synchronize()
+    return a.elapsed_time(b) / steps
+
+
+for size, n in ((20, 1 << 24), (64, 1 << 23), (1024, 1 << 20)):
+    for bpc in os.environ.get("PROBE_BPC", "0").split(","):
+        os.environ["PNETGPU_SLICE_BLOCKS_PER_CU"] = bpc
+        print(f"blocks/CU {bpc} (0 = occupancy)")
+        d = torch.full((n * size + 32,), 99, dtype=torch.uint8, device=dev)
+        offs = torch.arange(n, dtype=torch.int64, device=dev) * size
+        lens = torch.full((n,), size, dtype=torch.int32, device=dev)
+        sk = torch.full((n,), 5, dtype=torch.int32, device=dev)
+        for _ in range(2):
+            t_st = timeit(lambda: lp.checksum_slices_strided(d, n, size, size, 5, stream=s))
+            t_de = timeit(lambda: lp.checksum_slices(d, offs, lens, sk, stream=s))
+            print(f"{size:5d}-B x {n}: strided {t_st*1e3:7.1f} us ({n*(size+2)/(t_st*1e-3)/8e12:.1%} of 8 TB/s)  "
+                  f"descriptors {t_de*1e3:7.1f} us ({n*(size+18)/(t_de*1e-3)/8e12:.1%})", flush=True)
