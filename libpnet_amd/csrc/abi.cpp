@@ -22,7 +22,7 @@ struct pnetgpu_ctx {
     // resident blocks per CU of each receive kernel (kind x EXT), queried once
     int per_cu[8][2] = {};
     // of each slice kernel: [strided, run, group] x pseudo {0, 4, 16} x extra
-    int slice_per_cu[3][3][2] = {};
+    int slice_per_cu[3][8][2] = {};
 };
 
 namespace pnetgpu {
@@ -45,7 +45,9 @@ constexpr int kBlock = 256;
 
 // persistent slice grid: one resident wave of blocks (at most `want`)
 int slice_grid(pnetgpu_ctx* ctx, int which, int pseudo, bool extra, uint64_t want) {
-    int& c = ctx->slice_per_cu[which][pseudo == 0 ? 0 : pseudo == 4 ? 1 : 2][extra ? 1 : 0];
+    // which 0 (strided): pseudo = strided_variant() in 0..7
+    const int k = which == 0 ? pseudo : (pseudo == 0 ? 0 : pseudo == 4 ? 1 : 2);
+    int& c = ctx->slice_per_cu[which][k][extra ? 1 : 0];
     if (c <= 0) c = pnetgpu::slice_blocks_per_cu(which, pseudo, extra);
     const char* env = std::getenv("PNETGPU_SLICE_BLOCKS_PER_CU");   // tuning override (tools/)
     const int v = env ? std::atoi(env) : 0;
@@ -289,7 +291,8 @@ int pnetgpu_checksum_slices_strided(pnetgpu_ctx* ctx, const uint8_t* data, uint6
     const bool small = stride <= 64 && slice_len <= 64;
     const bool run = !small && slice_len <= 256;
     const uint64_t per_block = small || run ? kBlock : kBlock / 16;
-    const int blocks = slice_grid(ctx, small ? 0 : run ? 1 : 2, 0, false, (n + per_block - 1) / per_block);
+    const int blocks = slice_grid(ctx, small ? 0 : run ? 1 : 2, small ? pnetgpu::strided_variant(slice_len, stride) : 0, false,
+                                  (n + per_block - 1) / per_block);
     const int e = small ? pnetgpu::launch_slices_strided_small(a, blocks, static_cast<hipStream_t>(stream))
                         : pnetgpu::launch_slices(a, 0, run, blocks, static_cast<hipStream_t>(stream));
     if (e) return pnetgpu::hip_fail((hipError_t)e);

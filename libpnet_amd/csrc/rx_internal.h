@@ -67,8 +67,10 @@ int rx_waves_per_block(int kind);
 // from earlier, unrelated HIP calls are cleared first
 int launch_rx(const RxArgs& args, int kind, int blocks, bool tx, hipStream_t stream);
 int launch_slices(const SliceArgs& args, int pseudo, bool run, int blocks, hipStream_t stream);
-// resident blocks per CU of slice kernel `which` (0 strided, 1 run, 2 group)
+// resident blocks per CU of slice kernel `which` (0 strided: `pseudo` = its
+// strided_variant(), 1 run, 2 group)
 int slice_blocks_per_cu(int which, int pseudo, bool extra);
+int strided_variant(uint32_t slice_len, uint32_t stride);
 // uniform slices of at most 64 B at a stride of at most 64 B (util::checksum)
 int launch_slices_strided_small(const SliceArgs& args, int blocks, hipStream_t stream);
 // the HIP error code behind the last PNETGPU_EHIP a launch returned on this thread

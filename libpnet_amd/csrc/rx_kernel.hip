@@ -194,11 +194,39 @@ int launch_rx(const RxArgs& args, int kind, int blocks, bool tx, hipStream_t str
     return (int)hipGetLastError();
 }
 
+// The instantiation of slice_strided_kernel<ND, EXACT, PAD> for a batch: ND =
+// dwords a slice may touch at any alignment, (len + 6) / 4 — exact (the cheaper
+// sum) for 18..21-B (6) and 62..64-B (17) slices, else the next masked one of
+// 2 / 6 / 10 / 17; PAD for strides that are multiples of 8 B (bank spread).
+int strided_variant(uint32_t slice_len, uint32_t stride) {
+    const uint32_t nd = (slice_len + 6) / 4;
+    const bool pad = stride % 8 == 0;
+    if (nd == 6) return pad ? 1 : 0;
+    if (nd == 17) return pad ? 3 : 2;
+    return nd <= 2 ? 4 : nd <= 6 ? 5 : nd <= 10 ? 6 : 7;
+}
+
+template <int ND, bool EXACT, bool PAD>
+static const void* strided_fn() { return reinterpret_cast<const void*>(slice_strided_kernel<ND, EXACT, PAD>); }
+static const void* strided_pick(int v) {
+    switch (v) {
+    case 0: return strided_fn<6, true, false>();
+    case 1: return strided_fn<6, true, true>();
+    case 2: return strided_fn<17, true, false>();
+    case 3: return strided_fn<17, true, true>();
+    case 4: return strided_fn<2, false, true>();
+    case 5: return strided_fn<6, false, true>();
+    case 6: return strided_fn<10, false, true>();
+    default: return strided_fn<17, false, true>();
+    }
+}
+
 // Resident 256-thread blocks per CU of a slice kernel (0 strided, 1 run, 2 group),
 // so that the persistent grid is exactly one resident wave of blocks (a grid
 // larger than what fits runs its last blocks after the first ones finish).
 int slice_blocks_per_cu(int which, int pseudo, bool extra) {
-    const void* fn = which == 0 ? reinterpret_cast<const void*>(slice_strided_kernel<17>)
+    // which 0 (strided): pseudo holds strided_variant() of the instantiation
+    const void* fn = which == 0 ? strided_pick(pseudo)
                    : which == 1 ? (pseudo == 0 ? reinterpret_cast<const void*>(slice_run_kernel<0>)
                                   : pseudo == 4 ? reinterpret_cast<const void*>(slice_run_kernel<4>)
                                                 : reinterpret_cast<const void*>(slice_run_kernel<16>))
@@ -212,12 +240,20 @@ int slice_blocks_per_cu(int which, int pseudo, bool extra) {
 
 int launch_slices_strided_small(const SliceArgs& args, int blocks, hipStream_t stream) {
     (void)hipGetLastError();
-    // dwords a slice may touch at any alignment: ceil((len + 3) / 4)
-    const uint32_t nd = (args.slice_len + 6) / 4;
-    if (nd <= 2) hipLaunchKernelGGL(slice_strided_kernel<2>, dim3(blocks), dim3(kBlock), 0, stream, args);
-    else if (nd <= 6) hipLaunchKernelGGL(slice_strided_kernel<6>, dim3(blocks), dim3(kBlock), 0, stream, args);
-    else if (nd <= 10) hipLaunchKernelGGL(slice_strided_kernel<10>, dim3(blocks), dim3(kBlock), 0, stream, args);
-    else hipLaunchKernelGGL(slice_strided_kernel<17>, dim3(blocks), dim3(kBlock), 0, stream, args);
+    // one launch per instantiation (hipLaunchKernelGGL needs the template at compile time)
+#define PNET_STRIDED(ND, EX, PAD) \
+    hipLaunchKernelGGL((slice_strided_kernel<ND, EX, PAD>), dim3(blocks), dim3(kBlock), 0, stream, args)
+    switch (strided_variant(args.slice_len, args.stride)) {
+    case 0: PNET_STRIDED(6, true, false); break;
+    case 1: PNET_STRIDED(6, true, true); break;
+    case 2: PNET_STRIDED(17, true, false); break;
+    case 3: PNET_STRIDED(17, true, true); break;
+    case 4: PNET_STRIDED(2, false, true); break;
+    case 5: PNET_STRIDED(6, false, true); break;
+    case 6: PNET_STRIDED(10, false, true); break;
+    default: PNET_STRIDED(17, false, true);
+    }
+#undef PNET_STRIDED
     return (int)hipGetLastError();
 }
 

@@ -248,13 +248,17 @@ __global__ __launch_bounds__(kBlock) void slice_run_kernel(SliceArgs a) {
 // at once, masks past its ends), and lanes 16, 32 or 64 B apart hit distinct
 // banks (17 l instead of 16 l). Then the skipped word is removed and each run's
 // 64 results go out as one coalesced 2-B store per lane.
-// ND = dwords read per slice (>= ceil((slice_len + 3) / 4)): 6 for the 20-B shape.
+// ND = dwords read per slice (>= ceil((slice_len + 3) / 4)); EXACT: ND equals it
+// (the 20-B and 64-B shapes), which allows the cheaper sum.
 constexpr int kStageDwords = 1152;   // padded (4175 + 4 * 17) / 4 * 17 / 16, rounded up
-__device__ __forceinline__ int stage_index(int d) { return d + (d >> 4); }
+// PAD: one pad dword per 16 (strides that are multiples of 8 B would put lanes
+// on the same banks); without it the ND reads are one address + immediate offsets
+template <bool PAD>
+__device__ __forceinline__ int stage_index(int d) { return PAD ? d + (d >> 4) : d; }
 
-template <int ND>
+template <int ND, bool EXACT, bool PAD>
 __global__ __launch_bounds__(kBlock) void slice_strided_kernel(SliceArgs a) {
-    __shared__ uint32_t stage[kWavesPerBlock][kStageDwords];
+    __shared__ __attribute__((aligned(16))) uint32_t stage[kWavesPerBlock][kStageDwords];
     const int lane = threadIdx.x & (kWave - 1);
     const int wv = threadIdx.x / kWave;
     uint32_t* st = stage[wv];
@@ -298,12 +302,20 @@ __global__ __launch_bounds__(kBlock) void slice_strided_kernel(SliceArgs a) {
         for (int c = 0; c < 5; ++c) {
             const int g = 64 * c + lane;
             if ((uint32_t)g < cur.ng) {
-                uint32_t* dst = st + stage_index(4 * g);   // a granule never straddles a pad
-                dst[0] = v[c].x; dst[1] = v[c].y; dst[2] = v[c].z; dst[3] = v[c].w;
+                if (PAD) {
+                    uint32_t* dst = st + stage_index<PAD>(4 * g);   // a granule never straddles a pad
+                    dst[0] = v[c].x; dst[1] = v[c].y; dst[2] = v[c].z; dst[3] = v[c].w;
+                } else {
+                    *reinterpret_cast<uint4*>(st + 4 * g) = v[c];
+                }
             }
         }
         wave_sync();
         const int pb = (int)(a.first + a.delta + cur.i0 * s - cur.g0);   // stage byte of the block's slice 0
+#ifdef PNET_STRIDED_NOCOMP   // A/B: one result per block from the stage, no slice sums
+        if (lane == 0 && st[lane * 17] == 0x12345u) a.out[cur.i0] = 1;
+        if (false)
+#endif
 #pragma unroll 1
         for (uint32_t r = 0; r < R; ++r) {
             const uint32_t k = 64u * r + lane;
@@ -313,22 +325,47 @@ __global__ __launch_bounds__(kBlock) void slice_strided_kernel(SliceArgs a) {
                 const int d0 = p >> 2;
                 uint32_t x[ND];
 #pragma unroll
-                for (int t = 0; t < ND; ++t) x[t] = st[stage_index(d0 + t)];
+                for (int t = 0; t < ND; ++t) x[t] = st[stage_index<PAD>(d0 + t)];
+                // every dword read summed whole, then the excess removed: the
+                // bytes before p in dword 0 and the bytes from q on (dword tq,
+                // ND-2 or ND-1, in part; the dwords after it whole). VALU is the
+                // limit of this shape (a wave64 op takes 4 cycles), so no
+                // per-dword masks (round 3: 20-B slices 85 -> see DESIGN §3)
                 uint32_t acc = 0;
+                if constexpr (EXACT) {
+                    // ND = (slice_len + 6) / 4 exactly: every dword read summed
+                    // whole, then the excess removed — the bytes before p in
+                    // dword 0 and the 0..6 bytes from q on (dword tq = ND - 2 or
+                    // ND - 1 in part and the dword after it; none when q ends
+                    // dword ND - 1). VALU is this shape's limit (a wave64 op
+                    // takes 4 cycles), so no per-dword masks.
 #pragma unroll
-                for (int t = 0; t < ND; ++t) {
-                    const int pos = 4 * (d0 + t);
-                    acc = sad(x[t] & first_bytes(clamp04(q - pos)) & ~first_bytes(clamp04(p - pos)), acc);
+                    for (int t = 0; t < ND; ++t) acc = sad(x[t], acc);
+                    const uint32_t ph = (uint32_t)p & 3u, qt = (uint32_t)q & 3u;
+                    const uint32_t hmask = ph ? 0xFFFFFFFFu >> (32u - 8u * ph) : 0u;   // bytes [4 d0, p)
+                    const uint32_t tkeep = qt ? 0xFFFFFFFFu >> (32u - 8u * qt) : 0u;   // bytes [4 (q>>2), q)
+                    acc -= sad(x[0] & hmask, 0u);
+                    const int tq = (q >> 2) - d0;
+                    const uint32_t ex1 = sad(x[ND - 1] & ~tkeep, 0u);
+                    uint32_t ex = tq == ND - 1 ? ex1 : 0u;
+                    if constexpr (ND >= 2) ex = tq == ND - 2 ? sad(x[ND - 2] & ~tkeep, sad(x[ND - 1], 0u)) : ex;
+                    acc -= ex;
+                } else {
+#pragma unroll
+                    for (int t = 0; t < ND; ++t) {
+                        const int pos = 4 * (d0 + t);
+                        acc = sad(x[t] & first_bytes(clamp04(q - pos)) & ~first_bytes(clamp04(p - pos)), acc);
+                    }
                 }
                 // skipped word: its bytes [2 skip, 2 skip + 2) that lie in the slice (util.rs:166-178)
                 const uint64_t qq = 2ull * a.skipword;
                 if (qq < L) {
                     const int y = p + (int)qq;
-                    const uint32_t b0 = sb[4 * stage_index(y >> 2) + (y & 3)];
+                    const uint32_t b0 = sb[4 * stage_index<PAD>(y >> 2) + (y & 3)];
                     acc -= (y & 1) ? (b0 << 8) : b0;
                     if (qq + 1 < L) {
                         const int z = y + 1;
-                        const uint32_t b1 = sb[4 * stage_index(z >> 2) + (z & 3)];
+                        const uint32_t b1 = sb[4 * stage_index<PAD>(z >> 2) + (z & 3)];
                         acc -= (z & 1) ? (b1 << 8) : b1;
                     }
                 }
@@ -336,7 +373,11 @@ __global__ __launch_bounds__(kBlock) void slice_strided_kernel(SliceArgs a) {
                 if (!(p & 1)) f = bswap16(f);
                 res = (~f) & 0xFFFFu;                           // util.rs:76-82 (non-empty)
             }
+#ifdef PNET_STRIDED_NOSTORE   // A/B: results stored only if they hit a magic value
+            if (k < cur.nsl && res == 0x12345u) a.out[cur.i0 + k] = (uint16_t)res;
+#else
             if (k < cur.nsl) a.out[cur.i0 + k] = (uint16_t)res;
+#endif
         }
         wave_sync();   // the stage is rewritten by the next block
         cur = nxt;

@@ -722,7 +722,8 @@ def test_strided_slices_reference_bench_shapes():
 
 
 @pytest.mark.parametrize("stride,slen", [(20, 20), (0, 7), (1, 64), (7, 20), (16, 16), (63, 64), (64, 64),
-                                         (64, 1), (65, 20), (100, 256), (300, 257), (1024, 1000), (40, 0)])
+                                         (64, 1), (65, 20), (100, 256), (300, 257), (1024, 1000), (40, 0),
+                                         (19, 18), (21, 21), (62, 62), (64, 63), (3, 3), (40, 35)])
 def test_strided_slices_random_vs_oracle(stride, slen):
     rng = np.random.default_rng(stride * 1000 + slen)
     n = 5000
