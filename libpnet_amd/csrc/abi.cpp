@@ -245,13 +245,17 @@ static int slices_common(pnetgpu_ctx* ctx, const uint8_t* data, uint64_t data_by
     a.extra_offsets = extra_offsets;
     a.extra_lengths = extra_lengths;
     a.out = out;
-    // Kernel choice (slice lengths are device-resident, so by the batch's bytes
-    // per slice): slice_run_kernel, one wave per 64 slices, each slice of at most
-    // 4 granules summed by its own lane, for batches averaging <= 256 B per
-    // slice (9.4x on the reference's 20-B bench shape, same box); slice_kernel,
-    // one 16-lane group per slice in grid-stride order, for longer slices (the
-    // run kernel's per-wave slice ranges ran 1-KiB slices 16 % slower) and for
-    // every *_adv batch. PNETGPU_SLICE_KERNEL=run|group overrides.
+    // Kernel choice. The slice lengths are device-resident, so the host decides
+    // by the BUFFER bytes per slice (data_bytes / n), which equals the bytes per
+    // slice only for slices that tile the buffer: slice_run_kernel (one wave per
+    // 64 slices, a slice of at most 4 granules summed by its own lane; 9.4x on
+    // the reference's 20-B bench shape, same box) when the buffer averages
+    // <= 256 B per slice; slice_kernel (one 16-lane group per slice, grid-stride;
+    // 16 % faster on 1-KiB slices) otherwise and for every *_adv batch. Short
+    // slices spread through a large buffer (e.g. headers of MTU frames) thus
+    // take slice_kernel; callers that know their slice sizes set
+    // PNETGPU_SLICE_KERNEL=run|group, and uniform slices have
+    // pnetgpu_checksum_slices_strided, which decides by the slice length itself.
     const char* kenv = std::getenv("PNETGPU_SLICE_KERNEL");
     bool run = !extra_offsets && data_bytes / n <= 256;
     if (kenv && !extra_offsets) run = kenv[0] == 'r' ? true : kenv[0] == 'g' ? false : run;
