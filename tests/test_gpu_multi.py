@@ -132,3 +132,41 @@ def test_bench_four_ranks_one_gpu():
     for w in ("udp64", "imix"):
         r = line["workloads"][w]
         assert 0 < r["kernel_ms_min"] <= r["kernel_avg_ms"] <= r["kernel_ms_max"]
+
+
+def _rccl_worker(port, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    dist.init_process_group("nccl", rank=0, world_size=1)   # nccl = RCCL on ROCm
+    try:
+        import libpnet_amd as lp
+        from libpnet_amd import shard
+        lengths = lp.synth.lengths("imix", 100003, 7)
+        cuts = shard.broadcast_byte_cuts(lambda: lengths, 1, 0, device=dev)
+        ctr = torch.arange(8, dtype=torch.int64, device=dev)
+        shard.all_reduce_counters(ctr)
+        mx = shard.all_reduce_max(2.5, dev)
+        mn_mx = shard.all_reduce_min_max(1.25, dev)
+        q.put((cuts, ctr.cpu().tolist(), mx, mn_mx, dist.get_backend()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rccl_collectives_one_rank():
+    """The RCCL (`nccl` backend) code path of the multi-GPU bench on this box's
+    one GPU: the byte-cut broadcast, the counter all-reduce and the MIN/MAX
+    time reductions run through RCCL on device tensors (the 8-GPU run uses the
+    same calls with 8 ranks; two ranks cannot share one device under RCCL)."""
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_worker, args=(_free_port(), q))
+    p.start()
+    cuts, ctr, mx, mn_mx, backend = q.get(timeout=100)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    assert backend == "nccl"
+    assert cuts == (0, 100003)
+    assert ctr == list(range(8)) and mx == 2.5 and mn_mx == (1.25, 1.25)

@@ -746,3 +746,26 @@ def test_strided_slices_bounds_are_checked():
     out = lp.checksum_slices_strided(d, 10, 100, 100, 0)      # exactly fits
     assert (out.cpu().numpy().view(np.uint16) == 0xFFFF).all()   # finalize(0) of non-empty zero slices
     assert lp.checksum_slices_strided(d, 0, 100, 100, 0).numel() == 0
+
+
+def test_strided_slices_random_shapes_fuzz():
+    """400 random uniform-slice batches (stride 0-300, length 0-300, first offset,
+    data-pointer misalignment, skipword in or past the slice), each against the
+    oracle: every kernel the strided entry point can pick."""
+    rng = np.random.default_rng(2024)
+    for _ in range(400):
+        stride = int(rng.integers(0, 301))
+        slen = int(rng.integers(0, 301))
+        n = int(rng.integers(1, 700))
+        first = int(rng.integers(0, 40))
+        mis = int(rng.integers(0, 16))
+        skip = int(rng.integers(0, slen // 2 + 3))
+        total = first + (n - 1) * stride + slen
+        buf = rng.integers(0, 256, max(total, 1), dtype=np.uint8)
+        full = to_dev(np.concatenate([np.zeros(16, np.uint8), buf, np.zeros(64, np.uint8)]))
+        d = full[16 + mis:16 + max(total, mis)]
+        if first < mis:
+            continue
+        got = lp.checksum_slices_strided(d, n, stride, slen, skip, first_offset=first - mis)
+        want = _strided_want(buf[mis:], n, first - mis, stride, slen, skip)
+        assert np.array_equal(got.cpu().numpy().view(np.uint16), want), (stride, slen, n, first, mis, skip)
