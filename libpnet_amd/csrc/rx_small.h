@@ -16,7 +16,22 @@ namespace {
 // ============================================================================
 // rx_small_kernel: fixed stride, frames 16-B aligned, span <= 64 B.
 // ============================================================================
+#ifndef PNET_SMALL_LINEAR   // A/B: the round-2 linear 80-B slots
+// 64-B slots with granule c of frame f at slot granule (c + f/4) & 3: the
+// transpose's ds_write_b128 (4 frames x 4 granules per 16-lane pass) and its
+// ds_read_b128 (16 frames, one granule each) both hit 16 distinct 4-bank groups
+// (the 80-B linear slots had 2-way conflicts on every write pass:
+// SQ_LDS_BANK_CONFLICT 2.9e7 per launch, profiles/r03/pmc_lds). Paths that read
+// the slot as frame bytes (slow parse, TX, header fields, IPv6 addresses)
+// first rewrite it linearly from the lane's registers. Same box, four
+// interleaved rounds (profiles/r03/small_swz): udp64 275-280 vs 277-280 us,
+// the verify-only record 221-225 vs 222-232 us; bit-exact.
+constexpr int kSmallSlot = 64;
+__device__ __forceinline__ int small_gpos(int f, int c) { return f * kSmallSlot + 16 * ((c + (f >> 2)) & 3); }
+#else
 constexpr int kSmallSlot = 80;   // 16-B aligned slots; ds_read_b128 conflict-free (20l mod 64 distinct per 16 lanes)
+__device__ __forceinline__ int small_gpos(int f, int c) { return f * kSmallSlot + 16 * c; }
+#endif
 
 struct SmallRun {
     uint4 g[4];
@@ -154,7 +169,7 @@ __device__ __forceinline__ bool small_fast(const uint32_t (&w)[16], uint32_t len
 // their code in the loop cost the plain record 3-10 % on MI355X)
 template <bool TX, bool FIELDS>
 __global__ __launch_bounds__(kBlock, PNET_SMALL_WAVES) void rx_small_kernel(RxArgs a) {
-    __shared__ __attribute__((aligned(16))) uint8_t lds_slots[kWavesPerBlock][kWave * kSmallSlot];
+    __shared__ __attribute__((aligned(16))) uint8_t lds_slots[kWavesPerBlock][kWave * kSmallSlot + 16];
     __shared__ uint64_t blk_ctr[kWavesPerBlock][PNETGPU_NCOUNTERS];
     const int lane = threadIdx.x & (kWave - 1);
     const int wv = threadIdx.x / kWave;
@@ -179,11 +194,11 @@ __global__ __launch_bounds__(kBlock, PNET_SMALL_WAVES) void rx_small_kernel(RxAr
             // granule (frame 16i + lane/4, chunk lane%4) -> that frame's slot; read back own frame
 #pragma unroll
             for (int i = 0; i < 4; ++i)
-                *reinterpret_cast<uint4*>(lds_slots[wv] + (16 * i + (lane >> 2)) * kSmallSlot + 16 * (lane & 3)) =
-                    cur.g[i];
+                *reinterpret_cast<uint4*>(lds_slots[wv] + small_gpos(16 * i + (lane >> 2), lane & 3)) = cur.g[i];
             wave_sync();
 #pragma unroll
-            for (int c = 0; c < 4; ++c) cur.g[c] = *reinterpret_cast<const uint4*>(slot + 16 * c);
+            for (int c = 0; c < 4; ++c)
+                cur.g[c] = *reinterpret_cast<const uint4*>(lds_slots[wv] + small_gpos(lane, c));
         }
 
         Parsed P{};
@@ -194,6 +209,14 @@ __global__ __launch_bounds__(kBlock, PNET_SMALL_WAVES) void rx_small_kernel(RxAr
         const bool slow = in_batch && small_fast(wv16, len, P, ipc, l4c);
         // ---- generic path through LDS for the lanes the fast path did not take ----
         const bool need_v6 = a.cols.src_ipv6 || a.cols.dst_ipv6;
+#ifndef PNET_SMALL_LINEAR
+        // the slot as frame bytes (wave-uniform): each lane rewrites its own slot
+        // linearly from its registers (no other lane reads it before the next sync)
+        if (TX || (FIELDS && a.field_cols) || need_v6 || __ballot(slow)) {
+#pragma unroll
+            for (int c = 0; c < 4; ++c) *reinterpret_cast<uint4*>(slot + 16 * c) = cur.g[c];
+        }
+#endif
 #ifdef PNET_SMALL_NOSLOW
         if (slow) P.st = 0xFFFFu;
         if (false) {
