@@ -135,6 +135,9 @@ static void test_abi_validation() {
     uint32_t len[4] = {1, 1, 1, 1}, skip[4] = {0, 0, 0, 0};
     uint8_t data[16] = {};
     CHECK(pnetgpu_checksum_slices(nullptr, data, 16, 4, off, len, skip, out, nullptr) == PNETGPU_EINVAL);
+    CHECK(pnetgpu_checksum_slices_strided(nullptr, data, 16, 4, 0, 4, 4, 0, out, nullptr) == PNETGPU_EINVAL);
+    CHECK(pnetgpu_last_rx_kernel() != nullptr && std::strlen(pnetgpu_last_rx_kernel()) == 0);   // no launch yet
+    CHECK(pnetgpu_last_hip_error() == 0);
     CHECK(pnetgpu_ipv4_checksum_adv_slices(nullptr, data, 16, 4, off, len, skip, off, len, data, data, out,
                                            nullptr) == PNETGPU_EINVAL);
     pnetgpu_ring* r = nullptr;
