@@ -236,6 +236,30 @@ class L4View:
     def get_icmp_code(self):
         return int(self._rec("src_port")) & 0xFF
 
+    # ---- the ICMP message views the reference defines over an IcmpPacket's
+    # bytes (icmp.rs:153-437; icmpv6.rs:837-995), each None unless the type is
+    # its own and the slice holds its 8-B fixed part
+    def _icmp_sub(self, cls, types):
+        if self.kind not in ("icmp", "icmpv6") or self.get_icmp_type() not in types:
+            return None
+        return cls(self) if len(self.packet()) >= 8 else None
+
+    def echo_request(self):
+        """echo_request::EchoRequestPacket (ICMP type 8, icmp.rs:304-314; ICMPv6 128)."""
+        return self._icmp_sub(EchoView, (8,) if self.kind == "icmp" else (128,))
+
+    def echo_reply(self):
+        """echo_reply::EchoReplyPacket (ICMP type 0, icmp.rs:221-232; ICMPv6 129)."""
+        return self._icmp_sub(EchoView, (0,) if self.kind == "icmp" else (129,))
+
+    def destination_unreachable(self):
+        """destination_unreachable::DestinationUnreachablePacket (ICMP type 3, icmp.rs:378-389)."""
+        return self._icmp_sub(DestinationUnreachableView, (3,)) if self.kind == "icmp" else None
+
+    def time_exceeded(self):
+        """time_exceeded::TimeExceededPacket (ICMP type 11, icmp.rs:425-436)."""
+        return self._icmp_sub(TimeExceededView, (11,)) if self.kind == "icmp" else None
+
     def get_checksum(self):
         """The stored checksum field (big-endian in the frame)."""
         p = self.packet()
@@ -251,6 +275,79 @@ class L4View:
     def checksum_ok(self):
         st = int(self._rec("status"))
         return bool(st & ST["L4_CSUM_DONE"]) and bool(st & ST["L4_CSUM_OK"])
+
+
+class _IcmpMessage:
+    """Common part of the ICMP message views: type, code, checksum, then 4
+    message-specific bytes, payload from byte 8 (packet_size 8)."""
+
+    def __init__(self, icmp):
+        self._icmp = icmp
+
+    def packet(self):
+        return self._icmp.packet()
+
+    def payload(self):
+        return self.packet()[8:]
+
+    def packet_mut(self):
+        return self._icmp.packet_mut()
+
+    def payload_mut(self):
+        return self._icmp.packet_mut()[8:]
+
+    def packet_size(self):
+        return 8
+
+    def get_icmp_type(self):
+        return self._icmp.get_icmp_type()
+
+    def get_icmp_code(self):
+        return self._icmp.get_icmp_code()
+
+    def get_checksum(self):
+        return self._icmp.get_checksum()
+
+
+class EchoView(_IcmpMessage):
+    """EchoRequest / EchoReply: identifier (+4), sequence_number (+6), the GPU's columns."""
+
+    def get_identifier(self):
+        return self._icmp.get_identifier()
+
+    def get_sequence_number(self):
+        return self._icmp.get_sequence_number()
+
+    def from_packet(self):
+        return dict(icmp_type=self.get_icmp_type(), icmp_code=self.get_icmp_code(), checksum=self.get_checksum(),
+                    identifier=self.get_identifier(), sequence_number=self.get_sequence_number(),
+                    payload=bytes(self.payload()))
+
+
+class DestinationUnreachableView(_IcmpMessage):
+    """DestinationUnreachable: unused u16be (+4), next_hop_mtu u16be (+6), payload = the
+    quoted IP header + 64 bits of the original datagram."""
+
+    def get_unused(self):
+        return _be16(self.packet(), 4)
+
+    def get_next_hop_mtu(self):
+        return _be16(self.packet(), 6)
+
+    def from_packet(self):
+        return dict(icmp_type=self.get_icmp_type(), icmp_code=self.get_icmp_code(), checksum=self.get_checksum(),
+                    unused=self.get_unused(), next_hop_mtu=self.get_next_hop_mtu(), payload=bytes(self.payload()))
+
+
+class TimeExceededView(_IcmpMessage):
+    """TimeExceeded: unused u32be (+4), payload = the quoted datagram."""
+
+    def get_unused(self):
+        return int.from_bytes(bytes(self.packet()[4:8]), "big")
+
+    def from_packet(self):
+        return dict(icmp_type=self.get_icmp_type(), icmp_code=self.get_icmp_code(), checksum=self.get_checksum(),
+                    unused=self.get_unused(), payload=bytes(self.payload()))
 
 
 class IpView:

@@ -259,3 +259,37 @@ def test_packet_mut_and_payload_mut():
     assert buf[0] == 0xAA and len(fv.payload_mut()) == len(buf) - 14
     ip = fv.ipv4()
     assert len(ip.packet_mut()) == len(buf) - 14 and len(ip.payload_mut()) == 40
+
+
+def test_icmp_message_views():
+    """The ICMP message views over a record (icmp.rs:153-437): each answers only
+    for its own type with >= 8 B; echo fields come from the GPU columns,
+    DestinationUnreachable's next_hop_mtu / TimeExceeded's unused from the bytes."""
+    frames, _ = framegen.icmp_type_frames(np.random.default_rng(31))
+    rec = _records(frames)
+    seen = set()
+    for i, f in enumerate(frames):
+        ip = lp.frame_view(rec, i, f).ipv4() or lp.frame_view(rec, i, f).ipv6()
+        ic = ip.icmp() or ip.icmpv6()
+        p = bytes(ic.packet())
+        t, long_enough = p[0], len(p) >= 8
+        v4 = ic.kind == "icmp"
+        for name, want_type in (("echo_request", 8 if v4 else 128), ("echo_reply", 0 if v4 else 129),
+                                ("destination_unreachable", 3 if v4 else None),
+                                ("time_exceeded", 11 if v4 else None)):
+            view = getattr(ic, name)()
+            assert (view is not None) == (long_enough and t == want_type), (name, t, len(p))
+            if view is None:
+                continue
+            seen.add(name)
+            assert view.packet_size() == 8 and bytes(view.payload()) == p[8:]
+            if name.startswith("echo"):
+                assert view.get_identifier() == (p[4] << 8 | p[5])
+                assert view.get_sequence_number() == (p[6] << 8 | p[7])
+                assert view.from_packet()["sequence_number"] == (p[6] << 8 | p[7])
+            elif name == "destination_unreachable":
+                assert (view.get_unused(), view.get_next_hop_mtu()) == (p[4] << 8 | p[5], p[6] << 8 | p[7])
+            else:
+                assert view.get_unused() == int.from_bytes(p[4:8], "big")
+                assert view.from_packet()["payload"] == p[8:]
+    assert seen == {"echo_request", "echo_reply", "destination_unreachable", "time_exceeded"}
