@@ -12,14 +12,14 @@ import pytest
 import torch
 
 import libpnet_amd as lp
-from libpnet_amd.engine import ALL_COLUMNS
+from libpnet_amd.engine import ALL_COLUMNS, RX_IPV6_EXT, RX_VLAN
 from oracle import coracle
 from tests import framegen
 from tests.test_gpu_parity import compare, oracle_counters, to_dev
 
 pytestmark = pytest.mark.gpu
 
-FLAG_SETS = (0, 0, 0, lp.RX_VLAN, lp.RX_IPV6_EXT, lp.RX_VLAN | lp.RX_IPV6_EXT)
+FLAG_SETS = (0, 0, 0, RX_VLAN, RX_IPV6_EXT, RX_VLAN | RX_IPV6_EXT)
 
 
 def _frames(rng, n, flags, fixed_len):
