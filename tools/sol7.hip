@@ -45,11 +45,13 @@ __device__ __forceinline__ void put(T* c, uint64_t i, T v) { __builtin_nontempor
 
 constexpr int kStep = 4096;
 
-template <int S, bool COLS, bool SCAN>
+template <int S, bool COLS, bool SCAN, int PV = 0, bool WIN = false>
 __global__ __launch_bounds__(64) void glds_persist(const uint8_t* data, const uint32_t* offs, const uint16_t* lens,
                                                    uint64_t n, Cols C, uint32_t* out) {
     __shared__ __attribute__((aligned(16))) uint8_t ring[S * kStep];
     __shared__ __attribute__((aligned(16))) uint32_t ptab[256];
+    // WIN: 64 padded 132-B window slots (the mixed kernel's), filled from the ring
+    __shared__ __attribute__((aligned(16))) uint32_t slots[WIN ? 64 * 33 : 1];
     const int lane = threadIdx.x;
     const uint64_t nruns = (n + 63) / 64;
     const uint64_t nw = gridDim.x, w = blockIdx.x;
@@ -102,12 +104,32 @@ __global__ __launch_bounds__(64) void glds_persist(const uint8_t* data, const ui
         } else {
             acc += g[0] + g[1] + g[2] + g[3];
         }
+        if (WIN) {
+            // every lane copies 8 ring granules into a slot (an upper bound on the
+            // per-step window capture: ~10 frames start per 4 KiB of IMIX)
+#pragma unroll
+            for (int c = 0; c < 8; ++c) {
+                const uint4 v = *reinterpret_cast<const uint4*>(slot + 16 * ((lane * 7 + c * 13) & 255));
+                uint32_t* dst = slots + ((lane * 5 + c) & 63) * 33 + 4 * c;
+                dst[0] = v.x; dst[1] = v.y; dst[2] = v.z; dst[3] = v.w;
+            }
+        }
         cslot = cslot == S - 1 ? 0 : cslot + 1;
         const uint32_t done_b = (s + 1) * kStep;
         while (run < r1 && rend <= done_b) {   // wave-uniform
             const uint64_t f = run * 64 + lane;
+            uint32_t e0 = acc, e1 = acc ^ 1u, e2 = acc ^ 2u, e3 = acc ^ 3u;
+            if (PV) {
+                // the per-run parse emulated: PV VALU ops in four independent chains
+                // reading the slots (WIN) so they cannot be hoisted
+                const uint32_t sv = WIN ? slots[lane * 33] : 0u;
+#pragma unroll 1
+                for (int k = 0; k < PV / 4; ++k) {
+                    e0 = sad(e0 ^ sv, e0); e1 = sad(e1 + sv, e1); e2 = sad(e2 ^ (uint32_t)k, e2); e3 = sad(e3 + (uint32_t)k, e3);
+                }
+            }
             if (f < n) {
-                const uint32_t r = acc + (uint32_t)f;
+                const uint32_t r = acc + (uint32_t)f + (e0 ^ e1 ^ e2 ^ e3);
                 if (COLS) {
                     put<uint16_t>(C.st, f, (uint16_t)r);
                     put<uint16_t>(C.ipc, f, (uint16_t)(r >> 1));
@@ -132,15 +154,15 @@ __global__ __launch_bounds__(64) void glds_persist(const uint8_t* data, const ui
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-template <int S, bool COLS, bool SCAN>
+template <int S, bool COLS, bool SCAN, int PV = 0, bool WIN = false>
 static float timeit(const uint8_t* d, const uint32_t* o, const uint16_t* l, uint64_t n, Cols c, uint32_t* out,
                     int blocks, int reps) {
     hipEvent_t a, b;
     (void)hipEventCreate(&a);
     (void)hipEventCreate(&b);
-    for (int i = 0; i < 3; ++i) hipLaunchKernelGGL((glds_persist<S, COLS, SCAN>), dim3(blocks), dim3(64), 0, 0, d, o, l, n, c, out);
+    for (int i = 0; i < 3; ++i) hipLaunchKernelGGL((glds_persist<S, COLS, SCAN, PV, WIN>), dim3(blocks), dim3(64), 0, 0, d, o, l, n, c, out);
     (void)hipEventRecord(a, 0);
-    for (int i = 0; i < reps; ++i) hipLaunchKernelGGL((glds_persist<S, COLS, SCAN>), dim3(blocks), dim3(64), 0, 0, d, o, l, n, c, out);
+    for (int i = 0; i < reps; ++i) hipLaunchKernelGGL((glds_persist<S, COLS, SCAN, PV, WIN>), dim3(blocks), dim3(64), 0, 0, d, o, l, n, c, out);
     (void)hipEventRecord(b, 0);
     (void)hipEventSynchronize(b);
     float ms = 0;
@@ -148,7 +170,8 @@ static float timeit(const uint8_t* d, const uint32_t* o, const uint16_t* l, uint
     return ms / reps;
 }
 
-int main() {
+int main(int argc, char** argv) {
+    (void)argv;
     const uint64_t n = 1ull << 22;
     std::mt19937_64 rng(7);
     std::vector<uint32_t> offs(n);
@@ -184,13 +207,25 @@ int main() {
     const double alg_cols = (double)bytes + 32.0 * n, alg_read = (double)bytes + 10.0 * n;
     printf("IMIX-shaped batch: %llu frames, %.3f GB\n", (unsigned long long)n, bytes / 1e9);
     for (int round = 0; round < 3; ++round) {
-        for (int wpc : {8, 12, 16}) {
+        for (int wpc : (argc > 1 ? std::vector<int>{7, 8} : std::vector<int>{8, 12, 16})) {
             const int blocks = prop.multiProcessorCount * wpc;
             float t;
 #define RUN(S, COLS, SCAN, ALG)                                                                                  \
     t = timeit<S, COLS, SCAN>(d, o, l, n, c, out, blocks, 20);                                                   \
     printf("waves/CU %2d S=%d %-9s %-5s %8.1f us  %6.0f GB/s (%.1f%% of 8 TB/s)\n", wpc, S, COLS ? "read+cols" : "read", \
            SCAN ? "+scan" : "", t * 1e3, (ALG) / (t * 1e-3) / 1e9, (ALG) / (t * 1e-3) / 1e9 / 80.0);
+            if (argc > 1) {   // the per-run parse and window capture emulated (wpc 7/8: LDS allows 7)
+#define RUNP(PV, WIN)                                                                                          \
+    t = timeit<3, true, true, PV, WIN>(d, o, l, n, c, out, blocks, 20);                                        \
+    printf("waves/CU %2d cols+scan PV=%4d WIN=%d %8.1f us  %6.0f GB/s (%.1f%% of 8 TB/s)\n", wpc, PV, (int)WIN, t * 1e3, \
+           alg_cols / (t * 1e-3) / 1e9, alg_cols / (t * 1e-3) / 1e9 / 80.0);
+                RUNP(0, false)
+                RUNP(0, true)
+                RUNP(400, true)
+                RUNP(800, true)
+                RUNP(1600, true)
+                continue;
+            }
             RUN(3, false, false, alg_read)
             RUN(3, true, false, alg_cols)
             RUN(3, true, true, alg_cols)
