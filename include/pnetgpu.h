@@ -24,8 +24,8 @@
  *                             benches/rs_sender.rs:38-39,70-71 does per frame.
  *   pnetgpu_checksum_slices   pnet_packet::util::checksum (pnet_packet/src/util.rs:76-82),
  *                             re-exported as pnet::util::checksum (src/util.rs:11-12),
- *                             over a batch of slices; _strided: uniform slices
- *                             without descriptor arrays.
+ *                             over a batch of slices; _compact: 8-B descriptors;
+ *                             _strided: uniform slices without descriptor arrays.
  *   pnetgpu_ipv4_checksum_slices  pnet_packet::util::ipv4_checksum with empty
  *                             extra_data (util.rs:92-117), batched.
  *   pnetgpu_ipv6_checksum_slices  pnet_packet::util::ipv6_checksum with empty
@@ -245,6 +245,20 @@ int pnetgpu_tx_fill_checksums(pnetgpu_ctx* ctx, const pnetgpu_batch* batch,
 int pnetgpu_checksum_slices(pnetgpu_ctx* ctx, const uint8_t* data, uint64_t data_bytes,
                             uint64_t n, const uint64_t* offsets, const uint32_t* lengths,
                             const uint32_t* skipwords, uint16_t* out, void* stream);
+
+/* Compact slice descriptor (8 B instead of the 16 B of the three arrays): for
+ * buffers under 4 GiB and slices under 64 KiB. */
+typedef struct pnetgpu_slice_desc {
+    uint32_t offset;     /* slice start, bytes from `data`  */
+    uint16_t length;     /* slice bytes                     */
+    uint16_t skipword;   /* util::checksum's skipword       */
+} pnetgpu_slice_desc;
+
+/* out[i] = util::checksum(data[desc[i].offset, +desc[i].length), desc[i].skipword):
+ * pnetgpu_checksum_slices with compact descriptors (one 8-B load per slice). */
+int pnetgpu_checksum_slices_compact(pnetgpu_ctx* ctx, const uint8_t* data, uint64_t data_bytes,
+                                    uint64_t n, const pnetgpu_slice_desc* desc, uint16_t* out,
+                                    void* stream);
 
 /* out[i] = util::checksum(data[first_offset + i*stride, +slice_len), skipword) for
  * i < n: uniform slices with no descriptor arrays (the reference's own bench

@@ -12,7 +12,7 @@ from .afpacket import AfPacket, tpacket3_walk  # noqa: F401
 from .views import frame_view  # noqa: F401
 from .engine import (ALL_COLUMNS, COUNTER_NAMES, DESC_COMPACT, FIELD_COLUMNS, IPV4_COLUMNS, RECORD_COLUMNS,  # noqa: F401
                      Context, RxResult,
-                     checksum_adv_slices, checksum_slices, checksum_slices_strided, column_bytes, context, ipv4_checksum_slices,
-                     ipv6_checksum_slices, last_rx_kernel, rx_process, tx_fill_checksums)
+                     checksum_adv_slices, checksum_slices, checksum_slices_compact, checksum_slices_strided, column_bytes, context, ipv4_checksum_slices,
+                     ipv6_checksum_slices, last_rx_kernel, rx_process, slice_descriptors, tx_fill_checksums)
 
 __version__ = "0.1.0"

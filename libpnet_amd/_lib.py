@@ -59,6 +59,11 @@ class Batch(ctypes.Structure):
                 ("reserved", ctypes.c_uint32)]
 
 
+class SliceDesc(ctypes.Structure):
+    """pnetgpu_slice_desc: the compact (8-B) slice descriptor."""
+    _fields_ = [("offset", ctypes.c_uint32), ("length", ctypes.c_uint16), ("skipword", ctypes.c_uint16)]
+
+
 # pnetgpu_rx_columns in struct order: the record columns, `counters`, then the
 # header-field columns of ABI v3
 COLUMN_NAMES = ("status", "ip_csum", "l4_csum", "ethertype", "ip_proto", "ttl", "l4_offset", "l4_length",
@@ -99,6 +104,8 @@ def _load():
         f.argtypes = [vp, ctypes.POINTER(Batch), ctypes.POINTER(RxColumns), vp]
     L.pnetgpu_checksum_slices.restype = i32
     L.pnetgpu_checksum_slices.argtypes = [vp, vp, u64, u64, vp, vp, vp, vp, vp]
+    L.pnetgpu_checksum_slices_compact.restype = i32
+    L.pnetgpu_checksum_slices_compact.argtypes = [vp, vp, u64, u64, vp, vp, vp]
     L.pnetgpu_checksum_slices_strided.restype = i32
     L.pnetgpu_checksum_slices_strided.argtypes = [vp, vp, u64, u64, u64, u32, u32, u32, vp, vp]
     for f in (L.pnetgpu_ipv4_checksum_slices, L.pnetgpu_ipv6_checksum_slices):

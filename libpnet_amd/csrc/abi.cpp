@@ -303,6 +303,30 @@ int pnetgpu_checksum_slices_strided(pnetgpu_ctx* ctx, const uint8_t* data, uint6
     return PNETGPU_OK;
 }
 
+int pnetgpu_checksum_slices_compact(pnetgpu_ctx* ctx, const uint8_t* data, uint64_t data_bytes, uint64_t n,
+                                    const pnetgpu_slice_desc* desc, uint16_t* out, void* stream) {
+    pnetgpu::set_last_hip_error(0);
+    if (!ctx) return PNETGPU_EINVAL;
+    if (n == 0) return PNETGPU_OK;
+    if (!data || !desc || !out) return PNETGPU_EINVAL;
+    int rc = set_device(ctx);
+    if (rc) return rc;
+    pnetgpu::SliceArgs a{};
+    align_base(data, data_bytes, &a.data, &a.delta, &a.limit);
+    a.n = n;
+    a.offsets = reinterpret_cast<const uint64_t*>(desc);
+    a.compact = 1;
+    a.out = out;
+    // the same choice as pnetgpu_checksum_slices (by the buffer bytes per slice)
+    const char* kenv = std::getenv("PNETGPU_SLICE_KERNEL");
+    bool run = data_bytes / n <= 256;
+    if (kenv) run = kenv[0] == 'r' ? true : kenv[0] == 'g' ? false : run;
+    const uint64_t per_block = run ? kBlock : kBlock / 16;
+    const int blocks = slice_grid(ctx, run ? 1 : 2, 0, false, (n + per_block - 1) / per_block);
+    if (const int e = pnetgpu::launch_slices(a, 0, run, blocks, static_cast<hipStream_t>(stream))) return pnetgpu::hip_fail((hipError_t)e);
+    return PNETGPU_OK;
+}
+
 int pnetgpu_checksum_slices(pnetgpu_ctx* ctx, const uint8_t* data, uint64_t data_bytes, uint64_t n,
                             const uint64_t* offsets, const uint32_t* lengths, const uint32_t* skipwords,
                             uint16_t* out, void* stream) {

@@ -42,6 +42,7 @@ struct SliceArgs {
     uint16_t* out;
     // strided form (pnetgpu_checksum_slices_strided): slice i = [first + i * stride,
     // +slice_len), one skipword for all; offsets/lengths/skipwords are unused
+    uint32_t compact;    // offsets points to pnetgpu_slice_desc[n] (u32 offset, u16 length, u16 skipword)
     uint32_t strided;
     uint32_t stride;
     uint32_t slice_len;

@@ -73,9 +73,23 @@ __global__ __launch_bounds__(kBlock) void slice_kernel(SliceArgs a) {
     // groups are 16-lane aligned, so every shuffle stays inside one group, whose
     // lanes share i (and therefore control flow)
     for (uint64_t i = gid; i < a.n; i += ngroups) {
-        const uint64_t off = (a.strided ? a.first + i * a.stride : a.offsets[i]) + a.delta;   // wave-uniform branch
-        uint32_t len = a.strided ? a.slice_len : a.lengths[i];
-        const uint32_t skip = a.strided ? a.skipword : a.skipwords[i];
+        uint64_t off;
+        uint32_t len, skip;
+        if (a.strided) {            // wave-uniform branches: strided, compact or full descriptors
+            off = a.first + i * a.stride;
+            len = a.slice_len;
+            skip = a.skipword;
+        } else if (a.compact) {
+            const uint2 dsc = reinterpret_cast<const uint2*>(a.offsets)[i];
+            off = dsc.x;
+            len = dsc.y & 0xFFFFu;
+            skip = dsc.y >> 16;
+        } else {
+            off = a.offsets[i];
+            len = a.lengths[i];
+            skip = a.skipwords[i];
+        }
+        off += a.delta;
         if (off > a.limit || (uint64_t)len > a.limit - off) len = 0;
         uint32_t acc = group_range_sum(a.data, off, len, j);
         uint32_t pe = 0, elen = 0;
@@ -146,9 +160,21 @@ __global__ __launch_bounds__(kBlock) void slice_run_kernel(SliceArgs a) {
         uint64_t off = 0;
         uint32_t len = 0, skip = 0;
         if (in) {
-            off = (a.strided ? a.first + i * a.stride : a.offsets[i]) + a.delta;   // wave-uniform branch
-            len = a.strided ? a.slice_len : a.lengths[i];
-            skip = a.strided ? a.skipword : a.skipwords[i];
+            if (a.strided) {        // wave-uniform branches: strided, compact (one 8-B load) or full descriptors
+                off = a.first + i * a.stride;
+                len = a.slice_len;
+                skip = a.skipword;
+            } else if (a.compact) {
+                const uint2 dsc = reinterpret_cast<const uint2*>(a.offsets)[i];
+                off = dsc.x;
+                len = dsc.y & 0xFFFFu;
+                skip = dsc.y >> 16;
+            } else {
+                off = a.offsets[i];
+                len = a.lengths[i];
+                skip = a.skipwords[i];
+            }
+            off += a.delta;
             if (off > a.limit || (uint64_t)len > a.limit - off) {
                 len = 0;
                 off = 0;
@@ -192,14 +218,36 @@ __global__ __launch_bounds__(kBlock) void slice_run_kernel(SliceArgs a) {
             v[c] = small && (uint32_t)c < nneed ? load16(fb + 16 * c) : make_uint4(0, 0, 0, 0);
         uint32_t acc = 0;
         if (small) {
+            // every loaded granule summed whole (the others are zero), then the
+            // bytes before the slice in granule 0 and after it in the last one
+            // subtracted: ~50 VALU instead of a mask pair per dword (~190; a
+            // wave64 VALU op takes 4 cycles, and VALU bound this shape)
 #pragma unroll
-            for (int c = 0; c < kSmall; ++c) {
-                const uint32_t dw[4] = {v[c].x, v[c].y, v[c].z, v[c].w};
+            for (int c = 0; c < kSmall; ++c) acc = sad(v[c].w, sad(v[c].z, sad(v[c].y, sad(v[c].x, acc))));
+            if (nneed) {
+                // head: bytes [0, sh) of granule 0
+                const uint32_t q = (uint32_t)sh >> 2, r = (uint32_t)sh & 3u;
+                const uint32_t s1 = sad(v[0].x, 0u), s2 = sad(v[0].y, s1), s3 = sad(v[0].z, s2);
+                uint32_t hw = v[0].x, hs = 0u;
+                hw = q == 1u ? v[0].y : hw; hs = q == 1u ? s1 : hs;
+                hw = q == 2u ? v[0].z : hw; hs = q == 2u ? s2 : hs;
+                hw = q == 3u ? v[0].w : hw; hs = q == 3u ? s3 : hs;
+                acc -= sad(hw & (r ? 0xFFFFFFFFu >> (32u - 8u * r) : 0u), hs);
+                // tail: bytes [eb, 16) of the last granule, eb = e - 16 (nneed - 1) in 1..16
+                const uint32_t lg = nneed - 1u;
+                uint4 g = v[0];
 #pragma unroll
-                for (int t = 0; t < 4; ++t) {
-                    const int p = 16 * c + 4 * t;
-                    acc = sad(dw[t] & first_bytes(clamp04(e - p)) & ~first_bytes(clamp04(sh - p)), acc);
-                }
+                for (int c = 1; c < kSmall; ++c) g = lg == (uint32_t)c ? v[c] : g;
+                const uint32_t eb = (uint32_t)e - 16u * lg;
+                const uint32_t tq = eb >> 2, tr = eb & 3u;           // dword and byte where the excess starts
+                const uint32_t u3 = sad(g.w, 0u), u2 = sad(g.z, u3), u1 = sad(g.y, u2);   // suffix sums from dword t+1
+                uint32_t tw = g.x, ts = u1;
+                tw = tq == 1u ? g.y : tw; ts = tq == 1u ? u2 : ts;
+                tw = tq == 2u ? g.z : tw; ts = tq == 2u ? u3 : ts;
+                tw = tq >= 3u ? g.w : tw; ts = tq >= 3u ? 0u : ts;
+                // eb == 16 (tq 4): nothing past the slice in this granule
+                const uint32_t keep = tr ? 0xFFFFFFFFu >> (32u - 8u * tr) : 0u;
+                acc -= tq >= 4u ? 0u : sad(tw & ~keep, ts);
             }
         } else {
             acc = gsum[wv][lane];

@@ -283,6 +283,31 @@ def checksum_slices(data, offsets, lengths, skipwords, stream=None):
     return _slices("pnetgpu_checksum_slices", data, offsets, lengths, skipwords, stream=stream)
 
 
+def slice_descriptors(offsets, lengths, skipwords, device=None):
+    """Pack (offset, length, skipword) triples into compact pnetgpu_slice_desc
+    records (u32, u16, u16 = 8 B each) as an int64 tensor (on `device` if given)."""
+    offsets = np.asarray(offsets, dtype=np.uint64)
+    lengths = np.asarray(lengths, dtype=np.uint64)
+    skipwords = np.asarray(skipwords, dtype=np.uint64)
+    if offsets.size and (offsets.max() > 0xFFFFFFFF or lengths.max() > 0xFFFF or skipwords.max() > 0xFFFF):
+        raise ValueError("compact slice descriptors need offsets < 2^32, lengths and skipwords < 2^16")
+    packed = offsets | (lengths << np.uint64(32)) | (skipwords << np.uint64(48))
+    t = torch.from_numpy(packed.view(np.int64))
+    return t.to(device) if device is not None else t
+
+
+def checksum_slices_compact(data, desc, stream=None):
+    """out[i] = util::checksum over compact descriptors (slice_descriptors(...) on the
+    data's device): pnetgpu_checksum_slices_compact."""
+    _check_u8_cuda(data, "data")
+    n = desc.numel()
+    out = torch.empty(n, dtype=torch.int16, device=data.device)
+    ctx = context(data.device.index)
+    check(lib.pnetgpu_checksum_slices_compact(ctx.handle, _ptr(data), data.numel(), n, _ptr(desc), _ptr(out),
+                                              _stream_handle(stream, data.device)), "pnetgpu_checksum_slices_compact")
+    return out
+
+
 def checksum_slices_strided(data, n, stride, slice_len, skipword, first_offset=0, stream=None):
     """out[i] = util::checksum(data[first_offset + i*stride, +slice_len), skipword), i < n:
     uniform slices without descriptor arrays (pnetgpu_checksum_slices_strided)."""

@@ -75,3 +75,24 @@ def test_include_headers_compile_as_c():
     for h in ("pnetgpu.h", "pnetgpu_synth.h", "pnetgpu_ring.h", "pnetgpu_afpacket.h"):
         subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-fsyntax-only", "-x", "c",
                         os.path.join(ROOT, "include", h)], check=True)
+
+
+def test_compact_slice_descriptor_packing():
+    """slice_descriptors packs (offset, length, skipword) exactly as the C struct
+    pnetgpu_slice_desc lays them out (u32, u16, u16 little-endian), and refuses
+    values the compact form cannot hold."""
+    import ctypes
+    import numpy as np
+    import pytest
+    from libpnet_amd import _lib
+    offs, lens, skips = [0, 5, 0xFFFFFFFF], [20, 0, 0xFFFF], [5, 0xFFFF, 0]
+    t = lp.slice_descriptors(offs, lens, skips)
+    raw = t.numpy().tobytes()
+    arr = (_lib.SliceDesc * 3).from_buffer_copy(raw)
+    assert ctypes.sizeof(_lib.SliceDesc) == 8
+    assert [(d.offset, d.length, d.skipword) for d in arr] == list(zip(offs, lens, skips))
+    with pytest.raises(ValueError):
+        lp.slice_descriptors([1 << 32], [1], [0])
+    with pytest.raises(ValueError):
+        lp.slice_descriptors([0], [1 << 16], [0])
+    assert np.asarray(lp.slice_descriptors([], [], [])).size == 0

@@ -18,7 +18,7 @@ from libpnet_amd import _lib, ring
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 STRUCTS = {"pnetgpu_batch": _lib.Batch, "pnetgpu_rx_columns": _lib.RxColumns,
-           "pnetgpu_ring_batch": ring.RingBatch}
+           "pnetgpu_ring_batch": ring.RingBatch, "pnetgpu_slice_desc": _lib.SliceDesc}
 RUST_SIZES = {"u8": 1, "u16": 2, "u32": 4, "u64": 8, "c_int": 4}
 
 

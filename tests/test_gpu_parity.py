@@ -769,3 +769,54 @@ def test_strided_slices_random_shapes_fuzz():
         got = lp.checksum_slices_strided(d, n, stride, slen, skip, first_offset=first - mis)
         want = _strided_want(buf[mis:], n, first - mis, stride, slen, skip)
         assert np.array_equal(got.cpu().numpy().view(np.uint16), want), (stride, slen, n, first, mis, skip)
+
+
+# ---- util::checksum over compact (8-B) slice descriptors ----
+
+def test_compact_slices_kats_and_random_vs_oracle():
+    """pnetgpu_checksum_slices_compact: the util.rs / icmp.rs KAT slices at six
+    misalignments, and 20,000 random slices (0..2000 B, any alignment, skipword
+    inside / at the edge of / past the slice, gaps and overlaps) through both
+    slice kernels, against the oracle."""
+    vs = kats.by_kind("sum_be_words", "checksum")
+    for misalign in (0, 1, 2, 3, 5, 15):
+        parts, offs, lens, skips, want = [], [], [], [], []
+        pos = 0
+        for v in vs:
+            pad = (misalign - pos) % 16
+            parts.append(bytes(pad))
+            pos += pad
+            offs.append(pos)
+            lens.append(len(v["data"]))
+            skips.append(v["skipword"])
+            parts.append(v["data"])
+            pos += len(v["data"])
+            want.append(v["expected"] if v["kind"] == "checksum" else
+                        (pyoracle.finalize(v["expected"]) if v["data"] else 0))
+        buf = np.frombuffer(b"".join(parts) + bytes(32), dtype=np.uint8)
+        desc = lp.slice_descriptors(offs, lens, skips, device=DEV)
+        got = lp.checksum_slices_compact(to_dev(buf), desc).cpu().numpy().view(np.uint16)
+        assert list(got) == want, misalign
+    rng = np.random.default_rng(77)
+    buf = rng.integers(0, 256, 3 << 20, dtype=np.uint8)
+    n = 20000
+    lens = rng.integers(0, 2001, n).astype(np.uint32)
+    lens[rng.random(n) < 0.5] %= 64                       # mostly short, as packets' headers are
+    offs = rng.integers(0, buf.size - 2001, n).astype(np.uint64)
+    skips = np.where(rng.random(n) < 0.8, rng.integers(0, 40, n), rng.integers(0, 1200, n)).astype(np.uint32)
+    want = coracle.checksum_slices(buf, offs, lens, skips)
+    desc = lp.slice_descriptors(offs, lens, skips, device=DEV)
+    d = to_dev(np.concatenate([buf, np.zeros(32, np.uint8)]))[: buf.size]
+    for kern in ("run", "group"):
+        os.environ["PNETGPU_SLICE_KERNEL"] = kern
+        try:
+            got = lp.checksum_slices_compact(d, desc).cpu().numpy().view(np.uint16)
+        finally:
+            del os.environ["PNETGPU_SLICE_KERNEL"]
+        assert np.array_equal(got, want), kern
+    big = np.full(70000, 7, np.uint8)                     # the compact maximum: 65535-B slices
+    desc = lp.slice_descriptors([0, 1, 4465], [65535, 65535, 65535], [0, 3, 32767], device=DEV)
+    got = lp.checksum_slices_compact(to_dev(big), desc).cpu().numpy().view(np.uint16)
+    want = coracle.checksum_slices(big, np.array([0, 1, 4465], np.uint64), np.full(3, 65535, np.uint32),
+                                   np.array([0, 3, 32767], np.uint32))
+    assert np.array_equal(got, want)

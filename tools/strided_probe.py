@@ -35,8 +35,12 @@ for size, n in ((20, 1 << 24), (64, 1 << 23), (1024, 1 << 20)):
         offs = torch.arange(n, dtype=torch.int64, device=dev) * size
         lens = torch.full((n,), size, dtype=torch.int32, device=dev)
         sk = torch.full((n,), 5, dtype=torch.int32, device=dev)
+        desc = lp.slice_descriptors(np.arange(n, dtype=np.uint64) * np.uint64(size), np.full(n, size),
+                                    np.full(n, 5), device=dev)
         for _ in range(2):
+            t_co = timeit(lambda: lp.checksum_slices_compact(d, desc, stream=s))
             t_st = timeit(lambda: lp.checksum_slices_strided(d, n, size, size, 5, stream=s))
             t_de = timeit(lambda: lp.checksum_slices(d, offs, lens, sk, stream=s))
             print(f"{size:5d}-B x {n}: strided {t_st*1e3:7.1f} us ({n*(size+2)/(t_st*1e-3)/8e12:.1%} of 8 TB/s)  "
-                  f"descriptors {t_de*1e3:7.1f} us ({n*(size+18)/(t_de*1e-3)/8e12:.1%})", flush=True)
+                  f"descriptors {t_de*1e3:7.1f} us ({n*(size+18)/(t_de*1e-3)/8e12:.1%})  "
+                  f"compact {t_co*1e3:7.1f} us ({n*(size+10)/(t_co*1e-3)/8e12:.1%})", flush=True)
