@@ -233,21 +233,23 @@ __global__ __launch_bounds__(kBlock) void slice_run_kernel(SliceArgs a) {
                 hw = q == 2u ? v[0].z : hw; hs = q == 2u ? s2 : hs;
                 hw = q == 3u ? v[0].w : hw; hs = q == 3u ? s3 : hs;
                 acc -= sad(hw & (r ? 0xFFFFFFFFu >> (32u - 8u * r) : 0u), hs);
-                // tail: bytes [eb, 16) of the last granule, eb = e - 16 (nneed - 1) in 1..16
-                const uint32_t lg = nneed - 1u;
-                uint4 g = v[0];
+                // tail: bytes [e - 16 c, 16) of every granule c, clamped: nothing
+                // below the last granule, zero data above it (no dynamic
+                // indexing of v: a select of whole granules became a scratch
+                // array and ran 3.5x slower)
 #pragma unroll
-                for (int c = 1; c < kSmall; ++c) g = lg == (uint32_t)c ? v[c] : g;
-                const uint32_t eb = (uint32_t)e - 16u * lg;
-                const uint32_t tq = eb >> 2, tr = eb & 3u;           // dword and byte where the excess starts
-                const uint32_t u3 = sad(g.w, 0u), u2 = sad(g.z, u3), u1 = sad(g.y, u2);   // suffix sums from dword t+1
-                uint32_t tw = g.x, ts = u1;
-                tw = tq == 1u ? g.y : tw; ts = tq == 1u ? u2 : ts;
-                tw = tq == 2u ? g.z : tw; ts = tq == 2u ? u3 : ts;
-                tw = tq >= 3u ? g.w : tw; ts = tq >= 3u ? 0u : ts;
-                // eb == 16 (tq 4): nothing past the slice in this granule
-                const uint32_t keep = tr ? 0xFFFFFFFFu >> (32u - 8u * tr) : 0u;
-                acc -= tq >= 4u ? 0u : sad(tw & ~keep, ts);
+                for (int c = 0; c < kSmall; ++c) {
+                    const int ebi = e - 16 * c;
+                    const uint32_t eb = (uint32_t)min(max(ebi, 0), 16);
+                    const uint32_t tq = eb >> 2, tr = eb & 3u;
+                    const uint32_t u3 = sad(v[c].w, 0u), u2 = sad(v[c].z, u3), u1 = sad(v[c].y, u2);
+                    uint32_t tw = v[c].x, ts = u1;
+                    tw = tq == 1u ? v[c].y : tw; ts = tq == 1u ? u2 : ts;
+                    tw = tq == 2u ? v[c].z : tw; ts = tq == 2u ? u3 : ts;
+                    tw = tq >= 3u ? v[c].w : tw; ts = tq >= 3u ? 0u : ts;
+                    const uint32_t keep = tr ? 0xFFFFFFFFu >> (32u - 8u * tr) : 0u;
+                    acc -= tq >= 4u ? 0u : sad(tw & ~keep, ts);
+                }
             }
         } else {
             acc = gsum[wv][lane];
