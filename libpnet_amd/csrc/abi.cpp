@@ -222,6 +222,17 @@ int pnetgpu_tx_fill_checksums(pnetgpu_ctx* ctx, const pnetgpu_batch* b, const pn
     return rx_common(ctx, b, cols, stream, true);
 }
 
+// slice_run_kernel stages a run of 64 small sorted slices through LDS when
+// they span at least this many bytes (up to 5 KiB): coalesced loads beat the
+// per-lane gathers once the slices are >= ~32 B apart (each gather then
+// touches one cache line per lane); below, the gathers share lines and the
+// staging's latency costs more than it saves. PNETGPU_SLICE_DENSE_SPAN
+// overrides (0: always stage, 65536: never).
+static uint32_t dense_span() {
+    const char* env = std::getenv("PNETGPU_SLICE_DENSE_SPAN");
+    return env ? (uint32_t)std::strtoul(env, nullptr, 10) : 2048u;
+}
+
 static int slices_common(pnetgpu_ctx* ctx, const uint8_t* data, uint64_t data_bytes, uint64_t n,
                          const uint64_t* offsets, const uint32_t* lengths, const uint32_t* skipwords,
                          const uint8_t* addrs, const uint8_t* protos, uint16_t* out, int pseudo,
@@ -245,6 +256,7 @@ static int slices_common(pnetgpu_ctx* ctx, const uint8_t* data, uint64_t data_by
     a.extra_offsets = extra_offsets;
     a.extra_lengths = extra_lengths;
     a.out = out;
+    a.dense_min = dense_span();
     // Kernel choice. The slice lengths are device-resident, so the host decides
     // by the BUFFER bytes per slice (data_bytes / n), which equals the bytes per
     // slice only for slices that tile the buffer: slice_run_kernel (one wave per
@@ -289,6 +301,7 @@ int pnetgpu_checksum_slices_strided(pnetgpu_ctx* ctx, const uint8_t* data, uint6
     a.stride = stride;
     a.slice_len = slice_len;
     a.skipword = skipword;
+    a.dense_min = dense_span();
     // small uniform slices (<= 64 B at <= 64 B apart): runs staged through LDS;
     // otherwise the descriptor kernels with computed offsets (the same choice
     // as pnetgpu_checksum_slices, by the slice length the caller gave)
@@ -317,6 +330,7 @@ int pnetgpu_checksum_slices_compact(pnetgpu_ctx* ctx, const uint8_t* data, uint6
     a.offsets = reinterpret_cast<const uint64_t*>(desc);
     a.compact = 1;
     a.out = out;
+    a.dense_min = dense_span();
     // the same choice as pnetgpu_checksum_slices (by the buffer bytes per slice)
     const char* kenv = std::getenv("PNETGPU_SLICE_KERNEL");
     bool run = data_bytes / n <= 256;

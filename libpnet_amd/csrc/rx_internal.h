@@ -48,6 +48,9 @@ struct SliceArgs {
     uint32_t slice_len;
     uint32_t skipword;
     uint64_t first;
+    // slice_run_kernel: a run of small sorted slices is staged through LDS when
+    // its span is at least this many bytes (dense_span())
+    uint32_t dense_min;
 };
 
 // Kernel kinds: the register-resident small-frame kernel (fixed stride, frames

@@ -21,12 +21,42 @@ namespace {
 #ifndef PNET_SLICE_U
 #define PNET_SLICE_U 4   // loads in flight per lane in the slice kernels
 #endif
+// Sum of bytes [b, 16) of granule g: the dword holding b in part, the ones
+// after it whole (b = 16: none). Granules by value, picked with selects: an
+// indexed pick (or one through an array reference) becomes a scratch array.
+__device__ __forceinline__ uint32_t granule_tail(uint4 g, uint32_t b) {
+    const uint32_t tq = b >> 2, tr = b & 3u;
+    const uint32_t u3 = sad(g.w, 0u), u2 = sad(g.z, u3), u1 = sad(g.y, u2);
+    uint32_t tw = g.x, ts = u1;
+    tw = tq == 1u ? g.y : tw; ts = tq == 1u ? u2 : ts;
+    tw = tq == 2u ? g.z : tw; ts = tq == 2u ? u3 : ts;
+    tw = tq >= 3u ? g.w : tw; ts = tq >= 3u ? 0u : ts;
+    const uint32_t keep = tr ? 0xFFFFFFFFu >> (32u - 8u * tr) : 0u;
+    return tq >= 4u ? 0u : sad(tw & ~keep, ts);
+}
+
+// Sum of bytes [0, b) of granule g (b < 16).
+__device__ __forceinline__ uint32_t granule_head(uint4 g, uint32_t b) {
+    const uint32_t q = b >> 2, r = b & 3u;
+    const uint32_t s1 = sad(g.x, 0u), s2 = sad(g.y, s1), s3 = sad(g.z, s2);
+    uint32_t hw = g.x, hs = 0u;
+    hw = q == 1u ? g.y : hw; hs = q == 1u ? s1 : hs;
+    hw = q == 2u ? g.z : hw; hs = q == 2u ? s2 : hs;
+    hw = q == 3u ? g.w : hw; hs = q == 3u ? s3 : hs;
+    return sad(hw & (r ? 0xFFFFFFFFu >> (32u - 8u * r) : 0u), hs);
+}
+
+__device__ __forceinline__ uint32_t granule_sum(uint4 g, uint32_t acc) {
+    return sad(g.w, sad(g.z, sad(g.y, sad(g.x, acc))));
+}
+
 // Weighted byte sum of [off, off+len) (absolute offsets into a.data) by one
-// 16-lane group: coalesced aligned granules, U loads in flight per lane (the
-// 16 lanes cover 256 B per load round), byte masks only on the slice's first
-// and last granule, shuffle-reduced so every lane of the group returns the total.
+// G-lane group (G-aligned lanes): coalesced aligned granules, U loads in
+// flight per lane (the group covers 16 G U B per load round), byte masks only
+// on the slice's first and last granule, shuffle-reduced so every lane of the
+// group returns the total.
+template <int G, int U>
 __device__ __forceinline__ uint32_t group_range_sum(const uint8_t* data, uint64_t off, uint32_t len, int j) {
-    constexpr int G = 16, U = PNET_SLICE_U;
     const int sh = (int)(off & 15);
     const uint8_t* fb = data + (off - (uint64_t)sh);
     const int e = sh + (int)len;
@@ -43,16 +73,13 @@ __device__ __forceinline__ uint32_t group_range_sum(const uint8_t* data, uint64_
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint32_t c = c0 + u * G;
-            const uint32_t dw[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-            if (c == 0 || c + 1 == nneed) {          // edge granule (zero when c >= nneed)
-                const int p = (int)(16u * c);
-#pragma unroll
-                for (int t = 0; t < 4; ++t) {
-                    const uint32_t mk = first_bytes(clamp04(e - p - 4 * t)) & ~first_bytes(clamp04(sh - p - 4 * t));
-                    acc = sad(dw[t] & mk, acc);
-                }
-            } else {
-                acc = sad(dw[3], sad(dw[2], sad(dw[1], sad(dw[0], acc))));
+            acc = granule_sum(v[u], acc);
+            // edge granules (the slice's first and last; zero data past nneed):
+            // the bytes before sh and from e on subtracted, without divergence
+            // (a masked-sum branch ran both paths whenever any lane had an edge)
+            if (__ballot(c == 0 || c + 1 >= nneed)) {   // wave-uniform
+                acc -= granule_head(v[u], c == 0 ? (uint32_t)sh : 0u);
+                acc -= granule_tail(v[u], (uint32_t)min(max(e - (int)(16u * c), 0), 16));
             }
         }
     }
@@ -91,7 +118,7 @@ __global__ __launch_bounds__(kBlock) void slice_kernel(SliceArgs a) {
         }
         off += a.delta;
         if (off > a.limit || (uint64_t)len > a.limit - off) len = 0;
-        uint32_t acc = group_range_sum(a.data, off, len, j);
+        uint32_t acc = group_range_sum<G, PNET_SLICE_U>(a.data, off, len, j);
         uint32_t pe = 0, elen = 0;
         if (EXTRA) {
             // sum_be_words(extra, extra.len() / 2): every whole word, never the odd
@@ -100,7 +127,7 @@ __global__ __launch_bounds__(kBlock) void slice_kernel(SliceArgs a) {
             const uint64_t eoff = a.extra_offsets[i] + a.delta;
             elen = a.extra_lengths[i];
             if (eoff > a.limit || (uint64_t)elen > a.limit - eoff) elen = 0;
-            const uint32_t te = group_range_sum(a.data, eoff, elen & ~1u, j);
+            const uint32_t te = group_range_sum<G, PNET_SLICE_U>(a.data, eoff, elen & ~1u, j);
             pe = fold16(te);
             if (!(eoff & 1)) pe = bswap16(pe);
         }
@@ -134,20 +161,68 @@ __global__ __launch_bounds__(kBlock) void slice_kernel(SliceArgs a) {
     }
 }
 
+// Weighted byte sum of granules c0..c0+3 (g0..g3, zero past the slice's nneed)
+// of a slice [sh, e) (bytes from its first granule's start): every granule
+// summed whole, then the bytes before the slice in granule 0 (c0 == 0 only)
+// and from e on in every granule subtracted, clamped: nothing below the last
+// granule, zero data above it. ~50 VALU instead of a mask pair per dword
+// (~190; a wave64 VALU op takes 4 cycles, and VALU bounds the 20-B shape).
+// two (wave-uniform): no lane has granules c0+2, c0+3.
+__device__ __forceinline__ uint32_t chunk_sum(uint4 g0, uint4 g1, uint4 g2, uint4 g3, int c0, int sh, int e,
+                                              uint32_t nneed, bool two) {
+    const auto clamp16 = [](int x) { return (uint32_t)min(max(x, 0), 16); };
+    uint32_t acc = granule_sum(g1, granule_sum(g0, 0u));
+    if (!two) acc = granule_sum(g3, granule_sum(g2, acc));
+    if (nneed > (uint32_t)c0) {
+        if (c0 == 0) acc -= granule_head(g0, (uint32_t)sh);
+        acc -= granule_tail(g0, clamp16(e - 16 * c0)) + granule_tail(g1, clamp16(e - 16 * (c0 + 1)));
+        if (!two) acc -= granule_tail(g2, clamp16(e - 16 * (c0 + 2))) + granule_tail(g3, clamp16(e - 16 * (c0 + 3)));
+    }
+    return acc;
+}
+
+// Sums of the slices of a run listed in mask (a bit per lane), G lanes per
+// slice, 64 / G slices per pass: lane sl's slice total lands in gsum[sl].
+template <int G, int U>
+__device__ __forceinline__ void listed_sums(uint64_t mask, int lane, uint8_t* list, uint32_t* gsum,
+                                            const uint8_t* data, uint64_t off, uint32_t len) {
+    if ((mask >> lane) & 1ull) list[__popcll(mask & ((1ull << lane) - 1ull))] = (uint8_t)lane;
+    wave_sync();
+    const int nb = __popcll(mask);
+    const int j = lane % G;
+    for (int k0 = 0; k0 < nb; k0 += kWave / G) {   // wave-uniform; a group's lanes share k
+        const int k = k0 + lane / G;
+        const int sl = k < nb ? list[k] : 0;
+        // both shuffles unconditional: a shuffle under `k < nb` would read its
+        // source lane with that lane masked off
+        const uint64_t soff = (uint64_t)__shfl((unsigned long long)off, sl);
+        const uint32_t sl_len = (uint32_t)__shfl((int)len, sl);
+        const uint32_t t = group_range_sum<G, U>(data, soff, k < nb ? sl_len : 0u, j);
+        if (k < nb && j == 0) gsum[sl] = t;
+    }
+    wave_sync();
+}
+
 // slice_run_kernel: the same results without the extra slice (util::checksum,
 // ipv4_checksum, ipv6_checksum), for batches of any slice sizes but built for
 // small ones (the reference's own bench shape is a 20-B slice,
 // checksum_benchmarks.rs:8-12). One wave per run of 64 slices, lane l <-> slice
 // l: coalesced descriptor loads, a slice of at most kSmall granules summed by
-// its own lane (all its loads issued at once, with the two skipped-word bytes),
-// longer slices listed and summed by 16-lane groups as in slice_kernel, and one
-// coalesced 2-B store per lane. slice_kernel gave 16 lanes to every slice: a
-// 20-B slice left 14 of them idle and the results went out as 2-B stores
-// scattered 32 B apart.
+// its own lane (all its loads issued at once, with the two skipped-word
+// bytes), runs of small sorted slices staged through LDS instead (dense runs,
+// below), longer slices listed and summed by 2-, 4- or 16-lane groups (the
+// last as in slice_kernel), and one coalesced 2-B store per lane.
+// slice_kernel gave 16 lanes to every slice: a 20-B slice left 14 of them idle
+// and the results went out as 2-B stores scattered 32 B apart.
+#ifndef PNET_RUN_MINWAVES
+#define PNET_RUN_MINWAVES 1   // A/B: waves per SIMD the register allocation must allow
+#endif
 template <int PSEUDO>
-__global__ __launch_bounds__(kBlock) void slice_run_kernel(SliceArgs a) {
-    constexpr int kSmall = 4;    // granules summed by the slice's own lane
-    constexpr int G = 16;
+__global__ __launch_bounds__(kBlock, PNET_RUN_MINWAVES) void slice_run_kernel(SliceArgs a) {
+    constexpr int kSmall = 4;    // granules summed by the slice's own lane (<= 49 B at any alignment)
+    constexpr int kMedium = 16;  // granules of a medium slice, one load round of its group (<= 241 B)
+    constexpr int kDense = 5 * kWave;   // granules a dense run may span (5 KiB)
+    __shared__ uint4 dstage[kWavesPerBlock][kDense];
     __shared__ uint32_t gsum[kWavesPerBlock][kWave];
     __shared__ uint8_t glist[kWavesPerBlock][kWave];
     const int lane = threadIdx.x & (kWave - 1);
@@ -188,69 +263,69 @@ __global__ __launch_bounds__(kBlock) void slice_run_kernel(SliceArgs a) {
         // skipped word: its bytes [2 skip, 2 skip + 2) that lie in the slice (util.rs:166-178)
         const uint64_t q = 2ull * skip;
         const bool s0 = q < len, s1 = q + 1 < len;
+        // dense run: every slice small and inside [lane 0's granule, the last
+        // lane's end) with that span at most kDense granules and at least
+        // a.dense_min bytes (sorted, packed slices: header fields, back-to-back
+        // records). The span then arrives as
+        // coalesced 1-KiB wave loads into an LDS stage and each lane reads its
+        // granules there, instead of 3 granule + 2 byte gathers per lane at the
+        // slice stride (the strided kernel's staging, for descriptors).
+        const int last = (int)min<uint64_t>((uint64_t)kWave - 1, a.n - 1 - run * kWave);
+        const uint64_t base = (uint64_t)__shfl((unsigned long long)off, 0) & ~15ull;
+        const uint64_t top = (uint64_t)__shfl((unsigned long long)(off + len), last);
+        const bool fits = !in || !len || (small && off >= base && off + len <= top);
+        const bool dense = __ballot(!fits) == 0ull && top > base && top - base <= 16ull * kDense &&
+                           top - base >= a.dense_min;
         uint32_t b0 = 0, b1 = 0;                 // in flight across the group phase
-        if (s0) b0 = a.data[off + q];
-        if (s1) b1 = a.data[off + q + 1];
-        // slices past kSmall granules: 16-lane groups over the wave's list of them
-        // (before the small slices' loads: no granule registers held across it)
-        const uint64_t bmask = __ballot(in && !small);
-        if (bmask) {
-            if (in && !small) glist[wv][__popcll(bmask & ((1ull << lane) - 1ull))] = (uint8_t)lane;
-            wave_sync();
-            const int nb = __popcll(bmask);
-            const int j = lane % G;
-            for (int k0 = 0; k0 < nb; k0 += kWave / G) {   // wave-uniform; a group's lanes share k
-                const int k = k0 + lane / G;
-                const int sl = k < nb ? glist[wv][k] : 0;
-                // both shuffles unconditional: a shuffle under `k < nb` would read
-                // its source lane with that lane masked off
-                const uint64_t soff = (uint64_t)__shfl((unsigned long long)off, sl);
-                const uint32_t sl_len = (uint32_t)__shfl((int)len, sl);
-                const uint32_t slen = k < nb ? sl_len : 0u;
-                const uint32_t t = group_range_sum(a.data, soff, slen, j);
-                if (k < nb && j == 0) gsum[wv][sl] = t;
-            }
-            wave_sync();
+        if (!dense) {
+            if (s0) b0 = a.data[off + q];
+            if (s1) b1 = a.data[off + q + 1];
         }
-        uint4 v[kSmall];
-#pragma unroll
-        for (int c = 0; c < kSmall; ++c)
-            v[c] = small && (uint32_t)c < nneed ? load16(fb + 16 * c) : make_uint4(0, 0, 0, 0);
+        // slices past kSmall granules: listed by size class and summed by groups
+        // of G lanes, 4 granules per lane (2 lanes up to 8 granules, 4 up to
+        // kMedium; one load round, 32 or 16 slices per pass) and 16-lane groups
+        // for longer ones. Narrow groups: the VALU of a pass is spent on the
+        // slices of that pass (80-B slices: 2 lanes 150 us, 4: 172, 8: 205,
+        // 16: 335; profiles/r03/slices); a slice-own gather at a 128-B stride
+        // was 177-200 us. Before the small slices' loads: no granule registers
+        // held across them.
+        const bool med8 = in && !small && nneed <= 8u;
+        const bool med16 = in && !small && !med8 && nneed <= (uint32_t)kMedium;
+        const uint64_t m8 = __ballot(med8), m16 = __ballot(med16);
+        const uint64_t lmask = __ballot(in && !small && !med8 && !med16);
+        if (m8) listed_sums<2, 4>(m8, lane, glist[wv], gsum[wv], a.data, off, len);
+        if (m16) listed_sums<4, 4>(m16, lane, glist[wv], gsum[wv], a.data, off, len);
+        if (lmask) listed_sums<16, PNET_SLICE_U>(lmask, lane, glist[wv], gsum[wv], a.data, off, len);
         uint32_t acc = 0;
-        if (small) {
-            // every loaded granule summed whole (the others are zero), then the
-            // bytes before the slice in granule 0 and after it in the last one
-            // subtracted: ~50 VALU instead of a mask pair per dword (~190; a
-            // wave64 VALU op takes 4 cycles, and VALU bound this shape)
+        if (dense) {                             // wave-uniform
+            uint4* st = dstage[wv];
+            const uint64_t g0 = base >> 4;
+            const uint32_t ng = (uint32_t)(((top + 15) >> 4) - g0);
+            uint4 t[kDense / kWave];
 #pragma unroll
-            for (int c = 0; c < kSmall; ++c) acc = sad(v[c].w, sad(v[c].z, sad(v[c].y, sad(v[c].x, acc))));
-            if (nneed) {
-                // head: bytes [0, sh) of granule 0
-                const uint32_t q = (uint32_t)sh >> 2, r = (uint32_t)sh & 3u;
-                const uint32_t s1 = sad(v[0].x, 0u), s2 = sad(v[0].y, s1), s3 = sad(v[0].z, s2);
-                uint32_t hw = v[0].x, hs = 0u;
-                hw = q == 1u ? v[0].y : hw; hs = q == 1u ? s1 : hs;
-                hw = q == 2u ? v[0].z : hw; hs = q == 2u ? s2 : hs;
-                hw = q == 3u ? v[0].w : hw; hs = q == 3u ? s3 : hs;
-                acc -= sad(hw & (r ? 0xFFFFFFFFu >> (32u - 8u * r) : 0u), hs);
-                // tail: bytes [e - 16 c, 16) of every granule c, clamped: nothing
-                // below the last granule, zero data above it (no dynamic
-                // indexing of v: a select of whole granules became a scratch
-                // array and ran 3.5x slower)
-#pragma unroll
-                for (int c = 0; c < kSmall; ++c) {
-                    const int ebi = e - 16 * c;
-                    const uint32_t eb = (uint32_t)min(max(ebi, 0), 16);
-                    const uint32_t tq = eb >> 2, tr = eb & 3u;
-                    const uint32_t u3 = sad(v[c].w, 0u), u2 = sad(v[c].z, u3), u1 = sad(v[c].y, u2);
-                    uint32_t tw = v[c].x, ts = u1;
-                    tw = tq == 1u ? v[c].y : tw; ts = tq == 1u ? u2 : ts;
-                    tw = tq == 2u ? v[c].z : tw; ts = tq == 2u ? u3 : ts;
-                    tw = tq >= 3u ? v[c].w : tw; ts = tq >= 3u ? 0u : ts;
-                    const uint32_t keep = tr ? 0xFFFFFFFFu >> (32u - 8u * tr) : 0u;
-                    acc -= tq >= 4u ? 0u : sad(tw & ~keep, ts);
-                }
+            for (int k = 0; k < kDense / kWave; ++k) {
+                const uint32_t gi = (uint32_t)(k * kWave + lane);
+                t[k] = gi < ng ? load16(a.data + 16 * (g0 + gi)) : make_uint4(0, 0, 0, 0);
             }
+#pragma unroll
+            for (int k = 0; k < kDense / kWave; ++k)
+                if ((uint32_t)(k * kWave) < ng) st[k * kWave + lane] = t[k];
+            wave_sync();
+            const uint32_t lg = (uint32_t)((off >> 4) - g0);
+            uint4 v[kSmall];
+#pragma unroll
+            for (int c = 0; c < kSmall; ++c)
+                v[c] = (uint32_t)c < nneed ? st[lg + c] : make_uint4(0, 0, 0, 0);
+            const uint8_t* sb = reinterpret_cast<const uint8_t*>(st);
+            if (s0) b0 = sb[off + q - base];
+            if (s1) b1 = sb[off + q + 1 - base];
+            acc = chunk_sum(v[0], v[1], v[2], v[3], 0, sh, e, nneed, __ballot(nneed > 2u) == 0ull);
+        } else if (small) {
+            uint4 v[kSmall];
+#pragma unroll
+            for (int c = 0; c < kSmall; ++c)
+                v[c] = (uint32_t)c < nneed ? load16(fb + 16 * c) : make_uint4(0, 0, 0, 0);
+            acc = chunk_sum(v[0], v[1], v[2], v[3], 0, sh, e, nneed, __ballot(nneed > 2u) == 0ull);
         } else {
             acc = gsum[wv][lane];
         }
@@ -298,8 +373,9 @@ __global__ __launch_bounds__(kBlock) void slice_run_kernel(SliceArgs a) {
 // at once, masks past its ends), and lanes 16, 32 or 64 B apart hit distinct
 // banks (17 l instead of 16 l). Then the skipped word is removed and each run's
 // 64 results go out as one coalesced 2-B store per lane.
-// ND = dwords read per slice (>= ceil((slice_len + 3) / 4)); EXACT: ND equals it
-// (the 20-B and 64-B shapes), which allows the cheaper sum.
+// ND = the most dwords a slice can span (>= (slice_len + 6) / 4, the batch's
+// nde); EXACT: ND equals it (the 20-B and 64-B shapes), so nde is a constant;
+// otherwise reads past nde are skipped by wave-uniform branches.
 constexpr int kStageDwords = 1152;   // padded (4175 + 4 * 17) / 4 * 17 / 16, rounded up
 // PAD: one pad dword per 16 (strides that are multiples of 8 B would put lanes
 // on the same banks); without it the ND reads are one address + immediate offsets
@@ -373,40 +449,43 @@ __global__ __launch_bounds__(kBlock) void slice_strided_kernel(SliceArgs a) {
             if (k < cur.nsl && L) {
                 const int p = pb + (int)(k * s), q = p + (int)L;   // unpadded stage bytes [p, q)
                 const int d0 = p >> 2;
+                // dwords the slice can span at any alignment: ND itself when EXACT,
+                // otherwise the batch's (slice_len + 6) / 4 <= ND (wave-uniform)
+                const int nde = EXACT ? ND : (int)((L + 6u) >> 2);
                 uint32_t x[ND];
 #pragma unroll
-                for (int t = 0; t < ND; ++t) x[t] = st[stage_index<PAD>(d0 + t)];
+                for (int t = 0; t < ND; ++t) x[t] = t < nde ? st[stage_index<PAD>(d0 + t)] : 0u;
                 // every dword read summed whole, then the excess removed: the
                 // bytes before p in dword 0 and the bytes from q on (dword tq,
                 // ND-2 or ND-1, in part; the dwords after it whole). VALU is the
                 // limit of this shape (a wave64 op takes 4 cycles), so no
                 // per-dword masks (round 3: 20-B slices 85 -> see DESIGN §3)
+                // nde dwords summed whole, then the excess removed — the bytes
+                // before p in dword 0 and the 0..6 bytes from q on (dword tq =
+                // nde - 2 or nde - 1 in part and the dword after it; none when q
+                // ends dword nde - 1). VALU is this shape's limit (a wave64 op
+                // takes 4 cycles), so no per-dword masks. The last two dwords
+                // are read again by index when nde is not a constant (a select
+                // over x[] by a runtime index would become a scratch array).
                 uint32_t acc = 0;
+#pragma unroll
+                for (int t = 0; t < ND; ++t) acc = sad(x[t], acc);
+                const uint32_t ph = (uint32_t)p & 3u, qt = (uint32_t)q & 3u;
+                const uint32_t hmask = ph ? 0xFFFFFFFFu >> (32u - 8u * ph) : 0u;   // bytes [4 d0, p)
+                const uint32_t tkeep = qt ? 0xFFFFFFFFu >> (32u - 8u * qt) : 0u;   // bytes [4 (q>>2), q)
+                acc -= sad(x[0] & hmask, 0u);
+                const int tq = (q >> 2) - d0;
+                uint32_t xl, xp;
                 if constexpr (EXACT) {
-                    // ND = (slice_len + 6) / 4 exactly: every dword read summed
-                    // whole, then the excess removed — the bytes before p in
-                    // dword 0 and the 0..6 bytes from q on (dword tq = ND - 2 or
-                    // ND - 1 in part and the dword after it; none when q ends
-                    // dword ND - 1). VALU is this shape's limit (a wave64 op
-                    // takes 4 cycles), so no per-dword masks.
-#pragma unroll
-                    for (int t = 0; t < ND; ++t) acc = sad(x[t], acc);
-                    const uint32_t ph = (uint32_t)p & 3u, qt = (uint32_t)q & 3u;
-                    const uint32_t hmask = ph ? 0xFFFFFFFFu >> (32u - 8u * ph) : 0u;   // bytes [4 d0, p)
-                    const uint32_t tkeep = qt ? 0xFFFFFFFFu >> (32u - 8u * qt) : 0u;   // bytes [4 (q>>2), q)
-                    acc -= sad(x[0] & hmask, 0u);
-                    const int tq = (q >> 2) - d0;
-                    const uint32_t ex1 = sad(x[ND - 1] & ~tkeep, 0u);
-                    uint32_t ex = tq == ND - 1 ? ex1 : 0u;
-                    if constexpr (ND >= 2) ex = tq == ND - 2 ? sad(x[ND - 2] & ~tkeep, sad(x[ND - 1], 0u)) : ex;
-                    acc -= ex;
+                    xl = x[ND - 1];
+                    xp = ND >= 2 ? x[ND >= 2 ? ND - 2 : 0] : 0u;
                 } else {
-#pragma unroll
-                    for (int t = 0; t < ND; ++t) {
-                        const int pos = 4 * (d0 + t);
-                        acc = sad(x[t] & first_bytes(clamp04(q - pos)) & ~first_bytes(clamp04(p - pos)), acc);
-                    }
+                    xl = st[stage_index<PAD>(d0 + nde - 1)];
+                    xp = nde >= 2 ? st[stage_index<PAD>(d0 + nde - 2)] : 0u;
                 }
+                uint32_t ex = tq == nde - 1 ? sad(xl & ~tkeep, 0u) : 0u;
+                ex = tq == nde - 2 ? sad(xp & ~tkeep, sad(xl, 0u)) : ex;
+                acc -= ex;
                 // skipped word: its bytes [2 skip, 2 skip + 2) that lie in the slice (util.rs:166-178)
                 const uint64_t qq = 2ull * a.skipword;
                 if (qq < L) {

@@ -820,3 +820,69 @@ def test_compact_slices_kats_and_random_vs_oracle():
     want = coracle.checksum_slices(big, np.array([0, 1, 4465], np.uint64), np.full(3, 65535, np.uint32),
                                    np.array([0, 3, 32767], np.uint32))
     assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("span", ["0", None])
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_dense_runs_of_packed_slices(seed, span, monkeypatch):
+    """slice_run_kernel's dense-run path: runs of 64 sorted small slices packed
+    in a span of at most 5 KiB arrive as coalesced loads into LDS. Packed
+    slices (0..64 B, gaps 0..k), every alignment, and runs that must fall back
+    to per-lane gathers: one slice out of order, a span just past 5 KiB, lane
+    0 or the last lane empty, a slice past the buffer, a slice ending after
+    the last one's end, a final partial run. Full and compact descriptors,
+    ipv4/ipv6 pseudo-header forms, against the oracle; with every eligible run
+    staged (PNETGPU_SLICE_DENSE_SPAN=0) and with the default span threshold."""
+    if span is not None:
+        monkeypatch.setenv("PNETGPU_SLICE_DENSE_SPAN", span)
+    monkeypatch.setenv("PNETGPU_SLICE_KERNEL", "run")
+    rng = np.random.default_rng(900 + seed)
+    n = 64 * 200 + 23
+    maxgap = (0, 4, 20)[seed]
+    lens = rng.integers(0, 65, n).astype(np.uint32)
+    gaps = rng.integers(0, maxgap + 1, n)
+    offs = (np.cumsum(lens.astype(np.int64) + gaps) - lens - gaps + int(rng.integers(0, 16))).astype(np.uint64)
+    runs = n // 64
+    for r in rng.choice(runs, 40, replace=False):         # break the dense condition in some runs
+        b = 64 * int(r)
+        kind = int(rng.integers(0, 6))
+        if kind == 0:
+            offs[b + 10], offs[b + 30] = offs[b + 30], offs[b + 10]
+        elif kind == 1:
+            lens[b + 63] = 0
+        elif kind == 2:
+            lens[b] = 0
+        elif kind == 3:
+            lens[b + 5] = 64
+            offs[b + 5] = offs[b + 63] + 10
+        elif kind == 4:
+            offs[b + 63] = int(offs[b]) + 5120 - int(lens[b + 63]) + int(rng.integers(-2, 3))
+        else:
+            offs[b + 20] = 1 << 40
+    size = int(max(o + l for o, l in zip(offs, lens) if o < (1 << 40))) + 7
+    buf = rng.integers(0, 256, size, dtype=np.uint8)
+    lens[-1] = 3
+    offs[-1] = size - 3                                    # the very last bytes of the buffer
+    skips = np.where(rng.random(n) < 0.7, rng.integers(0, 34, n), rng.integers(0, 100, n)).astype(np.uint32)
+    bad = offs > size
+    rec_off = np.where(bad, 0, offs)
+    rec_len = np.where(bad, 0, lens).astype(np.uint32)
+    want = coracle.checksum_slices(buf, rec_off, rec_len, skips)
+    d = to_dev(np.concatenate([buf, np.zeros(32, np.uint8)]))[:size]
+    do, dl, ds = to_dev(offs.astype(np.int64)), to_dev(lens.astype(np.int32)), to_dev(skips.astype(np.int32))
+    got = lp.checksum_slices(d, do, dl, ds).cpu().numpy().view(np.uint16)
+    assert np.array_equal(got, want)
+    ok = ~bad
+    desc = lp.slice_descriptors(rec_off[ok], rec_len[ok], skips[ok], device=DEV)
+    got = lp.checksum_slices_compact(d, desc).cpu().numpy().view(np.uint16)
+    assert np.array_equal(got, want[ok])
+    protos = rng.integers(0, 256, n, dtype=np.uint8)
+    for fn, alen, ofn in ((lp.ipv4_checksum_slices, 8, coracle.ipv4_checksum),
+                          (lp.ipv6_checksum_slices, 32, coracle.ipv6_checksum)):
+        a = rng.integers(0, 256, (n, alen), dtype=np.uint8)
+        got = fn(d, do, dl, ds, to_dev(a), to_dev(protos)).cpu().numpy().view(np.uint16)
+        h = alen // 2
+        for i in list(range(0, n, 37)) + list(np.nonzero(bad)[0]):
+            o, ln = int(rec_off[i]), int(rec_len[i])
+            assert got[i] == ofn(bytes(buf[o:o + ln]), int(skips[i]), b"", bytes(a[i, :h]), bytes(a[i, h:]),
+                                 int(protos[i])), (alen, i)

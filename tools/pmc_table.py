@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""Mean per-dispatch counter values of the rx kernels from pmc_probe.sh output dirs."""
+"""Mean per-dispatch counter values of the rx kernels (or the kernels whose name
+contains argv[2]) from pmc_probe.sh / slice_pmc.sh output dirs."""
 import collections
 import csv
 import glob
@@ -7,6 +8,7 @@ import os
 import sys
 
 root = sys.argv[1]
+name = sys.argv[2] if len(sys.argv) > 2 else "rx_"
 rows = collections.defaultdict(dict)
 for d in sorted(glob.glob(os.path.join(root, "k*_*"))):
     if not os.path.isdir(d):
@@ -15,7 +17,7 @@ for d in sorted(glob.glob(os.path.join(root, "k*_*"))):
     acc = collections.defaultdict(list)
     for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
         for r in csv.DictReader(open(f)):
-            if "rx_" in r["Kernel_Name"]:
+            if name in r["Kernel_Name"]:
                 acc[(r["Counter_Name"], r["Dispatch_Id"])].append(float(r["Counter_Value"]))
     per = collections.defaultdict(list)
     for (c, _), v in acc.items():

@@ -27,10 +27,16 @@ def timeit(fn, steps=20):
     return a.elapsed_time(b) / steps
 
 
-for size, n in ((20, 1 << 24), (64, 1 << 23), (1024, 1 << 20)):
-    for bpc in os.environ.get("PROBE_BPC", "0").split(","):
+# PROBE_SIZES: slice sizes (n = 2^29 / size); PROBE_BPC: grid sweep;
+# PROBE_DENSE: PNETGPU_SLICE_DENSE_SPAN sweep (descriptor forms)
+sizes = [int(x) for x in os.environ.get("PROBE_SIZES", "20,64,1024").split(",")]
+for size, n in ((z, 1 << 24 if z <= 32 else (1 << 29) // z) for z in sizes):
+    for bpc, dspan in ((b, ds) for b in os.environ.get("PROBE_BPC", "0").split(",")
+                       for ds in os.environ.get("PROBE_DENSE", "").split(",")):
         os.environ["PNETGPU_SLICE_BLOCKS_PER_CU"] = bpc
-        print(f"blocks/CU {bpc} (0 = occupancy)")
+        if dspan:
+            os.environ["PNETGPU_SLICE_DENSE_SPAN"] = dspan
+        print(f"blocks/CU {bpc} (0 = occupancy) dense span {dspan or 'default'}")
         d = torch.full((n * size + 32,), 99, dtype=torch.uint8, device=dev)
         offs = torch.arange(n, dtype=torch.int64, device=dev) * size
         lens = torch.full((n,), size, dtype=torch.int32, device=dev)
