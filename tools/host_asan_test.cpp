@@ -136,6 +136,9 @@ static void test_abi_validation() {
     uint8_t data[16] = {};
     CHECK(pnetgpu_checksum_slices(nullptr, data, 16, 4, off, len, skip, out, nullptr) == PNETGPU_EINVAL);
     CHECK(pnetgpu_checksum_slices_strided(nullptr, data, 16, 4, 0, 4, 4, 0, out, nullptr) == PNETGPU_EINVAL);
+    pnetgpu_slice_desc cd[4] = {{0, 1, 0}, {1, 1, 0}, {2, 1, 0}, {3, 1, 0}};
+    CHECK(pnetgpu_checksum_slices_compact(nullptr, data, 16, 4, cd, out, nullptr) == PNETGPU_EINVAL);
+    CHECK(pnetgpu_checksum_slices_compact(nullptr, data, 16, 0, cd, out, nullptr) == PNETGPU_EINVAL);
     CHECK(pnetgpu_last_rx_kernel() != nullptr && std::strlen(pnetgpu_last_rx_kernel()) == 0);   // no launch yet
     CHECK(pnetgpu_last_hip_error() == 0);
     CHECK(pnetgpu_ipv4_checksum_adv_slices(nullptr, data, 16, 4, off, len, skip, off, len, data, data, out,
