@@ -260,16 +260,18 @@ static int slices_common(pnetgpu_ctx* ctx, const uint8_t* data, uint64_t data_by
     // Kernel choice. The slice lengths are device-resident, so the host decides
     // by the BUFFER bytes per slice (data_bytes / n), which equals the bytes per
     // slice only for slices that tile the buffer: slice_run_kernel (one wave per
-    // 64 slices, a slice of at most 4 granules summed by its own lane; 9.4x on
-    // the reference's 20-B bench shape, same box) when the buffer averages
-    // <= 256 B per slice; slice_kernel (one 16-lane group per slice, grid-stride;
-    // 16 % faster on 1-KiB slices) otherwise and for every *_adv batch. Short
+    // 64 slices, a slice of at most 4 granules summed by its own lane, longer
+    // ones by 2/4/8/16-lane groups of their size class; 9.4x on the reference's
+    // 20-B bench shape, 384-B slices 0.64 vs 0.39 of 8 TB/s) when the buffer
+    // averages <= 512 B per slice (even at 768 B); slice_kernel (one 16-lane group
+    // per slice, grid-stride; 7 % faster on 1-KiB slices) otherwise and for
+    // every *_adv batch. Short
     // slices spread through a large buffer (e.g. headers of MTU frames) thus
     // take slice_kernel; callers that know their slice sizes set
     // PNETGPU_SLICE_KERNEL=run|group, and uniform slices have
     // pnetgpu_checksum_slices_strided, which decides by the slice length itself.
     const char* kenv = std::getenv("PNETGPU_SLICE_KERNEL");
-    bool run = !extra_offsets && data_bytes / n <= 256;
+    bool run = !extra_offsets && data_bytes / n <= 512;
     if (kenv && !extra_offsets) run = kenv[0] == 'r' ? true : kenv[0] == 'g' ? false : run;
     const uint64_t per_block = run ? kBlock : kBlock / 16;
     const int blocks = slice_grid(ctx, run ? 1 : 2, pseudo, extra_offsets != nullptr, (n + per_block - 1) / per_block);
@@ -306,7 +308,7 @@ int pnetgpu_checksum_slices_strided(pnetgpu_ctx* ctx, const uint8_t* data, uint6
     // otherwise the descriptor kernels with computed offsets (the same choice
     // as pnetgpu_checksum_slices, by the slice length the caller gave)
     const bool small = stride <= 64 && slice_len <= 64;
-    const bool run = !small && slice_len <= 256;
+    const bool run = !small && slice_len <= 512;
     const uint64_t per_block = small || run ? kBlock : kBlock / 16;
     const int blocks = slice_grid(ctx, small ? 0 : run ? 1 : 2, small ? pnetgpu::strided_variant(slice_len, stride) : 0, false,
                                   (n + per_block - 1) / per_block);
@@ -333,7 +335,7 @@ int pnetgpu_checksum_slices_compact(pnetgpu_ctx* ctx, const uint8_t* data, uint6
     a.dense_min = dense_span();
     // the same choice as pnetgpu_checksum_slices (by the buffer bytes per slice)
     const char* kenv = std::getenv("PNETGPU_SLICE_KERNEL");
-    bool run = data_bytes / n <= 256;
+    bool run = data_bytes / n <= 512;
     if (kenv) run = kenv[0] == 'r' ? true : kenv[0] == 'g' ? false : run;
     const uint64_t per_block = run ? kBlock : kBlock / 16;
     const int blocks = slice_grid(ctx, run ? 1 : 2, 0, false, (n + per_block - 1) / per_block);

@@ -210,8 +210,8 @@ __device__ __forceinline__ void listed_sums(uint64_t mask, int lane, uint8_t* li
 // l: coalesced descriptor loads, a slice of at most kSmall granules summed by
 // its own lane (all its loads issued at once, with the two skipped-word
 // bytes), runs of small sorted slices staged through LDS instead (dense runs,
-// below), longer slices listed and summed by 2-, 4- or 16-lane groups (the
-// last as in slice_kernel), and one coalesced 2-B store per lane.
+// below), longer slices listed and summed by 2-, 4-, 8- or 16-lane groups
+// (the last as in slice_kernel), and one coalesced 2-B store per lane.
 // slice_kernel gave 16 lanes to every slice: a 20-B slice left 14 of them idle
 // and the results went out as 2-B stores scattered 32 B apart.
 #ifndef PNET_RUN_MINWAVES
@@ -220,7 +220,6 @@ __device__ __forceinline__ void listed_sums(uint64_t mask, int lane, uint8_t* li
 template <int PSEUDO>
 __global__ __launch_bounds__(kBlock, PNET_RUN_MINWAVES) void slice_run_kernel(SliceArgs a) {
     constexpr int kSmall = 4;    // granules summed by the slice's own lane (<= 49 B at any alignment)
-    constexpr int kMedium = 16;  // granules of a medium slice, one load round of its group (<= 241 B)
     constexpr int kDense = 5 * kWave;   // granules a dense run may span (5 KiB)
     __shared__ uint4 dstage[kWavesPerBlock][kDense];
     __shared__ uint32_t gsum[kWavesPerBlock][kWave];
@@ -283,18 +282,20 @@ __global__ __launch_bounds__(kBlock, PNET_RUN_MINWAVES) void slice_run_kernel(Sl
         }
         // slices past kSmall granules: listed by size class and summed by groups
         // of G lanes, 4 granules per lane (2 lanes up to 8 granules, 4 up to
-        // kMedium; one load round, 32 or 16 slices per pass) and 16-lane groups
-        // for longer ones. Narrow groups: the VALU of a pass is spent on the
+        // 16, 8 up to 32; one load round, 32, 16 or 8 slices per pass) and
+        // 16-lane groups for longer ones. Narrow groups: the VALU of a pass is spent on the
         // slices of that pass (80-B slices: 2 lanes 150 us, 4: 172, 8: 205,
         // 16: 335; profiles/r03/slices); a slice-own gather at a 128-B stride
         // was 177-200 us. Before the small slices' loads: no granule registers
         // held across them.
         const bool med8 = in && !small && nneed <= 8u;
-        const bool med16 = in && !small && !med8 && nneed <= (uint32_t)kMedium;
-        const uint64_t m8 = __ballot(med8), m16 = __ballot(med16);
-        const uint64_t lmask = __ballot(in && !small && !med8 && !med16);
+        const bool med16 = in && !small && !med8 && nneed <= 16u;
+        const bool med32 = in && !small && !med8 && !med16 && nneed <= 32u;
+        const uint64_t m8 = __ballot(med8), m16 = __ballot(med16), m32 = __ballot(med32);
+        const uint64_t lmask = __ballot(in && !small && !med8 && !med16 && !med32);
         if (m8) listed_sums<2, 4>(m8, lane, glist[wv], gsum[wv], a.data, off, len);
         if (m16) listed_sums<4, 4>(m16, lane, glist[wv], gsum[wv], a.data, off, len);
+        if (m32) listed_sums<8, 4>(m32, lane, glist[wv], gsum[wv], a.data, off, len);
         if (lmask) listed_sums<16, PNET_SLICE_U>(lmask, lane, glist[wv], gsum[wv], a.data, off, len);
         uint32_t acc = 0;
         if (dense) {                             // wave-uniform
