@@ -264,15 +264,15 @@ static int slices_common(pnetgpu_ctx* ctx, const uint8_t* data, uint64_t data_by
     // ones by 2/4/8/16-lane groups of their size class; 9.4x on the reference's
     // 20-B bench shape, 384-B slices 0.64 vs 0.39 of 8 TB/s) when the buffer
     // averages <= 512 B per slice (even at 768 B); slice_kernel (one 16-lane group
-    // per slice, grid-stride; 7 % faster on 1-KiB slices) otherwise and for
-    // every *_adv batch. Short
+    // per slice, grid-stride; 7 % faster on 1-KiB slices) otherwise; *_adv
+    // batches the same way (their extra slices summed as a second range). Short
     // slices spread through a large buffer (e.g. headers of MTU frames) thus
     // take slice_kernel; callers that know their slice sizes set
     // PNETGPU_SLICE_KERNEL=run|group, and uniform slices have
     // pnetgpu_checksum_slices_strided, which decides by the slice length itself.
     const char* kenv = std::getenv("PNETGPU_SLICE_KERNEL");
-    bool run = !extra_offsets && data_bytes / n <= 512;
-    if (kenv && !extra_offsets) run = kenv[0] == 'r' ? true : kenv[0] == 'g' ? false : run;
+    bool run = data_bytes / n <= 512;
+    if (kenv) run = kenv[0] == 'r' ? true : kenv[0] == 'g' ? false : run;
     const uint64_t per_block = run ? kBlock : kBlock / 16;
     const int blocks = slice_grid(ctx, run ? 1 : 2, pseudo, extra_offsets != nullptr, (n + per_block - 1) / per_block);
     if (const int e = pnetgpu::launch_slices(a, pseudo, run, blocks, static_cast<hipStream_t>(stream))) {

@@ -227,9 +227,11 @@ static const void* strided_pick(int v) {
 int slice_blocks_per_cu(int which, int pseudo, bool extra) {
     // which 0 (strided): pseudo holds strided_variant() of the instantiation
     const void* fn = which == 0 ? strided_pick(pseudo)
-                   : which == 1 ? (pseudo == 0 ? reinterpret_cast<const void*>(slice_run_kernel<0>)
-                                  : pseudo == 4 ? reinterpret_cast<const void*>(slice_run_kernel<4>)
-                                                : reinterpret_cast<const void*>(slice_run_kernel<16>))
+                   : which == 1 ? (pseudo == 0 ? reinterpret_cast<const void*>(slice_run_kernel<0, false>)
+                                  : pseudo == 4 ? (extra ? reinterpret_cast<const void*>(slice_run_kernel<4, true>)
+                                                         : reinterpret_cast<const void*>(slice_run_kernel<4, false>))
+                                                : (extra ? reinterpret_cast<const void*>(slice_run_kernel<16, true>)
+                                                         : reinterpret_cast<const void*>(slice_run_kernel<16, false>)))
                    : (pseudo == 0 ? reinterpret_cast<const void*>(slice_kernel<0, false>)
                       : pseudo == 4 ? (extra ? reinterpret_cast<const void*>(slice_kernel<4, true>)
                                              : reinterpret_cast<const void*>(slice_kernel<4, false>))
@@ -260,12 +262,15 @@ int launch_slices_strided_small(const SliceArgs& args, int blocks, hipStream_t s
 int launch_slices(const SliceArgs& args, int pseudo, bool run, int blocks, hipStream_t stream) {
     const bool extra = args.extra_offsets != nullptr;
     (void)hipGetLastError();
-    if (run && !extra) {
-        if (pseudo == 0) hipLaunchKernelGGL((slice_run_kernel<0>), dim3(blocks), dim3(kBlock), 0, stream, args);
-        else if (pseudo == 4) hipLaunchKernelGGL((slice_run_kernel<4>), dim3(blocks), dim3(kBlock), 0, stream, args);
-        else hipLaunchKernelGGL((slice_run_kernel<16>), dim3(blocks), dim3(kBlock), 0, stream, args);
+    if (pseudo == 0 && extra) return -1;   // util::checksum has no extra slice
+#define PNET_RUN(P, X) hipLaunchKernelGGL((slice_run_kernel<P, X>), dim3(blocks), dim3(kBlock), 0, stream, args)
+    if (run) {
+        if (pseudo == 0) PNET_RUN(0, false);
+        else if (pseudo == 4 && !extra) PNET_RUN(4, false);
+        else if (pseudo == 4) PNET_RUN(4, true);
+        else if (!extra) PNET_RUN(16, false);
+        else PNET_RUN(16, true);
     } else if (pseudo == 0) {
-        if (extra) return -1;   // util::checksum has no extra slice
         hipLaunchKernelGGL((slice_kernel<0, false>), dim3(blocks), dim3(kBlock), 0, stream, args);
     } else if (pseudo == 4 && !extra) {
         hipLaunchKernelGGL((slice_kernel<4, false>), dim3(blocks), dim3(kBlock), 0, stream, args);
@@ -276,6 +281,7 @@ int launch_slices(const SliceArgs& args, int pseudo, bool run, int blocks, hipSt
     } else {
         hipLaunchKernelGGL((slice_kernel<16, true>), dim3(blocks), dim3(kBlock), 0, stream, args);
     }
+#undef PNET_RUN
     return (int)hipGetLastError();
 }
 

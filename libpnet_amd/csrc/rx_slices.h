@@ -203,8 +203,102 @@ __device__ __forceinline__ void listed_sums(uint64_t mask, int lane, uint8_t* li
     wave_sync();
 }
 
-// slice_run_kernel: the same results without the extra slice (util::checksum,
-// ipv4_checksum, ipv6_checksum), for batches of any slice sizes but built for
+constexpr int kRunSmall = 4;          // granules summed by the slice's own lane (<= 49 B at any alignment)
+constexpr int kRunDense = 5 * kWave;   // granules a dense run may span (5 KiB)
+
+// slice_run_kernel's weighted byte sum of lane's range [off, off + len) of
+// run `run` (off already offset by a.delta and bounds-checked; len 0 for an
+// empty or invalid one) without the skipped word's bytes (skip: word index, or
+// ~0 for none), with the wave's LDS stage, list and sums. Ends with the LDS
+// it used free for the next call.
+__device__ __forceinline__ uint32_t run_range_sum(const SliceArgs& a, uint64_t run, int lane, bool in, uint64_t off,
+                                                  uint32_t len, uint32_t skip, uint4* stage, uint32_t* gsum,
+                                                  uint8_t* list) {
+    constexpr int kSmall = kRunSmall, kDense = kRunDense;
+    const int sh = (int)(off & 15);
+    const uint8_t* fb = a.data + (off - (uint64_t)sh);
+    const int e = sh + (int)len;
+    const uint32_t nneed = len ? (uint32_t)((e + 15) >> 4) : 0u;
+    const bool small = nneed <= (uint32_t)kSmall;
+    // skipped word: its bytes [2 skip, 2 skip + 2) that lie in the slice (util.rs:166-178)
+    const uint64_t q = 2ull * skip;
+    const bool s0 = q < len, s1 = q + 1 < len;
+    // dense run: every slice small and inside [lane 0's granule, the last
+    // lane's end) with that span at most kDense granules and at least
+    // a.dense_min bytes (sorted, packed slices: header fields, back-to-back
+    // records). The span then arrives as coalesced 1-KiB wave loads into an
+    // LDS stage and each lane reads its granules there, instead of 3 granule
+    // + 2 byte gathers per lane at the slice stride (the strided kernel's
+    // staging, for descriptors).
+    const int last = (int)min<uint64_t>((uint64_t)kWave - 1, a.n - 1 - run * kWave);
+    const uint64_t base = (uint64_t)__shfl((unsigned long long)off, 0) & ~15ull;
+    const uint64_t top = (uint64_t)__shfl((unsigned long long)(off + len), last);
+    const bool fits = !in || !len || (small && off >= base && off + len <= top);
+    const bool dense = __ballot(!fits) == 0ull && top > base && top - base <= 16ull * kDense &&
+                       top - base >= a.dense_min;
+    uint32_t b0 = 0, b1 = 0;                 // in flight across the group phase
+    if (!dense) {
+        if (s0) b0 = a.data[off + q];
+        if (s1) b1 = a.data[off + q + 1];
+    }
+    // slices past kSmall granules: listed by size class and summed by groups
+    // of G lanes, 4 granules per lane (2 lanes up to 8 granules, 4 up to
+    // 16, 8 up to 32; one load round, 32, 16 or 8 slices per pass) and
+    // 16-lane groups for longer ones. Narrow groups: the VALU of a pass is
+    // spent on the slices of that pass (80-B slices: 2 lanes 150 us, 4: 172, 8: 205,
+    // 16: 335; profiles/r03/slices); a slice-own gather at a 128-B stride
+    // was 177-200 us. Before the small slices' loads: no granule registers
+    // held across them.
+    const bool med8 = in && !small && nneed <= 8u;
+    const bool med16 = in && !small && !med8 && nneed <= 16u;
+    const bool med32 = in && !small && !med8 && !med16 && nneed <= 32u;
+    const uint64_t m8 = __ballot(med8), m16 = __ballot(med16), m32 = __ballot(med32);
+    const uint64_t lmask = __ballot(in && !small && !med8 && !med16 && !med32);
+    if (m8) listed_sums<2, 4>(m8, lane, list, gsum, a.data, off, len);
+    if (m16) listed_sums<4, 4>(m16, lane, list, gsum, a.data, off, len);
+    if (m32) listed_sums<8, 4>(m32, lane, list, gsum, a.data, off, len);
+    if (lmask) listed_sums<16, PNET_SLICE_U>(lmask, lane, list, gsum, a.data, off, len);
+    uint32_t acc = 0;
+    if (dense) {                             // wave-uniform
+        uint4* st = stage;
+        const uint64_t g0 = base >> 4;
+        const uint32_t ng = (uint32_t)(((top + 15) >> 4) - g0);
+        uint4 t[kDense / kWave];
+#pragma unroll
+        for (int k = 0; k < kDense / kWave; ++k) {
+            const uint32_t gi = (uint32_t)(k * kWave + lane);
+            t[k] = gi < ng ? load16(a.data + 16 * (g0 + gi)) : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int k = 0; k < kDense / kWave; ++k)
+            if ((uint32_t)(k * kWave) < ng) st[k * kWave + lane] = t[k];
+        wave_sync();
+        const uint32_t lg = (uint32_t)((off >> 4) - g0);
+        uint4 v[kSmall];
+#pragma unroll
+        for (int c = 0; c < kSmall; ++c)
+            v[c] = (uint32_t)c < nneed ? st[lg + c] : make_uint4(0, 0, 0, 0);
+        const uint8_t* sb = reinterpret_cast<const uint8_t*>(st);
+        if (s0) b0 = sb[off + q - base];
+        if (s1) b1 = sb[off + q + 1 - base];
+        acc = chunk_sum(v[0], v[1], v[2], v[3], 0, sh, e, nneed, __ballot(nneed > 2u) == 0ull);
+    } else if (small) {
+        uint4 v[kSmall];
+#pragma unroll
+        for (int c = 0; c < kSmall; ++c)
+            v[c] = (uint32_t)c < nneed ? load16(fb + 16 * c) : make_uint4(0, 0, 0, 0);
+        acc = chunk_sum(v[0], v[1], v[2], v[3], 0, sh, e, nneed, __ballot(nneed > 2u) == 0ull);
+    } else {
+        acc = gsum[lane];
+    }
+    acc -= s0 ? (((off + q) & 1) ? (b0 << 8) : b0) : 0u;
+    acc -= s1 ? (((off + q + 1) & 1) ? (b1 << 8) : b1) : 0u;
+    wave_sync();   // list / gsum / stage are rewritten by the next call
+    return acc;
+}
+
+// slice_run_kernel: the same results (util::checksum, ipv4_checksum,
+// ipv6_checksum, *_adv), for batches of any slice sizes but built for
 // small ones (the reference's own bench shape is a 20-B slice,
 // checksum_benchmarks.rs:8-12). One wave per run of 64 slices, lane l <-> slice
 // l: coalesced descriptor loads, a slice of at most kSmall granules summed by
@@ -217,11 +311,13 @@ __device__ __forceinline__ void listed_sums(uint64_t mask, int lane, uint8_t* li
 #ifndef PNET_RUN_MINWAVES
 #define PNET_RUN_MINWAVES 1   // A/B: waves per SIMD the register allocation must allow
 #endif
-template <int PSEUDO>
+// EXTRA: the *_checksum_adv form (util.rs:109-114): the extra slice summed
+// by the same machinery as a second range (whole words only, its own word
+// alignment), where slice_kernel gave 16 lanes to every slice (80-B slices
+// 10 % of 8 TB/s).
+template <int PSEUDO, bool EXTRA>
 __global__ __launch_bounds__(kBlock, PNET_RUN_MINWAVES) void slice_run_kernel(SliceArgs a) {
-    constexpr int kSmall = 4;    // granules summed by the slice's own lane (<= 49 B at any alignment)
-    constexpr int kDense = 5 * kWave;   // granules a dense run may span (5 KiB)
-    __shared__ uint4 dstage[kWavesPerBlock][kDense];
+    __shared__ uint4 dstage[kWavesPerBlock][kRunDense];
     __shared__ uint32_t gsum[kWavesPerBlock][kWave];
     __shared__ uint8_t glist[kWavesPerBlock][kWave];
     const int lane = threadIdx.x & (kWave - 1);
@@ -254,86 +350,28 @@ __global__ __launch_bounds__(kBlock, PNET_RUN_MINWAVES) void slice_run_kernel(Sl
                 off = 0;
             }
         }
-        const int sh = (int)(off & 15);
-        const uint8_t* fb = a.data + (off - (uint64_t)sh);
-        const int e = sh + (int)len;
-        const uint32_t nneed = len ? (uint32_t)((e + 15) >> 4) : 0u;
-        const bool small = nneed <= (uint32_t)kSmall;
-        // skipped word: its bytes [2 skip, 2 skip + 2) that lie in the slice (util.rs:166-178)
-        const uint64_t q = 2ull * skip;
-        const bool s0 = q < len, s1 = q + 1 < len;
-        // dense run: every slice small and inside [lane 0's granule, the last
-        // lane's end) with that span at most kDense granules and at least
-        // a.dense_min bytes (sorted, packed slices: header fields, back-to-back
-        // records). The span then arrives as
-        // coalesced 1-KiB wave loads into an LDS stage and each lane reads its
-        // granules there, instead of 3 granule + 2 byte gathers per lane at the
-        // slice stride (the strided kernel's staging, for descriptors).
-        const int last = (int)min<uint64_t>((uint64_t)kWave - 1, a.n - 1 - run * kWave);
-        const uint64_t base = (uint64_t)__shfl((unsigned long long)off, 0) & ~15ull;
-        const uint64_t top = (uint64_t)__shfl((unsigned long long)(off + len), last);
-        const bool fits = !in || !len || (small && off >= base && off + len <= top);
-        const bool dense = __ballot(!fits) == 0ull && top > base && top - base <= 16ull * kDense &&
-                           top - base >= a.dense_min;
-        uint32_t b0 = 0, b1 = 0;                 // in flight across the group phase
-        if (!dense) {
-            if (s0) b0 = a.data[off + q];
-            if (s1) b1 = a.data[off + q + 1];
-        }
-        // slices past kSmall granules: listed by size class and summed by groups
-        // of G lanes, 4 granules per lane (2 lanes up to 8 granules, 4 up to
-        // 16, 8 up to 32; one load round, 32, 16 or 8 slices per pass) and
-        // 16-lane groups for longer ones. Narrow groups: the VALU of a pass is spent on the
-        // slices of that pass (80-B slices: 2 lanes 150 us, 4: 172, 8: 205,
-        // 16: 335; profiles/r03/slices); a slice-own gather at a 128-B stride
-        // was 177-200 us. Before the small slices' loads: no granule registers
-        // held across them.
-        const bool med8 = in && !small && nneed <= 8u;
-        const bool med16 = in && !small && !med8 && nneed <= 16u;
-        const bool med32 = in && !small && !med8 && !med16 && nneed <= 32u;
-        const uint64_t m8 = __ballot(med8), m16 = __ballot(med16), m32 = __ballot(med32);
-        const uint64_t lmask = __ballot(in && !small && !med8 && !med16 && !med32);
-        if (m8) listed_sums<2, 4>(m8, lane, glist[wv], gsum[wv], a.data, off, len);
-        if (m16) listed_sums<4, 4>(m16, lane, glist[wv], gsum[wv], a.data, off, len);
-        if (m32) listed_sums<8, 4>(m32, lane, glist[wv], gsum[wv], a.data, off, len);
-        if (lmask) listed_sums<16, PNET_SLICE_U>(lmask, lane, glist[wv], gsum[wv], a.data, off, len);
-        uint32_t acc = 0;
-        if (dense) {                             // wave-uniform
-            uint4* st = dstage[wv];
-            const uint64_t g0 = base >> 4;
-            const uint32_t ng = (uint32_t)(((top + 15) >> 4) - g0);
-            uint4 t[kDense / kWave];
-#pragma unroll
-            for (int k = 0; k < kDense / kWave; ++k) {
-                const uint32_t gi = (uint32_t)(k * kWave + lane);
-                t[k] = gi < ng ? load16(a.data + 16 * (g0 + gi)) : make_uint4(0, 0, 0, 0);
-            }
-#pragma unroll
-            for (int k = 0; k < kDense / kWave; ++k)
-                if ((uint32_t)(k * kWave) < ng) st[k * kWave + lane] = t[k];
-            wave_sync();
-            const uint32_t lg = (uint32_t)((off >> 4) - g0);
-            uint4 v[kSmall];
-#pragma unroll
-            for (int c = 0; c < kSmall; ++c)
-                v[c] = (uint32_t)c < nneed ? st[lg + c] : make_uint4(0, 0, 0, 0);
-            const uint8_t* sb = reinterpret_cast<const uint8_t*>(st);
-            if (s0) b0 = sb[off + q - base];
-            if (s1) b1 = sb[off + q + 1 - base];
-            acc = chunk_sum(v[0], v[1], v[2], v[3], 0, sh, e, nneed, __ballot(nneed > 2u) == 0ull);
-        } else if (small) {
-            uint4 v[kSmall];
-#pragma unroll
-            for (int c = 0; c < kSmall; ++c)
-                v[c] = (uint32_t)c < nneed ? load16(fb + 16 * c) : make_uint4(0, 0, 0, 0);
-            acc = chunk_sum(v[0], v[1], v[2], v[3], 0, sh, e, nneed, __ballot(nneed > 2u) == 0ull);
-        } else {
-            acc = gsum[wv][lane];
-        }
-        acc -= s0 ? (((off + q) & 1) ? (b0 << 8) : b0) : 0u;
-        acc -= s1 ? (((off + q + 1) & 1) ? (b1 << 8) : b1) : 0u;
+        const uint32_t acc = run_range_sum(a, run, lane, in, off, len, skip, dstage[wv], gsum[wv], glist[wv]);
         uint32_t p = fold16(acc);
         if (!(off & 1)) p = bswap16(p);
+        uint32_t pe = 0, elen = 0;
+        if (EXTRA) {
+            // sum_be_words(extra, extra.len() / 2): every whole word, never the
+            // odd trailing byte (util.rs:114; the quirk documented at
+            // udp.rs:42-44); the extra slice starts its own word alignment
+            uint64_t eoff = 0;
+            if (in) {
+                eoff = a.extra_offsets[i] + a.delta;
+                elen = a.extra_lengths[i];
+                if (eoff > a.limit || (uint64_t)elen > a.limit - eoff) {
+                    elen = 0;
+                    eoff = 0;
+                }
+            }
+            const uint32_t te = run_range_sum(a, run, lane, in, eoff, elen & ~1u, 0xFFFFFFFFu, dstage[wv], gsum[wv],
+                                              glist[wv]);
+            pe = fold16(te);
+            if (!(eoff & 1)) pe = bswap16(pe);
+        }
         uint32_t r;
         if (PSEUDO == 0) {
             r = len ? ((~p) & 0xFFFFu) : 0u;                    // util.rs:77-79
@@ -353,11 +391,10 @@ __global__ __launch_bounds__(kBlock, PNET_RUN_MINWAVES) void slice_run_kernel(Sl
                 }
                 s += a.protos[i];
             }
-            s += len + p;                                        // util.rs:103-113
+            s += len + elen + p + pe;                            // util.rs:103-114
             r = (~fold16(s)) & 0xFFFFu;
         }
         if (in) a.out[i] = (uint16_t)r;
-        wave_sync();   // glist / gsum are rewritten by the next run
     }
 }
 

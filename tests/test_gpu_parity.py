@@ -488,16 +488,21 @@ def test_small_and_large_slices_mixed_in_runs(seed, kernel, monkeypatch):
                                      int(protos[i])), (alen, shift, i)
 
 
-def test_random_adv_slices_vs_oracle():
+@pytest.mark.parametrize("kernel", ["run", "group"])
+@pytest.mark.parametrize("short", [False, True])
+def test_random_adv_slices_vs_oracle(kernel, short, monkeypatch):
     """*_checksum_adv (extra_data) batched: main and extra slices at every byte
-    alignment, odd/even/empty extras, extras longer than one 16-lane pass."""
-    rng = np.random.default_rng(23)
+    alignment, odd/even/empty extras, extras longer than one 16-lane pass; short
+    main and extra slices (0-100 B: own-lane, 2- and 4-lane classes of
+    slice_run_kernel, its extra range a second pass), both slice kernels."""
+    monkeypatch.setenv("PNETGPU_SLICE_KERNEL", kernel)
+    rng = np.random.default_rng(23 + short)
     n = 6000
     buf = rng.integers(0, 256, 1 << 21, dtype=np.uint8)
-    lens = rng.integers(0, 1600, n).astype(np.uint32)
+    lens = rng.integers(0, 101 if short else 1600, n).astype(np.uint32)
     offs = rng.integers(0, buf.size - 1700, n).astype(np.uint64)
-    skips = rng.integers(0, 900, n).astype(np.uint32)
-    elens = rng.integers(0, 600, n).astype(np.uint32)
+    skips = rng.integers(0, 60 if short else 900, n).astype(np.uint32)
+    elens = rng.integers(0, 101 if short else 600, n).astype(np.uint32)
     elens[::5] = rng.integers(0, 4, elens[::5].size)
     elens[1::5] = 0
     eoffs = rng.integers(0, buf.size - 700, n).astype(np.uint64)
@@ -517,10 +522,12 @@ def test_random_adv_slices_vs_oracle():
             assert got[i] == want, (version, i, ln, el, o % 16, eo % 16)
 
 
-def test_adv_slices_match_tcp_with_options_split():
+@pytest.mark.parametrize("kernel", ["run", "group"])
+def test_adv_slices_match_tcp_with_options_split(kernel, monkeypatch):
     """A TCP segment checksummed whole equals the same segment split into a
     header slice + an even-length extra (the way tcp::ipv4_checksum_adv is used
     to checksum a header and a separately held payload)."""
+    monkeypatch.setenv("PNETGPU_SLICE_KERNEL", kernel)
     rng = np.random.default_rng(5)
     seg = rng.integers(0, 256, 1000, dtype=np.uint8)
     buf = np.concatenate([np.zeros(3, np.uint8), seg, np.zeros(64, np.uint8)])

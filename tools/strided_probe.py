@@ -50,3 +50,14 @@ for size, n in ((z, 1 << 24 if z <= 32 else (1 << 29) // z) for z in sizes):
             print(f"{size:5d}-B x {n}: strided {t_st*1e3:7.1f} us ({n*(size+2)/(t_st*1e-3)/8e12:.1%} of 8 TB/s)  "
                   f"descriptors {t_de*1e3:7.1f} us ({n*(size+18)/(t_de*1e-3)/8e12:.1%})  "
                   f"compact {t_co*1e3:7.1f} us ({n*(size+10)/(t_co*1e-3)/8e12:.1%})", flush=True)
+        if os.environ.get("PROBE_ADV"):
+            # ipv4_checksum_adv: each slice split into a main half and an extra half
+            # (bytes: slice + 2 x 16-B descriptors + 8 addresses + 1 proto + 2 result)
+            h = size // 2
+            hl = torch.full((n,), h, dtype=torch.int32, device=dev)
+            el = torch.full((n,), size - h, dtype=torch.int32, device=dev)
+            ad = torch.zeros((n, 8), dtype=torch.uint8, device=dev)
+            pr = torch.full((n,), 17, dtype=torch.uint8, device=dev)
+            t_adv = timeit(lambda: lp.checksum_adv_slices(4, d, offs, hl, sk, offs + h, el, ad, pr, stream=s))
+            print(f"{size:5d}-B x {n}: ipv4_checksum_adv halves {t_adv*1e3:7.1f} us "
+                  f"({n*(size+2*16+8+1+2)/(t_adv*1e-3)/8e12:.1%})", flush=True)
