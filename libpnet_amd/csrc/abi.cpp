@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <cstdint>
@@ -23,6 +24,10 @@ struct pnetgpu_ctx {
     int per_cu[8][2] = {};
     // of each slice kernel: [strided, run, group] x pseudo {0, 4, 16} x extra
     int slice_per_cu[3][8][2] = {};
+    // run-claim counters of the receive launches (RxArgs::sched): one 128-B
+    // line per slot, slots used round robin by launch epoch
+    unsigned long long* d_sched = nullptr;
+    std::atomic<uint32_t> epoch{0};
 };
 
 namespace pnetgpu {
@@ -55,6 +60,19 @@ int slice_grid(pnetgpu_ctx* ctx, int which, int pseudo, bool extra, uint64_t wan
     return (int)std::max<uint64_t>(1, std::min<uint64_t>(want, cap));
 }
 constexpr int kRunFrames = 64;      // frames per wave-run
+// run-claim counter slots per context: a launch uses slot epoch % kSchedSlots,
+// so up to kSchedSlots receive launches of one context may be in flight at once
+constexpr uint32_t kSchedSlots = 64;
+constexpr uint32_t kMaxCtrs = 128;                                   // counters per slot
+constexpr size_t kCtrStride = 256 / sizeof(unsigned long long);      // 256 B apart
+constexpr size_t kSchedStride = kMaxCtrs * kCtrStride;
+constexpr size_t kSchedBytes = kSchedSlots * kSchedStride * sizeof(unsigned long long);
+#ifndef PNET_STATIC_PCT
+#define PNET_STATIC_PCT 90   // share of a batch's runs assigned statically (100: no claims)
+#endif
+#ifndef PNET_CLAIM_COUNTERS
+#define PNET_CLAIM_COUNTERS 32
+#endif
 
 int set_device(const pnetgpu_ctx* ctx) {
     const hipError_t e = hipSetDevice(ctx->device);
@@ -119,11 +137,26 @@ int pnetgpu_ctx_create(int device, pnetgpu_ctx** out) {
     if (!c) return PNETGPU_ENOMEM;
     c->device = device;
     c->cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+    if (hipMalloc((void**)&c->d_sched, kSchedBytes) != hipSuccess) {
+        delete c;
+        return PNETGPU_ENOMEM;
+    }
+    if (hipMemset(c->d_sched, 0, kSchedBytes) != hipSuccess) {
+        pnetgpu_ctx_destroy(c);
+        return PNETGPU_EHIP;
+    }
     *out = c;
     return PNETGPU_OK;
 }
 
-void pnetgpu_ctx_destroy(pnetgpu_ctx* ctx) { delete ctx; }
+void pnetgpu_ctx_destroy(pnetgpu_ctx* ctx) {
+    if (!ctx) return;
+    if (ctx->d_sched) {
+        (void)hipSetDevice(ctx->device);
+        (void)hipFree(ctx->d_sched);
+    }
+    delete ctx;
+}
 
 static int rx_common(pnetgpu_ctx* ctx, const pnetgpu_batch* b, const pnetgpu_rx_columns* cols, void* stream,
                      bool tx) {
@@ -204,6 +237,32 @@ static int rx_common(pnetgpu_ctx* ctx, const pnetgpu_batch* b, const pnetgpu_rx_
     const uint64_t want = (a.nruns + wpb - 1) / wpb;
     const uint64_t cap = (uint64_t)ctx->cus * (uint64_t)per_cu;
     const int blocks = (int)std::max<uint64_t>(1, std::min(want, cap));
+    // Run scheduling: a static grid-stride share, then claimed runs, so that
+    // waves whose share ran slow (the younger waves of a SIMD, the slower XCDs)
+    // do not set the kernel's end. Batches of fewer than 8 runs per wave stay
+    // static (1500-B frames at 4 runs per wave: claims measured even to +1 %).
+    const char* static_env = std::getenv("PNETGPU_STATIC_PCT");   // tuning override (tools/)
+    const int static_pct = static_env ? std::atoi(static_env) : PNET_STATIC_PCT;
+    const uint64_t nwaves = (uint64_t)blocks * wpb;
+    a.nstatic = a.nruns;
+    if (static_pct >= 0 && static_pct < 100 && a.nruns >= 8 * nwaves) {
+        a.nstatic = (a.nruns * (uint64_t)static_pct / 100) / nwaves * nwaves;
+        uint32_t e = ++ctx->epoch;
+        if (e >= 0xFFFFFF00u) {   // epochs must grow: re-zero the slots before the count wraps
+            if (hipDeviceSynchronize() != hipSuccess || hipMemset(ctx->d_sched, 0, kSchedBytes) != hipSuccess)
+                return pnetgpu::hip_fail(hipGetLastError());
+            ctx->epoch = 1;
+            e = 1;
+        }
+        a.epoch = e;
+        a.sched = ctx->d_sched + (size_t)(e % kSchedSlots) * kSchedStride;
+        const char* nctr_env = std::getenv("PNETGPU_CLAIM_COUNTERS");   // tuning override (tools/)
+        const int nctr = nctr_env ? std::atoi(nctr_env) : PNET_CLAIM_COUNTERS;
+        // every counter needs home waves: wave ids [0, 32 nctr) cover them all
+        const uint64_t homes = std::max<uint64_t>(1, nwaves / 32);
+        a.nctr = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>({(uint64_t)std::max(nctr, 1), kMaxCtrs, homes}));
+        a.ctr_stride = (uint32_t)kCtrStride;
+    }
     if (const int e = pnetgpu::launch_rx(a, kind, blocks, tx, static_cast<hipStream_t>(stream))) {
         pnetgpu::set_last_hip_error(e);
         if (debug)

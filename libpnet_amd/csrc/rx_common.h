@@ -43,6 +43,107 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+#ifdef PNET_WAVE_TIMES
+// the wave-time probe (rx_internal.h): lane 0 writes its wave's record with
+// ordinary vector stores; the hardware ids come from s_getreg (XCC_ID, HW_ID)
+__device__ uint64_t pnet_wave_times[kWaveTimeSlots * kWaveTimeWords];
+struct WaveTimer {
+    uint64_t t0 = wall_clock64();
+    uint32_t runs = 0;
+    __device__ void end(uint64_t wid, int lane) {
+        const uint64_t t1 = wall_clock64();
+        uint32_t xcc, hwid;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid));
+        if (lane == 0 && wid < (uint64_t)kWaveTimeSlots) {
+            uint64_t* p = pnet_wave_times + wid * kWaveTimeWords;
+            p[0] = t0;
+            p[1] = t1;
+            p[2] = ((uint64_t)(xcc & 15u) << 32) | hwid;
+            p[3] = runs;
+        }
+    }
+};
+#define PNET_WT_BEGIN WaveTimer pnet_wt_
+#define PNET_WT_RUN ++pnet_wt_.runs
+#define PNET_WT_END(wid) pnet_wt_.end((wid), lane)
+#else
+#define PNET_WT_BEGIN
+#define PNET_WT_RUN
+#define PNET_WT_END(wid)
+#endif
+
+#ifdef PNET_PRIO_ROTATE
+// A/B probe: the wave's issue priority rotates with its run count, phased by
+// its hardware wave slot, so no wave of a SIMD keeps the age-order lead
+__device__ __forceinline__ void rotate_prio(uint32_t runs) {
+    uint32_t hwid;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid));
+    switch ((runs + hwid) & 3u) {
+    case 0: __builtin_amdgcn_s_setprio(0); break;
+    case 1: __builtin_amdgcn_s_setprio(1); break;
+    case 2: __builtin_amdgcn_s_setprio(2); break;
+    default: __builtin_amdgcn_s_setprio(3);
+    }
+}
+#define PNET_PRIO(k) rotate_prio(k)
+#else
+#define PNET_PRIO(k)
+#endif
+
+// The runs one wave processes (RxArgs::sched): its grid-stride share of
+// [0, nstatic), then runs claimed from one of the launch's nctr counters (the
+// wave's home counter, (wave id / 32) % nctr, owns an equal slice of
+// [nstatic, nruns); 32 consecutive wave ids are 8 blocks, which the dispatcher
+// spreads over the 8 XCDs, so every counter balances work across them),
+// one claim kept in flight ahead of its use so the atomic's round trip
+// overlaps a whole run. take() returns the next run; >= nruns ends the loop.
+struct RunQueue {
+    uint64_t next_static, stride, nstatic, nruns, lo, hi;
+    unsigned long long* ctr;
+    uint64_t pend;          // claimed ahead (dynamic phase), nruns when none is pending
+    uint32_t epoch;
+    bool stamped;
+
+    __device__ RunQueue(const RxArgs& a, uint64_t wave_id, uint64_t wave_stride)
+        : next_static(wave_id), stride(wave_stride), nstatic(a.nstatic), nruns(a.nruns), lo(0), hi(0),
+          ctr(a.sched), pend(a.nruns), epoch(a.epoch), stamped(false) {
+        if (ctr) {
+            const uint64_t h = (wave_id >> 5) % a.nctr, d = a.nruns - a.nstatic;
+            lo = a.nstatic + d * h / a.nctr;
+            hi = a.nstatic + d * (h + 1) / a.nctr;
+            ctr += h * a.ctr_stride;
+            if (next_static >= nstatic) claim();   // no static share: the first claim now
+        }
+    }
+    __device__ void claim() {
+        uint32_t k = 0;
+        if (__lane_id() == 0) {
+            if (!stamped) {
+                // the slot may hold an earlier launch's count: lift it to this
+                // epoch with a zero count (a no-op once any wave has done so)
+                (void)atomicMax(ctr, (unsigned long long)epoch << 32);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            k = (uint32_t)atomicAdd(ctr, 1ull);
+        }
+        stamped = true;
+        const uint64_t r = lo + (uint64_t)__builtin_amdgcn_readfirstlane(k);
+        pend = r < hi ? r : nruns;
+    }
+    __device__ uint64_t take() {
+        if (next_static < nstatic) {
+            const uint64_t r = next_static;
+            next_static += stride;
+            if (ctr && next_static >= nstatic) claim();   // last static run: the first claim goes out
+            return r;
+        }
+        const uint64_t r = pend;
+        if (r < nruns) claim();
+        return r;
+    }
+};
+
 // Inclusive scan over the wave: DPP row_shr 1/2/4/8 inside each 16-lane row,
 // then row_bcast:15 and row_bcast:31 carry the row totals forward.
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {

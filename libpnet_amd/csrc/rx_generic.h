@@ -172,8 +172,16 @@ __global__ __launch_bounds__(kBlock, NW < 8 ? 5 : 4) void rx_kernel(RxArgs a) {
             }
         }
     };
-    fetch_desc((uint64_t)blockIdx.x * kWavesPerBlock + wv);
-    for (uint64_t run = (uint64_t)blockIdx.x * kWavesPerBlock + wv; run < a.nruns; run += wave_stride) {
+    PNET_WT_BEGIN;
+    uint32_t run_count = 0;
+    (void)run_count;
+    RunQueue q(a, (uint64_t)blockIdx.x * kWavesPerBlock + wv, wave_stride);
+    uint64_t run = q.take();
+    fetch_desc(run);
+    while (run < a.nruns) {
+        PNET_WT_RUN;
+        PNET_PRIO(run_count++);
+        const uint64_t nrun = q.take();   // the next run (its claim went out a run ago)
         // ---- 1. descriptor -------------------------------------------------
         const uint64_t f0 = run * kWave;
         const uint64_t f = f0 + lane;
@@ -215,7 +223,7 @@ __global__ __launch_bounds__(kBlock, NW < 8 ? 5 : 4) void rx_kernel(RxArgs a) {
                 if ((uint32_t)c < L.end[fl])
                     g[i] = load16(a.data + L.base[fl] + 16u * c);
             }
-            fetch_desc(run + wave_stride);
+            fetch_desc(nrun);
 #pragma unroll
             for (int i = 0; i < NW; ++i) {
                 const int q = i * kWave + lane;
@@ -224,7 +232,7 @@ __global__ __launch_bounds__(kBlock, NW < 8 ? 5 : 4) void rx_kernel(RxArgs a) {
                 dst[0] = g[i].x; dst[1] = g[i].y; dst[2] = g[i].z; dst[3] = g[i].w;
             }
         } else {
-            fetch_desc(run + wave_stride);
+            fetch_desc(nrun);
         }
 
         // ---- 3. speculative tail: all frame bytes past the window ----------
@@ -280,8 +288,10 @@ __global__ __launch_bounds__(kBlock, NW < 8 ? 5 : 4) void rx_kernel(RxArgs a) {
 #endif
         if (a.cols.counters) K.add(in_batch && !desc_bad, len, P.st);
         wave_sync();   // slots and lists are rewritten by the next run
+        run = nrun;
     }
     if (a.cols.counters) K.flush(a.cols.counters, blk_ctr, wv, lane);
+    PNET_WT_END((uint64_t)blockIdx.x * kWavesPerBlock + wv);
 }
 
 }  // namespace

@@ -24,6 +24,16 @@ struct RxArgs {
     uint32_t desc_compact;   // offsets/lengths are uint32_t/uint16_t arrays (PNETGPU_DESC_COMPACT)
     uint32_t field_cols;     // any ABI-v3 header-field column requested (store_field_columns)
     uint32_t l3mode;         // PNETGPU_RX_L3: frames start at the IP header (no Ethernet view)
+    // Run scheduling: runs [0, nstatic) go to the persistent waves in grid-stride
+    // order (nstatic is a multiple of the wave count), runs [nstatic, nruns) are
+    // claimed one at a time from the launch's counter *sched (high 32 bits: the
+    // launch epoch, stamped by atomicMax; low 32 bits: claims), so waves whose
+    // share ran slow do not set the kernel's end. sched == nullptr: all static.
+    unsigned long long* sched;
+    uint64_t nstatic;
+    uint32_t epoch;
+    uint32_t nctr;           // counters of the launch, ctr_stride u64 apart
+    uint32_t ctr_stride;
     pnetgpu_rx_columns cols;
 };
 
@@ -61,6 +71,12 @@ constexpr int kKindMixed = 0;
 constexpr int kKindSmall = 1;
 constexpr int kKindMtu = 2;
 constexpr int kKindJumbo = 3;
+
+// Tuning probe (tools/wave_times.py; built only as a variant library with
+// -DPNET_WAVE_TIMES, never in the shipped one): every wave of a receive launch
+// records its start and end wall clock (100 MHz), hardware ids and run count.
+constexpr int kWaveTimeSlots = 16384;
+constexpr int kWaveTimeWords = 4;   // t_start, t_end, (xcc << 32) | HW_ID, runs
 
 // device index a context is bound to (abi.cpp)
 int ctx_device(const pnetgpu_ctx* ctx);

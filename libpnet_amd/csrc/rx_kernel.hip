@@ -286,3 +286,19 @@ int launch_slices(const SliceArgs& args, int pseudo, bool run, int blocks, hipSt
 }
 
 }  // namespace pnetgpu
+
+#ifdef PNET_WAVE_TIMES
+// The wave-time probe's host side (variant builds only, tools/wave_times.py):
+// clear the records before a launch, copy them out after it.
+extern "C" int pnetgpu_probe_wave_times(uint64_t* host, size_t words, int clear) {
+    using pnetgpu::pnet_wave_times;
+    const size_t cap = (size_t)pnetgpu::kWaveTimeSlots * pnetgpu::kWaveTimeWords;
+    if (words > cap) words = cap;
+    if (clear) {
+        void* p = nullptr;
+        if (hipGetSymbolAddress(&p, HIP_SYMBOL(pnet_wave_times)) != hipSuccess) return -1;
+        return hipMemset(p, 0, cap * sizeof(uint64_t)) == hipSuccess ? 0 : -1;
+    }
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(pnet_wave_times), words * sizeof(uint64_t)) == hipSuccess ? 0 : -1;
+}
+#endif

@@ -177,15 +177,19 @@ __global__ __launch_bounds__(kBlock, PNET_SMALL_WAVES) void rx_small_kernel(RxAr
     Counters K;
 
     const uint64_t wave_stride = (uint64_t)gridDim.x * kWavesPerBlock;
-    uint64_t run = (uint64_t)blockIdx.x * kWavesPerBlock + wv;
+    PNET_WT_BEGIN;
+    uint32_t run_count = 0;
+    (void)run_count;
+    RunQueue q(a, (uint64_t)blockIdx.x * kWavesPerBlock + wv, wave_stride);
+    uint64_t run = q.take();
     SmallRun cur = run < a.nruns ? small_load(a, run, lane) : SmallRun{};
-    for (; run < a.nruns; run += wave_stride) {
+    while (run < a.nruns) {
+        PNET_WT_RUN;
+        PNET_PRIO(run_count++);
         // software pipelining: the next run's loads are in flight while this one is processed
         // (two runs ahead measured no faster: the wave is not short of loads in flight)
-#ifndef PNET_SMALL_NOPF
-        const uint64_t nrun = run + wave_stride;
+        const uint64_t nrun = q.take();
         SmallRun nxt = nrun < a.nruns ? small_load(a, nrun, lane) : SmallRun{};
-#endif
 
         const uint64_t f0 = run * kWave;
         const bool in_batch = f0 + lane < a.n;
@@ -259,13 +263,11 @@ __global__ __launch_bounds__(kBlock, PNET_SMALL_WAVES) void rx_small_kernel(RxAr
 #endif
         if (a.cols.counters) K.add(in_batch, len, P.st);
         wave_sync();
-#ifndef PNET_SMALL_NOPF
         cur = nxt;
-#else
-        if (run + wave_stride < a.nruns) cur = small_load(a, run + wave_stride, lane);
-#endif
+        run = nrun;
     }
     if (a.cols.counters) K.flush(a.cols.counters, blk_ctr, wv, lane);
+    PNET_WT_END((uint64_t)blockIdx.x * kWavesPerBlock + wv);
 }
 
 }  // namespace

@@ -29,8 +29,16 @@ def main():
     ap.add_argument("--tx", action="store_true", help="time tx_fill_checksums instead of rx_process")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
-    key, vals = (a.env.split("=") + [""])[:2] if a.env else ("", "")
-    vals = vals.split(",") if vals else [None]
+    # --env KEY=v1,v2 or --env "K1=a+K2=b,K1=c+K2=d" (each comma-separated item one setting)
+    if a.env and "+" not in a.env and a.env.count("=") == 1:
+        key, vs = a.env.split("=")
+        configs = [(f"{key}={v}", {key: v}) for v in vs.split(",")]
+    elif a.env:
+        configs = [(item, dict(kv.split("=") for kv in item.split("+"))) for item in a.env.split(",")]
+    else:
+        configs = [("", {})]
+    vals = [c[0] for c in configs]
+    envs = dict(configs)
     s = torch.cuda.Stream()
     for name in a.workloads.split(","):
         n = WORKLOADS[name]["n"] if name in WORKLOADS else EXTRA[name]
@@ -45,8 +53,7 @@ def main():
         times = {v: [] for v in vals}
         for _ in range(a.rounds):
             for v in vals:
-                if key:
-                    os.environ[key] = v
+                os.environ.update(envs[v])
                 for _ in range(2):
                     sh.step(s)
                 evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.reps)]
@@ -59,7 +66,7 @@ def main():
         for v in vals:
             t = np.array(times[v])
             med = float(np.median(t))
-            print(f"{name:10s} {key}={v}: median {med*1e3:8.1f} us  min {t.min()*1e3:8.1f} us  "
+            print(f"{name:10s} {v}: median {med*1e3:8.1f} us  min {t.min()*1e3:8.1f} us  "
                   f"alg {sh.alg_bytes/med/1e6:7.0f} GB/s ({sh.alg_bytes/med/1e6/HBM_PEAK_GBS:.1%})  "
                   f"{sh.n/med/1e3:9.0f} Mpkts/s", flush=True)
         del sh
