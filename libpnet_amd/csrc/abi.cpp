@@ -68,11 +68,41 @@ constexpr size_t kCtrStride = 256 / sizeof(unsigned long long);      // 256 B ap
 constexpr size_t kSchedStride = kMaxCtrs * kCtrStride;
 constexpr size_t kSchedBytes = kSchedSlots * kSchedStride * sizeof(unsigned long long);
 #ifndef PNET_STATIC_PCT
-#define PNET_STATIC_PCT 90   // share of a batch's runs assigned statically (100: no claims)
+#define PNET_STATIC_PCT 88   // share of a batch's runs assigned statically (100: no claims)
 #endif
 #ifndef PNET_CLAIM_COUNTERS
-#define PNET_CLAIM_COUNTERS 32
+#define PNET_CLAIM_COUNTERS 64
 #endif
+
+// Run scheduling of a persistent-grid launch (RunSched): a static grid-stride
+// share, then claimed units, so that waves whose share ran slow (the younger
+// waves of a SIMD, the slower XCDs: tools/wave_times.py) do not set the
+// kernel's end. Launches of fewer than 8 units per wave stay static (1500-B
+// frames at 4 runs per wave: claims measured even to +1 %).
+int plan_sched(pnetgpu_ctx* ctx, uint64_t nunits, uint64_t nwaves, pnetgpu::RunSched* s) {
+    *s = pnetgpu::RunSched{};
+    s->nstatic = nunits;
+    const char* static_env = std::getenv("PNETGPU_STATIC_PCT");   // tuning override (tools/)
+    const int static_pct = static_env ? std::atoi(static_env) : PNET_STATIC_PCT;
+    if (static_pct < 0 || static_pct >= 100 || nwaves == 0 || nunits < 8 * nwaves) return PNETGPU_OK;
+    s->nstatic = (nunits * (uint64_t)static_pct / 100) / nwaves * nwaves;
+    uint32_t e = ++ctx->epoch;
+    if (e >= 0xFFFFFF00u) {   // epochs must grow: re-zero the slots before the count wraps
+        if (hipDeviceSynchronize() != hipSuccess || hipMemset(ctx->d_sched, 0, kSchedBytes) != hipSuccess)
+            return pnetgpu::hip_fail(hipGetLastError());
+        ctx->epoch = 1;
+        e = 1;
+    }
+    s->epoch = e;
+    s->ctr = ctx->d_sched + (size_t)(e % kSchedSlots) * kSchedStride;
+    const char* nctr_env = std::getenv("PNETGPU_CLAIM_COUNTERS");   // tuning override (tools/)
+    const int nctr = nctr_env ? std::atoi(nctr_env) : PNET_CLAIM_COUNTERS;
+    // every counter needs home waves: wave ids [0, 32 nctr) cover them all
+    const uint64_t homes = std::max<uint64_t>(1, nwaves / 32);
+    s->nctr = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>({(uint64_t)std::max(nctr, 1), kMaxCtrs, homes}));
+    s->ctr_stride = (uint32_t)kCtrStride;
+    return PNETGPU_OK;
+}
 
 int set_device(const pnetgpu_ctx* ctx) {
     const hipError_t e = hipSetDevice(ctx->device);
@@ -237,32 +267,7 @@ static int rx_common(pnetgpu_ctx* ctx, const pnetgpu_batch* b, const pnetgpu_rx_
     const uint64_t want = (a.nruns + wpb - 1) / wpb;
     const uint64_t cap = (uint64_t)ctx->cus * (uint64_t)per_cu;
     const int blocks = (int)std::max<uint64_t>(1, std::min(want, cap));
-    // Run scheduling: a static grid-stride share, then claimed runs, so that
-    // waves whose share ran slow (the younger waves of a SIMD, the slower XCDs)
-    // do not set the kernel's end. Batches of fewer than 8 runs per wave stay
-    // static (1500-B frames at 4 runs per wave: claims measured even to +1 %).
-    const char* static_env = std::getenv("PNETGPU_STATIC_PCT");   // tuning override (tools/)
-    const int static_pct = static_env ? std::atoi(static_env) : PNET_STATIC_PCT;
-    const uint64_t nwaves = (uint64_t)blocks * wpb;
-    a.nstatic = a.nruns;
-    if (static_pct >= 0 && static_pct < 100 && a.nruns >= 8 * nwaves) {
-        a.nstatic = (a.nruns * (uint64_t)static_pct / 100) / nwaves * nwaves;
-        uint32_t e = ++ctx->epoch;
-        if (e >= 0xFFFFFF00u) {   // epochs must grow: re-zero the slots before the count wraps
-            if (hipDeviceSynchronize() != hipSuccess || hipMemset(ctx->d_sched, 0, kSchedBytes) != hipSuccess)
-                return pnetgpu::hip_fail(hipGetLastError());
-            ctx->epoch = 1;
-            e = 1;
-        }
-        a.epoch = e;
-        a.sched = ctx->d_sched + (size_t)(e % kSchedSlots) * kSchedStride;
-        const char* nctr_env = std::getenv("PNETGPU_CLAIM_COUNTERS");   // tuning override (tools/)
-        const int nctr = nctr_env ? std::atoi(nctr_env) : PNET_CLAIM_COUNTERS;
-        // every counter needs home waves: wave ids [0, 32 nctr) cover them all
-        const uint64_t homes = std::max<uint64_t>(1, nwaves / 32);
-        a.nctr = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>({(uint64_t)std::max(nctr, 1), kMaxCtrs, homes}));
-        a.ctr_stride = (uint32_t)kCtrStride;
-    }
+    if (const int rc = plan_sched(ctx, a.nruns, (uint64_t)blocks * wpb, &a.sched)) return rc;
     if (const int e = pnetgpu::launch_rx(a, kind, blocks, tx, static_cast<hipStream_t>(stream))) {
         pnetgpu::set_last_hip_error(e);
         if (debug)
@@ -334,6 +339,7 @@ static int slices_common(pnetgpu_ctx* ctx, const uint8_t* data, uint64_t data_by
     if (kenv) run = kenv[0] == 'r' ? true : kenv[0] == 'g' ? false : run;
     const uint64_t per_block = run ? kBlock : kBlock / 16;
     const int blocks = slice_grid(ctx, run ? 1 : 2, pseudo, extra_offsets != nullptr, (n + per_block - 1) / per_block);
+    if (run && (rc = plan_sched(ctx, (n + 63) / 64, (uint64_t)blocks * 4, &a.sched))) return rc;
     if (const int e = pnetgpu::launch_slices(a, pseudo, run, blocks, static_cast<hipStream_t>(stream))) {
         pnetgpu::set_last_hip_error(e);
         return PNETGPU_EHIP;
@@ -371,6 +377,12 @@ int pnetgpu_checksum_slices_strided(pnetgpu_ctx* ctx, const uint8_t* data, uint6
     const uint64_t per_block = small || run ? kBlock : kBlock / 16;
     const int blocks = slice_grid(ctx, small ? 0 : run ? 1 : 2, small ? pnetgpu::strided_variant(slice_len, stride) : 0, false,
                                   (n + per_block - 1) / per_block);
+    // scheduled units: slice_strided_kernel's blocks of R runs (R as the kernel
+    // computes it), slice_run_kernel's runs
+    const uint64_t runs_per_unit = small ? (stride ? std::max(1u, std::min(16u, 4096u / (64u * stride))) : 16u) : 1u;
+    if ((small || run) && (rc = plan_sched(ctx, (n + 64 * runs_per_unit - 1) / (64 * runs_per_unit),
+                                           (uint64_t)blocks * 4, &a.sched)))
+        return rc;
     const int e = small ? pnetgpu::launch_slices_strided_small(a, blocks, static_cast<hipStream_t>(stream))
                         : pnetgpu::launch_slices(a, 0, run, blocks, static_cast<hipStream_t>(stream));
     if (e) return pnetgpu::hip_fail((hipError_t)e);
@@ -398,6 +410,7 @@ int pnetgpu_checksum_slices_compact(pnetgpu_ctx* ctx, const uint8_t* data, uint6
     if (kenv) run = kenv[0] == 'r' ? true : kenv[0] == 'g' ? false : run;
     const uint64_t per_block = run ? kBlock : kBlock / 16;
     const int blocks = slice_grid(ctx, run ? 1 : 2, 0, false, (n + per_block - 1) / per_block);
+    if (run && (rc = plan_sched(ctx, (n + 63) / 64, (uint64_t)blocks * 4, &a.sched))) return rc;
     if (const int e = pnetgpu::launch_slices(a, 0, run, blocks, static_cast<hipStream_t>(stream))) return pnetgpu::hip_fail((hipError_t)e);
     return PNETGPU_OK;
 }

@@ -105,14 +105,14 @@ struct RunQueue {
     uint32_t epoch;
     bool stamped;
 
-    __device__ RunQueue(const RxArgs& a, uint64_t wave_id, uint64_t wave_stride)
-        : next_static(wave_id), stride(wave_stride), nstatic(a.nstatic), nruns(a.nruns), lo(0), hi(0),
-          ctr(a.sched), pend(a.nruns), epoch(a.epoch), stamped(false) {
+    __device__ RunQueue(const RunSched& s, uint64_t n_units, uint64_t wave_id, uint64_t wave_stride)
+        : next_static(wave_id), stride(wave_stride), nstatic(s.ctr ? s.nstatic : n_units), nruns(n_units), lo(0),
+          hi(0), ctr(s.ctr), pend(n_units), epoch(s.epoch), stamped(false) {
         if (ctr) {
-            const uint64_t h = (wave_id >> 5) % a.nctr, d = a.nruns - a.nstatic;
-            lo = a.nstatic + d * h / a.nctr;
-            hi = a.nstatic + d * (h + 1) / a.nctr;
-            ctr += h * a.ctr_stride;
+            const uint64_t h = (wave_id >> 5) % s.nctr, d = nruns - nstatic;
+            lo = nstatic + d * h / s.nctr;
+            hi = nstatic + d * (h + 1) / s.nctr;
+            ctr += h * s.ctr_stride;
             if (next_static >= nstatic) claim();   // no static share: the first claim now
         }
     }

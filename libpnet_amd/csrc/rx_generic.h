@@ -175,7 +175,7 @@ __global__ __launch_bounds__(kBlock, NW < 8 ? 5 : 4) void rx_kernel(RxArgs a) {
     PNET_WT_BEGIN;
     uint32_t run_count = 0;
     (void)run_count;
-    RunQueue q(a, (uint64_t)blockIdx.x * kWavesPerBlock + wv, wave_stride);
+    RunQueue q(a.sched, a.nruns, (uint64_t)blockIdx.x * kWavesPerBlock + wv, wave_stride);
     uint64_t run = q.take();
     fetch_desc(run);
     while (run < a.nruns) {

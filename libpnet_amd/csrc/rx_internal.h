@@ -7,6 +7,21 @@
 
 namespace pnetgpu {
 
+// Run scheduling of a persistent-grid launch (RunQueue in rx_common.h): units
+// (runs, or slice blocks) [0, nstatic) go to the waves in grid-stride order
+// (nstatic is a multiple of the wave count); units [nstatic, n) are claimed one
+// at a time from nctr counters, ctr_stride u64 apart from ctr (high 32 bits of
+// a counter: the launch epoch, stamped by atomicMax; low 32 bits: claims), so
+// waves whose share ran slow do not set the kernel's end. ctr == nullptr: all
+// units static.
+struct RunSched {
+    unsigned long long* ctr;
+    uint64_t nstatic;
+    uint32_t epoch;
+    uint32_t nctr;
+    uint32_t ctr_stride;
+};
+
 // `data` is 16-B aligned; every descriptor offset is shifted by `delta` (the
 // caller pointer's misalignment) and must satisfy off + len <= limit.
 struct RxArgs {
@@ -24,16 +39,7 @@ struct RxArgs {
     uint32_t desc_compact;   // offsets/lengths are uint32_t/uint16_t arrays (PNETGPU_DESC_COMPACT)
     uint32_t field_cols;     // any ABI-v3 header-field column requested (store_field_columns)
     uint32_t l3mode;         // PNETGPU_RX_L3: frames start at the IP header (no Ethernet view)
-    // Run scheduling: runs [0, nstatic) go to the persistent waves in grid-stride
-    // order (nstatic is a multiple of the wave count), runs [nstatic, nruns) are
-    // claimed one at a time from the launch's counter *sched (high 32 bits: the
-    // launch epoch, stamped by atomicMax; low 32 bits: claims), so waves whose
-    // share ran slow do not set the kernel's end. sched == nullptr: all static.
-    unsigned long long* sched;
-    uint64_t nstatic;
-    uint32_t epoch;
-    uint32_t nctr;           // counters of the launch, ctr_stride u64 apart
-    uint32_t ctr_stride;
+    RunSched sched;          // run scheduling (static share + claimed runs)
     pnetgpu_rx_columns cols;
 };
 
@@ -61,6 +67,7 @@ struct SliceArgs {
     // slice_run_kernel: a run of small sorted slices is staged through LDS when
     // its span is at least this many bytes (dense_span())
     uint32_t dense_min;
+    RunSched sched;      // slice_run_kernel / slice_strided_kernel run scheduling
 };
 
 // Kernel kinds: the register-resident small-frame kernel (fixed stride, frames

@@ -324,7 +324,8 @@ __global__ __launch_bounds__(kBlock, PNET_RUN_MINWAVES) void slice_run_kernel(Sl
     const int wv = threadIdx.x / kWave;
     const uint64_t nruns = (a.n + kWave - 1) / kWave;
     const uint64_t wave_stride = (uint64_t)gridDim.x * kWavesPerBlock;
-    for (uint64_t run = (uint64_t)blockIdx.x * kWavesPerBlock + wv; run < nruns; run += wave_stride) {
+    RunQueue q(a.sched, nruns, (uint64_t)blockIdx.x * kWavesPerBlock + wv, wave_stride);
+    for (uint64_t run = q.take(); run < nruns; run = q.take()) {
         const uint64_t i = run * kWave + lane;
         const bool in = i < a.n;
         uint64_t off = 0;
@@ -455,12 +456,14 @@ __global__ __launch_bounds__(kBlock) void slice_strided_kernel(SliceArgs a) {
             v[c] = g < k.ng ? load16_nt(a.data + k.g0 + 16u * g) : make_uint4(0, 0, 0, 0);
         }
     };
-    uint64_t b = (uint64_t)blockIdx.x * kWavesPerBlock + wv;
+    RunQueue q(a.sched, nblk, (uint64_t)blockIdx.x * kWavesPerBlock + wv, wave_stride);
+    uint64_t b = q.take();
     Blk cur = locate(b);
     uint4 v[5], w[5];
     load(cur, v);
-    for (; b < nblk; b += wave_stride) {
-        const Blk nxt = locate(b + wave_stride);
+    while (b < nblk) {
+        const uint64_t nb = q.take();
+        const Blk nxt = locate(nb);
         load(nxt, w);                                 // in flight while this block is summed
 #pragma unroll
         for (int c = 0; c < 5; ++c) {
@@ -548,6 +551,7 @@ __global__ __launch_bounds__(kBlock) void slice_strided_kernel(SliceArgs a) {
         }
         wave_sync();   // the stage is rewritten by the next block
         cur = nxt;
+        b = nb;
 #pragma unroll
         for (int c = 0; c < 5; ++c) v[c] = w[c];
     }

@@ -180,7 +180,7 @@ __global__ __launch_bounds__(kBlock, PNET_SMALL_WAVES) void rx_small_kernel(RxAr
     PNET_WT_BEGIN;
     uint32_t run_count = 0;
     (void)run_count;
-    RunQueue q(a, (uint64_t)blockIdx.x * kWavesPerBlock + wv, wave_stride);
+    RunQueue q(a.sched, a.nruns, (uint64_t)blockIdx.x * kWavesPerBlock + wv, wave_stride);
     uint64_t run = q.take();
     SmallRun cur = run < a.nruns ? small_load(a, run, lane) : SmallRun{};
     while (run < a.nruns) {

@@ -28,9 +28,20 @@ def main():
                lp.ipv4_checksum_slices(b, o, ln, k, ad, pr, stream=s)) if pseudo else
               (lambda b=buf, o=offs, ln=lens, k=skips: lp.checksum_slices(b, o, ln, k, stream=s)))
         cases.append((name, n, size, fn))
+    # the reference's 20-B shape as uniform slices (no descriptors)
+    sbuf = torch.randint(0, 256, ((1 << 24) * 20 + 32,), dtype=torch.uint8, device=dev)
+    cases.append(("strided20", 1 << 24, 20,
+                  lambda b=sbuf: lp.checksum_slices_strided(b, 1 << 24, 20, 20, 5, stream=s)))
+    # --env KEY=v1,v2 (e.g. PNETGPU_STATIC_PCT=100,90): every case per value, interleaved
+    env = next((x.split("=", 1) for x in sys.argv[1:] if "=" in x), None)
+    vals = env[1].split(",") if env else [None]
+    cases = [(f"{name}{'' if v is None else ' ' + env[0] + '=' + v}", n, size, fn, v)
+             for name, n, size, fn in cases for v in vals]
     times = {c[0]: [] for c in cases}
     for _ in range(3):
-        for name, n, size, fn in cases:
+        for name, n, size, fn, v in cases:
+            if v is not None:
+                os.environ[env[0]] = v
             for _ in range(2):
                 fn()
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -40,9 +51,9 @@ def main():
             b.record(s)
             s.synchronize()
             times[name].append(a.elapsed_time(b) / 10)
-    for name, n, size, fn in cases:
+    for name, n, size, fn, v in cases:
         ms = float(np.median(times[name]))
-        print(f"{name:12s} {ms * 1e3:8.1f} us  {n / ms / 1e6:9.1f} Mslices/s  "
+        print(f"{name:36s} {ms * 1e3:8.1f} us  {n / ms / 1e6:9.1f} Mslices/s  "
               f"{n * (size + 18) / ms / 1e6:7.0f} GB/s alg", flush=True)
 
 
