@@ -50,6 +50,9 @@
  *     round_up(data + data_bytes, 16). (hipMalloc'd buffers always are.)
  *   - Threading: a context is bound to one device; calls on one context may be
  *     issued from one host thread at a time. Distinct contexts are independent.
+ *     Up to 64 receive / slice launches of one context may be in flight at once
+ *     (on any streams): each takes one of the context's 64 run-claim counter
+ *     slots by launch order (run scheduling).
  *   - Malformed input never faults: frames whose descriptor falls outside
  *     [0, data_bytes) get PNET_ST_DESC_INVALID, short frames get the
  *     *_MALFORMED bits (the reference's `new()` returning None).
