@@ -83,7 +83,10 @@ constexpr int kKindJumbo = 3;
 // -DPNET_WAVE_TIMES, never in the shipped one): every wave of a receive launch
 // records its start and end wall clock (100 MHz), hardware ids and run count.
 constexpr int kWaveTimeSlots = 16384;
-constexpr int kWaveTimeWords = 4;   // t_start, t_end, (xcc << 32) | HW_ID, runs
+// t_start, t_end, (xcc << 32) | HW_ID, runs, then the shader clocks (s_memtime)
+// the wave spent in each phase of its runs (PNET_PH marks: rx_kernel's window,
+// tail, parse, stores) and the wave's whole s_memtime span
+constexpr int kWaveTimeWords = 10;
 
 // device index a context is bound to (abi.cpp)
 int ctx_device(const pnetgpu_ctx* ctx);

@@ -210,6 +210,7 @@ __global__ __launch_bounds__(kBlock, PNET_SMALL_WAVES) void rx_small_kernel(RxAr
         const uint32_t wv16[16] = {cur.g[0].x, cur.g[0].y, cur.g[0].z, cur.g[0].w, cur.g[1].x, cur.g[1].y,
                                    cur.g[1].z, cur.g[1].w, cur.g[2].x, cur.g[2].y, cur.g[2].z, cur.g[2].w,
                                    cur.g[3].x, cur.g[3].y, cur.g[3].z, cur.g[3].w};
+        PNET_PH(0);   // probe: next run's loads issued, this run's transpose (waits for its loads)
         const bool slow = in_batch && small_fast(wv16, len, P, ipc, l4c);
         // ---- generic path through LDS for the lanes the fast path did not take ----
         const bool need_v6 = a.cols.src_ipv6 || a.cols.dst_ipv6;
@@ -229,7 +230,7 @@ __global__ __launch_bounds__(kBlock, PNET_SMALL_WAVES) void rx_small_kernel(RxAr
 #endif
             if (slow) {
                 // flags are 0 here and the frame (<= 64 B) is entirely in its slot
-                P = parse_frame(FrameBytes{slot, slot, 64}, len, 0u);
+                P = parse_frame(FrameBytes{slot, 0, 0u, slot, 64}, len, 0u);
                 uint32_t tA = 0, tB = 0;
                 window_sums(slot, P.a_lo, P.a_hi, P.b_lo, P.b_hi, tA, tB);
                 finalize(P, tA, tB, false, ipc, l4c);
@@ -256,13 +257,15 @@ __global__ __launch_bounds__(kBlock, PNET_SMALL_WAVES) void rx_small_kernel(RxAr
                 }
             }
         }
+        PNET_PH(2);   // probe: fast path / parse
         store_columns(a.cols, f0, lane, in_batch, P, ipc, l4c, slot, 0);
 #ifndef PNET_NO_FIELD_COLUMNS   // A/B: the header-field stores compiled out
         if (FIELDS && a.field_cols && in_batch)
-            store_field_columns(a.cols, f0 + lane, P, FrameBytes{slot, slot, 64}, false);
+            store_field_columns(a.cols, f0 + lane, P, FrameBytes{slot, 0, 0u, slot, 64}, false);
 #endif
         if (a.cols.counters) K.add(in_batch, len, P.st);
         wave_sync();
+        PNET_PH(3);   // probe: stores, counters
         cur = nxt;
         run = nrun;
     }

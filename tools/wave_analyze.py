@@ -34,7 +34,7 @@ def by(d, key, vals):
 
 
 def report(path):
-    d = decode(np.load(path))
+    d = decode(np.load(path)[:, :4] if np.load(path).shape[1] > 4 else np.load(path))
     dur = d["dur"]
     print(f"== {path}: {len(dur)} waves, duration mean {dur.mean():.1f} us, min {dur.min():.1f}, max {dur.max():.1f}")
     for name, key in [("wave slot", d["slot"]), ("simd", d["simd"]), ("xcc", d["xcc"]),

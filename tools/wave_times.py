@@ -26,7 +26,7 @@ from bench import Shard, WORKLOADS  # noqa: E402
 from libpnet_amd import _lib  # noqa: E402
 
 EXTRA = {"imix": 1 << 22, "udp6_jumbo": 1 << 17}
-SLOTS, WORDS = 16384, 4
+SLOTS, WORDS = 16384, 10
 TICK_US = 0.01   # wall_clock64: 100 MHz
 
 
@@ -112,6 +112,14 @@ def main():
                   flush=True)
             if rep == a.reps - 1:
                 print(f"{'':10s} runs total {runs.sum()} (batch {(sh.n + 63) // 64})", flush=True)
+                clk = t[:, 9].astype(np.float64)
+                if clk.max() > 0:
+                    mhz = clk / np.maximum(dur, 1e-9)            # s_memtime ticks per us
+                    ph = t[:, 4:8].astype(np.float64) / mhz[:, None] / np.maximum(runs, 1)[:, None]
+                    names = ("window/loads", "tail", "parse", "stores")
+                    print(f"{'':10s} per run (us, mean over waves; s_memtime {np.median(mhz):.0f} MHz): " +
+                          "  ".join(f"{nm} {ph[:, i].mean():.2f}" for i, nm in enumerate(names)) +
+                          f"  total {ph.sum(1).mean():.2f} ({dur.mean() / runs.mean():.2f} wall)", flush=True)
                 per = []
                 for x in range(8):
                     m = xcc == x
