@@ -170,28 +170,11 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
 
 // ---- LDS access --------------------------------------------------------------
 
-// Slot addressing. Linear slots hold a frame's window bytes in order. SWZ
-// slots (the mixed kernel's LDS-DMA window, 128 B unpadded) hold logical
-// granule c of frame f at granule position c ^ key, key = f & 7: lanes
-// reading the same frame offset then spread over the banks as the 132-B padded
-// slots do, while each 1-KiB LDS-DMA wave instruction still fills 8 whole slots.
-template <bool SWZ>
-__device__ __forceinline__ int slot_byte(int q, uint32_t key) {
-    return SWZ ? ((((q >> 4) ^ (int)key) << 4) | (q & 15)) : q;
-}
-template <bool SWZ>
-__device__ __forceinline__ int slot_dword(int k, uint32_t key) {   // k <= 32: past the slot wraps to dword 0
-    return SWZ ? (((((k >> 2) ^ (int)key) << 2) | (k & 3)) & 31) : k;
-}
-
 // 16 bytes of a run [p, p+16) of an LDS slot at any alignment, as 4 LE dwords.
-template <bool SWZ = false>
-__device__ __forceinline__ uint4 lds_read16_unaligned(const uint8_t* slot, int p, uint32_t key = 0) {
+__device__ __forceinline__ uint4 lds_read16_unaligned(const uint8_t* slot, int p) {
     const uint32_t* s32 = reinterpret_cast<const uint32_t*>(slot);
     const int q = p >> 2, sh = (p & 3);
-    const uint32_t d0 = s32[slot_dword<SWZ>(q, key)], d1 = s32[slot_dword<SWZ>(q + 1, key)],
-                   d2 = s32[slot_dword<SWZ>(q + 2, key)], d3 = s32[slot_dword<SWZ>(q + 3, key)],
-                   d4 = s32[slot_dword<SWZ>(q + 4, key)];
+    const uint32_t d0 = s32[q], d1 = s32[q + 1], d2 = s32[q + 2], d3 = s32[q + 3], d4 = s32[q + 4];
     uint4 r;
     r.x = __builtin_amdgcn_alignbyte(d1, d0, sh);
     r.y = __builtin_amdgcn_alignbyte(d2, d1, sh);
@@ -215,23 +198,19 @@ struct Parsed {
 // Frame bytes for the parse: the LDS window W holds bytes [0, wlim); anything
 // past it (long IPv6 extension chains, L4 headers behind them) is read from the
 // frame in HBM through G. The IPv4 header and VLAN tags always fit the window.
-template <bool SWZ = false>
-struct FrameBytesT {
-    const uint8_t* S;   // the LDS slot; frame byte p is slot byte sh + p
-    int sh;
-    uint32_t key;       // SWZ slots: the granule swizzle key
-    const uint8_t* G;   // the frame in HBM
+struct FrameBytes {
+    const uint8_t* W;
+    const uint8_t* G;
     int wlim;
-    __device__ __forceinline__ uint32_t near8(int p) const { return S[slot_byte<SWZ>(sh + p, key)]; }
+    __device__ __forceinline__ uint32_t near8(int p) const { return W[p]; }
     __device__ __forceinline__ uint32_t near16(int p) const { return (near8(p) << 8) | near8(p + 1); }
     __device__ __forceinline__ uint32_t near32(int p) const { return (near16(p) << 16) | near16(p + 2); }
     __device__ __forceinline__ uint32_t far8(int p) const {
-        if (p < wlim) return near8(p);
+        if (p < wlim) return W[p];
         return G[p];
     }
     __device__ __forceinline__ uint32_t far16(int p) const { return (far8(p) << 8) | far8(p + 1); }
 };
-using FrameBytes = FrameBytesT<false>;
 
 __device__ __forceinline__ bool is_vlan_tpid(uint32_t et) { return et == 0x8100u || et == 0x88A8u || et == 0x9100u; }
 
@@ -239,8 +218,7 @@ __device__ __forceinline__ bool is_vlan_tpid(uint32_t et) { return et == 0x8100u
 // packetdump.rs:155-217 + ipv4.rs:165-178,226-243 + ipv6.rs:21-137 + vlan.rs:62-72
 // + udp/tcp/icmp layouts and minimum sizes (decorator.rs:593-600) + payload
 // bounds (decorator.rs:713-769). Mirrors oracle_rx_frame_ex.
-template <class FB>
-__device__ __forceinline__ Parsed parse_frame(const FB& F, uint32_t len, uint32_t flags) {
+__device__ __forceinline__ Parsed parse_frame(const FrameBytes& F, uint32_t len, uint32_t flags) {
     Parsed P{};
     uint32_t et;
     int l3;
@@ -413,9 +391,8 @@ __device__ __forceinline__ Parsed parse_frame(const FB& F, uint32_t len, uint32_
 // pad dword, so p3>>2 may equal the dword count). With P(x) = weighted sum of
 // the slot bytes in [4*(p0>>2), x): tA = P(p1) - P(p0), tB = P(p3) - P(p2).
 // One runtime loop over whole dwords (v_sad_u16 each) plus four masked partials.
-template <bool SWZ = false>
 __device__ __forceinline__ void window_sums(const uint8_t* slot, int p0, int p1, int p2, int p3, uint32_t& tA,
-                                            uint32_t& tB, uint32_t key = 0) {
+                                            uint32_t& tB) {
     const uint32_t* s32 = reinterpret_cast<const uint32_t*>(slot);
     const int k0 = p0 >> 2, k1 = p1 >> 2, k2 = p2 >> 2, k3 = p3 >> 2;
     uint32_t acc = 0, c1 = 0, c2 = 0;
@@ -423,14 +400,14 @@ __device__ __forceinline__ void window_sums(const uint8_t* slot, int p0, int p1,
     for (int k = k0; k < k3; ++k) {
         if (k == k1) c1 = acc;
         if (k == k2) c2 = acc;
-        acc = sad(s32[slot_dword<SWZ>(k, key)], acc);
+        acc = sad(s32[k], acc);
     }
     if (k1 >= k3) c1 = acc;
     if (k2 >= k3) c2 = acc;
-    const uint32_t P0 = sad(s32[slot_dword<SWZ>(k0, key)] & first_bytes(p0 & 3), 0u);
-    const uint32_t P1 = sad(s32[slot_dword<SWZ>(k1, key)] & first_bytes(p1 & 3), c1);
-    const uint32_t P2 = sad(s32[slot_dword<SWZ>(k2, key)] & first_bytes(p2 & 3), c2);
-    const uint32_t P3 = sad(s32[slot_dword<SWZ>(k3, key)] & first_bytes(p3 & 3), acc);
+    const uint32_t P0 = sad(s32[k0] & first_bytes(p0 & 3), 0u);
+    const uint32_t P1 = sad(s32[k1] & first_bytes(p1 & 3), c1);
+    const uint32_t P2 = sad(s32[k2] & first_bytes(p2 & 3), c2);
+    const uint32_t P3 = sad(s32[k3] & first_bytes(p3 & 3), acc);
     tA += P1 - P0;
     tB += P3 - P2;
 }
@@ -554,10 +531,9 @@ __device__ __forceinline__ uint64_t opaque_index(uint64_t i) {
     return i;
 }
 
-template <bool SWZ = false>
 __device__ __forceinline__ void store_columns(const pnetgpu_rx_columns& C, uint64_t f0, int lane, bool in_batch,
                                               const Parsed& P, uint32_t ipc, uint32_t l4c, const uint8_t* slot,
-                                              int sh, uint32_t key = 0) {
+                                              int sh) {
     if (!in_batch) return;
     const uint64_t i = opaque_index(f0 + (uint64_t)lane);
     if (C.status) put<uint16_t>(C.status, i, (uint16_t)P.st);
@@ -578,8 +554,8 @@ __device__ __forceinline__ void store_columns(const pnetgpu_rx_columns& C, uint6
         const bool v6ok = (P.st & (PNET_ST_L3_MASK | PNET_ST_L3_MALFORMED)) == PNET_ST_L3_IPV6;
         uint4 sv = make_uint4(0, 0, 0, 0), dv = make_uint4(0, 0, 0, 0);
         if (v6ok) {
-            sv = lds_read16_unaligned<SWZ>(slot, sh + (int)P.l3 + 8, key);
-            dv = lds_read16_unaligned<SWZ>(slot, sh + (int)P.l3 + 24, key);
+            sv = lds_read16_unaligned(slot, sh + (int)P.l3 + 8);
+            dv = lds_read16_unaligned(slot, sh + (int)P.l3 + 24);
         }
         if (C.src_ipv6) reinterpret_cast<uint4*>(C.src_ipv6)[i] = sv;
         if (C.dst_ipv6) reinterpret_cast<uint4*>(C.dst_ipv6)[i] = dv;
@@ -593,9 +569,8 @@ __device__ __forceinline__ void store_columns(const pnetgpu_rx_columns& C, uint6
 // tcp.rs:55-71, icmp.rs:221-232,303-314 (getter bit extraction:
 // pnet_macros/src/decorator.rs:1563-1670). Mirrors oracle_rx_frame_ex.
 // `l3mode`: PNETGPU_RX_L3 batch (no Ethernet view).
-template <class FB>
 __device__ __forceinline__ void store_field_columns(const pnetgpu_rx_columns& C, uint64_t fi, const Parsed& P,
-                                                 const FB& F, bool l3mode) {
+                                                 const FrameBytes& F, bool l3mode) {
     const uint64_t i = opaque_index(fi);
     const uint32_t st = P.st;
     const bool eth = !l3mode && !(st & (PNET_ST_ETH_MALFORMED | PNET_ST_DESC_INVALID));

@@ -16,11 +16,9 @@ namespace {
 // ============================================================================
 // rx_kernel: generic (descriptor mode, any alignment, any length).
 // ============================================================================
-template <int NW, bool PAD = true>
+template <int NW>
 struct WaveLds {
-    // +4 B pad: conflict-free parse reads; unpadded 128-B slots (PAD false) are
-    // granule-swizzled instead (slot_byte<true>, rx_mixed_pf_kernel)
-    static constexpr int kSlot = NW * 16 + (PAD ? 4 : 0);
+    static constexpr int kSlot = NW * 16 + 4;   // +4 B pad: conflict-free parse reads
     uint8_t win[kWave * kSlot];
     uint64_t base[kWave];     // aligned byte offset of granule 0 of each frame
     uint32_t end[kWave];      // window granules to load; then slot-relative frame end
@@ -61,10 +59,10 @@ __device__ __forceinline__ uint32_t lane_range_sum(const uint8_t* fb, int lo, in
 // LDS counter instead of a fixed stride of the list, and the list holds the
 // frames needing more than one round first, so mixed sizes balance across the
 // groups (the caller sets L.qhead = kWave / G).
-template <int NW, int G, int U, bool NT, bool UNI, bool DYN, bool PAD>
-__device__ __forceinline__ void tail_sums(const uint8_t* data, WaveLds<NW, PAD>& L, int lane, int count) {
+template <int NW, int G, int U, bool NT, bool UNI, bool DYN>
+__device__ __forceinline__ void tail_sums(const uint8_t* data, WaveLds<NW>& L, int lane, int count) {
     constexpr int kGroups = kWave / G;
-    constexpr int kSlot = WaveLds<NW, PAD>::kSlot;
+    constexpr int kSlot = WaveLds<NW>::kSlot;
     constexpr uint32_t c_first = UNI ? 0u : (uint32_t)NW;
     static_assert(!UNI || G * U >= NW, "the first round must cover the window");
     const int j = lane % G;
@@ -257,7 +255,7 @@ __global__ __launch_bounds__(kBlock, NW < 8 ? 5 : 4) void rx_kernel(RxArgs a) {
             }
             if (DYN && lane == 0) L.qhead = kWave / G;
             wave_sync();
-            tail_sums<NW, G, U, NT, (PASS != 0), DYN, true>(a.data, L, lane, __popcll(tmask));
+            tail_sums<NW, G, U, NT, (PASS != 0), DYN>(a.data, L, lane, __popcll(tmask));
         }
         wave_sync();
 
@@ -266,7 +264,7 @@ __global__ __launch_bounds__(kBlock, NW < 8 ? 5 : 4) void rx_kernel(RxArgs a) {
         Parsed P{};
         if (desc_bad) P.st = PNET_ST_DESC_INVALID;
         else if (in_batch)
-            P = parse_frame(FrameBytes{slot, sh, 0u, a.data + off, kWin - sh}, len, EXT ? a.flags : 0u);
+            P = parse_frame(FrameBytes{slot + sh, a.data + off, kWin - sh}, len, EXT ? a.flags : 0u);
         // A (<= 97 B into the frame) lies in the window unless the window is
         // shorter than 8 granules (IPv4 options past it); B may run past it
         const int p0 = P.a_lo + sh, p1 = P.a_hi + sh, p2 = P.b_lo + sh, p3 = P.b_hi + sh;
@@ -289,184 +287,12 @@ __global__ __launch_bounds__(kBlock, NW < 8 ? 5 : 4) void rx_kernel(RxArgs a) {
         store_columns(a.cols, f0, lane, in_batch, P, ipc, l4c, slot, sh);
 #ifndef PNET_NO_FIELD_COLUMNS   // A/B: the header-field stores compiled out
         if (EXT && a.field_cols && in_batch)   // header-field columns: EXT instantiations only
-            store_field_columns(a.cols, f0 + lane, P, FrameBytes{slot, sh, 0u, a.data + off, kWin - sh}, EXT && a.l3mode);
+            store_field_columns(a.cols, f0 + lane, P, FrameBytes{slot + sh, a.data + off, kWin - sh}, EXT && a.l3mode);
 #endif
         if (a.cols.counters) K.add(in_batch && !desc_bad, len, P.st);
         wave_sync();   // slots and lists are rewritten by the next run
         PNET_PH(3);   // probe: stores, counters
         run = nrun;
-    }
-    if (a.cols.counters) K.flush(a.cols.counters, blk_ctr, wv, lane);
-    PNET_WT_END((uint64_t)blockIdx.x * kWavesPerBlock + wv);
-}
-
-// rx_mixed_pf_kernel: the mixed shape (descriptor batches) with each run's
-// window prefetched a run ahead. The window phase of rx_kernel<..., PASS 0>
-// waits one full memory round trip per run (5.0 of 20 us per IMIX run on
-// MI355X, tools/wave_times.py phase clocks). Here the next run's window
-// granules go out as eight 1-KiB LDS-DMA wave loads (global_load_lds_dwordx4:
-// no VGPRs) as soon as the current run's slots are no longer read, and land
-// while the current run's stores and the next run's tail phase proceed. An
-// LDS-DMA instruction fills 1 KiB of LDS linearly (8 unpadded 128-B slots), so
-// the slots are granule-swizzled instead of padded: lane L of instruction i
-// loads logical granule (L & 7) ^ (frame & 7) of frame 8 i + L / 8, and every
-// slot read goes through slot_byte<true> / slot_dword<true> (key = frame & 7).
-// Granules past a frame's span are zeroed with ordinary LDS stores.
-__device__ __forceinline__ void glds16(const void* src, uint32_t lds_base) {
-    uint32_t keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep)
-                 : "v"(src), "s"(lds_base)
-                 : "memory");
-}
-typedef __attribute__((address_space(3))) void* lds_void_ptr;
-
-template <int G, int U, bool DYN, bool EXT, bool TX>
-__global__ __launch_bounds__(kBlock, 4) void rx_mixed_pf_kernel(RxArgs a) {
-    constexpr int NW = 8, kSlot = 128, kWin = 128;
-    static_assert(WaveLds<NW, false>::kSlot == kSlot, "unpadded slots");
-    __shared__ __attribute__((aligned(16))) WaveLds<NW, false> lds_all[kWavesPerBlock];
-    __shared__ uint64_t blk_ctr[kWavesPerBlock][PNETGPU_NCOUNTERS];
-
-    const int lane = threadIdx.x & (kWave - 1);
-    const int wv = threadIdx.x / kWave;
-    WaveLds<NW, false>& L = lds_all[wv];
-    uint8_t* slot = L.win + lane * kSlot;
-    const uint32_t key = (uint32_t)lane & 7u;
-    const uint32_t win0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_void_ptr)L.win);
-    Counters K;
-
-    const uint64_t wave_stride = (uint64_t)gridDim.x * kWavesPerBlock;
-    uint64_t d_off = 0;
-    uint32_t d_len = 0;
-    auto fetch_desc = [&](uint64_t r) {
-        const uint64_t fr = r * kWave + lane;
-        if (!a.stride && r < a.nruns && fr < a.n) {
-            if (a.desc_compact) {   // wave-uniform
-                d_off = reinterpret_cast<const uint32_t*>(a.offsets)[fr];
-                d_len = reinterpret_cast<const uint16_t*>(a.lengths)[fr];
-            } else {
-                d_off = a.offsets[fr];
-                d_len = a.lengths[fr];
-            }
-        }
-    };
-    struct Fr {
-        uint64_t off;
-        uint32_t len;
-        bool in_batch, desc_bad;
-    };
-    // this lane's frame of run r (from d_off / d_len, fetched a run ahead)
-    auto frame_of = [&](uint64_t r) {
-        Fr x{0, 0, false, false};
-        const uint64_t f = r * kWave + lane;
-        x.in_batch = r < a.nruns && f < a.n;
-        if (x.in_batch) {
-            x.off = (a.stride ? a.first + f * a.stride : d_off) + a.delta;
-            x.len = a.stride ? a.frame_len : d_len;
-            x.desc_bad = x.off > a.limit || (uint64_t)x.len > a.limit - x.off;
-            if (x.desc_bad) {   // nothing is loaded for it (a wild offset must not be dereferenced)
-                x.off = 0;
-                x.len = 0;
-            }
-        }
-        return x;
-    };
-    // the run's window: eight 1-KiB LDS-DMA wave loads into the swizzled slots
-    auto issue_window = [&](const Fr& x) {
-        const uint32_t sh = (uint32_t)(x.off & 15);
-        const uint32_t span = (sh + x.len + 15u) >> 4;
-        L.base[lane] = x.off - sh;
-        L.end[lane] = span < (uint32_t)NW ? span : (uint32_t)NW;
-        wave_sync();
-#pragma unroll
-        for (int i = 0; i < NW; ++i) {
-            const int fl = 8 * i + (lane >> 3);
-            const uint32_t c = (uint32_t)((lane & 7) ^ (fl & 7));
-            if (c < L.end[fl])
-                glds16(a.data + L.base[fl] + 16u * c, win0 + 1024u * i);
-            else
-                *reinterpret_cast<uint4*>(L.win + 1024 * i + 16 * lane) = make_uint4(0, 0, 0, 0);
-        }
-    };
-
-    PNET_WT_BEGIN;
-    uint32_t run_count = 0;
-    (void)run_count;
-    RunQueue q(a.sched, a.nruns, (uint64_t)blockIdx.x * kWavesPerBlock + wv, wave_stride);
-    uint64_t run = q.take();
-    fetch_desc(run);
-    Fr cur = frame_of(run);
-    if (run < a.nruns) issue_window(cur);
-    uint64_t nrun = q.take();
-    fetch_desc(nrun);
-    while (run < a.nruns) {
-        PNET_WT_RUN;
-        PNET_PRIO(run_count++);
-        const uint64_t f0 = run * kWave;
-        const bool in_batch = cur.in_batch, desc_bad = cur.desc_bad;
-        const uint64_t off = cur.off;
-        const uint32_t len = cur.len;
-        const int sh = (int)(off & 15);
-        const uint64_t base = off - (uint64_t)sh;
-        const uint32_t fend = (uint32_t)sh + len;
-        const uint32_t span = (fend + 15u) >> 4;
-        const bool long_frame = fend > (uint32_t)kWin;
-        PNET_PH(0);
-
-        // ---- speculative tail (as rx_kernel PASS 0), while the window lands ----
-        const uint64_t tmask = __ballot(long_frame);
-        if (tmask) {
-            const bool big = DYN && long_frame && span > (uint32_t)(NW + G * U);
-            const uint64_t bmask = __ballot(big);
-            const uint64_t below = (1ull << lane) - 1ull;
-            if (long_frame) {
-                const int pos = big ? __popcll(bmask & below) : __popcll(bmask) + __popcll(tmask & ~bmask & below);
-                L.list[pos] = (uint8_t)lane;
-                L.end[lane] = fend;
-            }
-            if (DYN && lane == 0) L.qhead = kWave / G;
-            wave_sync();
-            tail_sums<NW, G, U, false, false, DYN, false>(a.data, L, lane, __popcll(tmask));
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the run's window LDS-DMA has landed
-        wave_sync();
-        PNET_PH(1);
-
-        // ---- parse + window sums from the swizzled slot ---------------------
-        Parsed P{};
-        const FrameBytesT<true> F{slot, sh, key, a.data + off, kWin - sh};
-        if (desc_bad) P.st = PNET_ST_DESC_INVALID;
-        else if (in_batch)
-            P = parse_frame(F, len, EXT ? a.flags : 0u);
-        const int p0 = P.a_lo + sh, p1 = P.a_hi + sh, p2 = P.b_lo + sh, p3 = P.b_hi + sh;
-        uint32_t tA = 0, tB = 0;
-        window_sums<true>(slot, p0, min(p1, kWin), min(p2, kWin), min(p3, kWin), tA, tB, key);
-        if (P.l4do && p3 > kWin) {
-            tB += L.tail[lane];
-            const uint8_t* fb = a.data + base;
-            if (p2 > kWin) tB -= lane_range_sum(fb, kWin, p2);
-            if ((uint32_t)p3 < fend) tB -= lane_range_sum(fb, p3, (int)fend);
-        }
-        uint32_t ipc = 0, l4c = 0;
-        finalize(P, tA, tB, (off & 1) != 0, ipc, l4c);
-        PNET_PH(2);
-        if (TX && in_batch && !desc_bad) tx_write(const_cast<uint8_t*>(a.data) + off, P, ipc, l4c);
-        store_columns<true>(a.cols, f0, lane, in_batch, P, ipc, l4c, slot, sh, key);
-#ifndef PNET_NO_FIELD_COLUMNS
-        if (EXT && a.field_cols && in_batch) store_field_columns(a.cols, f0 + lane, P, F, EXT && a.l3mode);
-#endif
-        if (a.cols.counters) K.add(in_batch && !desc_bad, len, P.st);
-        wave_sync();   // every slot read of this run is done: the next window may land
-
-        // ---- the next run's window goes out now ------------------------------
-        cur = frame_of(nrun);
-        if (nrun < a.nruns) issue_window(cur);
-        const uint64_t nnrun = q.take();
-        fetch_desc(nnrun);
-        PNET_PH(3);
-        run = nrun;
-        nrun = nnrun;
     }
     if (a.cols.counters) K.flush(a.cols.counters, blk_ctr, wv, lane);
     PNET_WT_END((uint64_t)blockIdx.x * kWavesPerBlock + wv);

@@ -107,16 +107,7 @@ static int resident_blocks(const void* fn, int block_threads) {
 #ifndef PNET_MIXED_NW
 #define PNET_MIXED_NW 8
 #endif
-// PNET_MIXED_PF: descriptor batches take rx_mixed_pf_kernel (the window
-// prefetched a run ahead by LDS-DMA) with the mixed tail shape G=4, U=8, DYN
-#ifndef PNET_MIXED_PF
-#define PNET_MIXED_PF 0
-#endif
-#if PNET_MIXED_PF
-#define PNET_MIXED_FN(EXT, TX) rx_mixed_pf_kernel<4, 8, true, EXT, TX>
-#else
 #define PNET_MIXED_FN(EXT, TX) rx_kernel<PNET_MIXED_NW, PNET_MIXED_CFG, EXT, TX>
-#endif
 #define PNET_JUMBO_FN(EXT, TX) rx_kernel<8, PNET_JUMBO_CFG, EXT, TX>
 
 template <bool EXT, bool TX>
@@ -177,11 +168,7 @@ int rx_waves_per_block(int) { return kWavesPerBlock; }
 const char* rx_kernel_name(int kind, bool ext, bool tx) {
 #define PNET_NAMES(HEAD)                                                                       \
     {HEAD ", false, false>", HEAD ", false, true>", HEAD ", true, false>", HEAD ", true, true>"}
-#if PNET_MIXED_PF
-    static const char* const mixed[4] = PNET_NAMES("rx_mixed_pf_kernel<4, 8, true");
-#else
     static const char* const mixed[4] = PNET_NAMES("rx_kernel<" PNET_STR(PNET_MIXED_NW) ", " PNET_STR(PNET_MIXED_CFG));
-#endif
     static const char* const mtu[4] = PNET_NAMES("rx_kernel<8, " PNET_STR(PNET_MTU_CFG));
     static const char* const jumbo[4] = PNET_NAMES("rx_kernel<8, " PNET_STR(PNET_JUMBO_CFG));
     static const char* const small[4] = {"rx_small_kernel<false, false>", "rx_small_kernel<true, false>",

@@ -230,7 +230,7 @@ __global__ __launch_bounds__(kBlock, PNET_SMALL_WAVES) void rx_small_kernel(RxAr
 #endif
             if (slow) {
                 // flags are 0 here and the frame (<= 64 B) is entirely in its slot
-                P = parse_frame(FrameBytes{slot, 0, 0u, slot, 64}, len, 0u);
+                P = parse_frame(FrameBytes{slot, slot, 64}, len, 0u);
                 uint32_t tA = 0, tB = 0;
                 window_sums(slot, P.a_lo, P.a_hi, P.b_lo, P.b_hi, tA, tB);
                 finalize(P, tA, tB, false, ipc, l4c);
@@ -261,7 +261,7 @@ __global__ __launch_bounds__(kBlock, PNET_SMALL_WAVES) void rx_small_kernel(RxAr
         store_columns(a.cols, f0, lane, in_batch, P, ipc, l4c, slot, 0);
 #ifndef PNET_NO_FIELD_COLUMNS   // A/B: the header-field stores compiled out
         if (FIELDS && a.field_cols && in_batch)
-            store_field_columns(a.cols, f0 + lane, P, FrameBytes{slot, 0, 0u, slot, 64}, false);
+            store_field_columns(a.cols, f0 + lane, P, FrameBytes{slot, slot, 64}, false);
 #endif
         if (a.cols.counters) K.add(in_batch, len, P.st);
         wave_sync();
