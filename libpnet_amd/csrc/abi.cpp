@@ -339,7 +339,8 @@ static int slices_common(pnetgpu_ctx* ctx, const uint8_t* data, uint64_t data_by
     if (kenv) run = kenv[0] == 'r' ? true : kenv[0] == 'g' ? false : run;
     const uint64_t per_block = run ? kBlock : kBlock / 16;
     const int blocks = slice_grid(ctx, run ? 1 : 2, pseudo, extra_offsets != nullptr, (n + per_block - 1) / per_block);
-    if (run && (rc = plan_sched(ctx, (n + 63) / 64, (uint64_t)blocks * 4, &a.sched))) return rc;
+    // scheduled units: slice_run_kernel's runs of 64 slices, slice_kernel's 4
+    if ((rc = plan_sched(ctx, run ? (n + 63) / 64 : (n + 3) / 4, (uint64_t)blocks * 4, &a.sched))) return rc;
     if (const int e = pnetgpu::launch_slices(a, pseudo, run, blocks, static_cast<hipStream_t>(stream))) {
         pnetgpu::set_last_hip_error(e);
         return PNETGPU_EHIP;
@@ -378,10 +379,10 @@ int pnetgpu_checksum_slices_strided(pnetgpu_ctx* ctx, const uint8_t* data, uint6
     const int blocks = slice_grid(ctx, small ? 0 : run ? 1 : 2, small ? pnetgpu::strided_variant(slice_len, stride) : 0, false,
                                   (n + per_block - 1) / per_block);
     // scheduled units: slice_strided_kernel's blocks of R runs (R as the kernel
-    // computes it), slice_run_kernel's runs
-    const uint64_t runs_per_unit = small ? (stride ? std::max(1u, std::min(16u, 4096u / (64u * stride))) : 16u) : 1u;
-    if ((small || run) && (rc = plan_sched(ctx, (n + 64 * runs_per_unit - 1) / (64 * runs_per_unit),
-                                           (uint64_t)blocks * 4, &a.sched)))
+    // computes it), slice_run_kernel's runs, slice_kernel's 4 slices
+    const uint64_t slices_per_unit =
+        small ? 64u * (stride ? std::max(1u, std::min(16u, 4096u / (64u * stride))) : 16u) : run ? 64u : 4u;
+    if ((rc = plan_sched(ctx, (n + slices_per_unit - 1) / slices_per_unit, (uint64_t)blocks * 4, &a.sched)))
         return rc;
     const int e = small ? pnetgpu::launch_slices_strided_small(a, blocks, static_cast<hipStream_t>(stream))
                         : pnetgpu::launch_slices(a, 0, run, blocks, static_cast<hipStream_t>(stream));
@@ -410,7 +411,7 @@ int pnetgpu_checksum_slices_compact(pnetgpu_ctx* ctx, const uint8_t* data, uint6
     if (kenv) run = kenv[0] == 'r' ? true : kenv[0] == 'g' ? false : run;
     const uint64_t per_block = run ? kBlock : kBlock / 16;
     const int blocks = slice_grid(ctx, run ? 1 : 2, 0, false, (n + per_block - 1) / per_block);
-    if (run && (rc = plan_sched(ctx, (n + 63) / 64, (uint64_t)blocks * 4, &a.sched))) return rc;
+    if ((rc = plan_sched(ctx, run ? (n + 63) / 64 : (n + 3) / 4, (uint64_t)blocks * 4, &a.sched))) return rc;
     if (const int e = pnetgpu::launch_slices(a, 0, run, blocks, static_cast<hipStream_t>(stream))) return pnetgpu::hip_fail((hipError_t)e);
     return PNETGPU_OK;
 }

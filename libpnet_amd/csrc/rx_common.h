@@ -85,22 +85,28 @@ struct WaveTimer {
 #define PNET_PH(i)
 #endif
 
-#ifdef PNET_PRIO_ROTATE
-// A/B probe: the wave's issue priority rotates with its run count, phased by
-// its hardware wave slot, so no wave of a SIMD keeps the age-order lead
-__device__ __forceinline__ void rotate_prio(uint32_t runs) {
+// The wave's issue priority rotated by a step count, phased by its hardware
+// wave slot, so no wave of a SIMD keeps the age-order lead the arbiter gives
+// the oldest (tools/wave_times.py: with fixed priorities the 4th wave of a
+// SIMD ran 11 % longer than the 1st on the same work). Used where a launch has
+// too few runs per wave to balance by claims (RunSched): the MTU shape.
+__device__ __forceinline__ void rotate_prio(uint32_t step) {
     uint32_t hwid;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid));
-    switch ((runs + hwid) & 3u) {
+    switch ((step + hwid) & 3u) {
     case 0: __builtin_amdgcn_s_setprio(0); break;
     case 1: __builtin_amdgcn_s_setprio(1); break;
     case 2: __builtin_amdgcn_s_setprio(2); break;
     default: __builtin_amdgcn_s_setprio(3);
     }
 }
+#ifdef PNET_PRIO_ROTATE   // A/B: every kernel rotates per run
 #define PNET_PRIO(k) rotate_prio(k)
 #else
 #define PNET_PRIO(k)
+#endif
+#ifndef PNET_ROTATE_MTU
+#define PNET_ROTATE_MTU 1   // the MTU shape rotates per run (0: A/B without)
 #endif
 
 // The runs one wave processes (RxArgs::sched): its grid-stride share of

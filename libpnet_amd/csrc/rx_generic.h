@@ -181,6 +181,11 @@ __global__ __launch_bounds__(kBlock, NW < 8 ? 5 : 4) void rx_kernel(RxArgs a) {
     while (run < a.nruns) {
         PNET_WT_RUN;
         PNET_PRIO(run_count++);
+        // the MTU shape (4 runs per wave at 2^20 frames: too few to balance by
+        // claims) rotates its issue priority per run: 1500-B batches -1.5 %,
+        // same box, four interleaved rounds (profiles/r03/claims/ab_rotate.txt);
+        // jumbo frames rotated per frame measured even, not done
+        if (PNET_ROTATE_MTU && PASS == 1) rotate_prio(run_count++);
         const uint64_t nrun = q.take();   // the next run (its claim went out a run ago)
         // ---- 1. descriptor -------------------------------------------------
         const uint64_t f0 = run * kWave;

@@ -92,14 +92,19 @@ __device__ __forceinline__ uint32_t group_range_sum(const uint8_t* data, uint64_
 // EXTRA: the *_checksum_adv form with an extra_data slice (util.rs:109-114).
 template <int PSEUDO, bool EXTRA>
 __global__ __launch_bounds__(kBlock) void slice_kernel(SliceArgs a) {
-    constexpr int G = 16;
+    constexpr int G = 16, kPerWave = kWave / G;
     const int lane = threadIdx.x & (kWave - 1);
     const int j = lane % G;
-    const uint64_t gid = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) / G;
-    const uint64_t ngroups = (uint64_t)gridDim.x * kBlock / G;
-    // groups are 16-lane aligned, so every shuffle stays inside one group, whose
-    // lanes share i (and therefore control flow)
-    for (uint64_t i = gid; i < a.n; i += ngroups) {
+    // a wave's unit is 4 consecutive slices, one per 16-lane group: its
+    // grid-stride share, then claimed units (RunSched). Groups are 16-lane
+    // aligned, so every shuffle stays inside one group, whose lanes share i
+    // (and therefore control flow)
+    const uint64_t nunits = (a.n + kPerWave - 1) / kPerWave;
+    RunQueue q(a.sched, nunits, ((uint64_t)blockIdx.x * kBlock + threadIdx.x) / kWave,
+               (uint64_t)gridDim.x * kWavesPerBlock);
+    for (uint64_t u = q.take(); u < nunits; u = q.take()) {
+        const uint64_t i = u * kPerWave + (uint64_t)(lane / G);
+        if (i >= a.n) continue;
         uint64_t off;
         uint32_t len, skip;
         if (a.strided) {            // wave-uniform branches: strided, compact or full descriptors
