@@ -484,6 +484,8 @@ def refshapes_block(steps, warmup, device):
                       of packetdump's chain), packet_benchmarks.rs:63-71
     Slices are packed back to back, one (u64 offset, u32 length, u32 skipword)
     descriptor each; algorithmic bytes = slice bytes + 16 B descriptor + 2 B result.
+    `compact`: the same slices through pnetgpu_checksum_slices_compact (8-B
+    pnetgpu_slice_desc records; algorithmic bytes = slice + 8 B + 2 B result).
     `strided`: the same slices through pnetgpu_checksum_slices_strided (no
     descriptor arrays; algorithmic bytes = slice + 2 B result)."""
     from oracle import coracle  # CPU baseline legs only
@@ -510,6 +512,17 @@ def refshapes_block(steps, warmup, device):
             reps, el = _timed_reps(lambda r: coracle.checksum_slices_reps(buf, offs[:k], lens[:k], skips[:k],
                                                                           cpu_out[:k], nthreads=nt, reps=r), 1.0)
             cpu[label] = round(k * reps / el / 1e6, 1)
+        # the same slices through 8-B compact descriptors (pnetgpu_checksum_slices_compact)
+        dc = lp.slice_descriptors(offs, lens, skips, device=device)
+        ms_c = time_launches(lambda s: res.__setitem__("c", lp.checksum_slices_compact(d, dc, stream=s)),
+                             steps, warmup, stream)
+        got_c = res["c"].cpu().numpy().view(np.uint16)
+        alg_c = n * (size + 8 + 2)
+        compact = {"kernel_avg_ms": round(ms_c, 4), "mslices_s": round(n / (ms_c * 1e-3) / 1e6, 1),
+                   "achieved_gbs": round(alg_c / (ms_c * 1e-3) / 1e9, 1),
+                   "frac": round(alg_c / (ms_c * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                   "parity": bool((got_c == want).all()), "alg_bytes_per_slice": size + 8 + 2}
+        del dc
         # the same slices without descriptor arrays (pnetgpu_checksum_slices_strided)
         ms_st = time_launches(lambda s: res.__setitem__("s", lp.checksum_slices_strided(d, n, size, size, 5, stream=s)),
                               steps, warmup, stream)
@@ -525,7 +538,7 @@ def refshapes_block(steps, warmup, device):
                      "frac": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                      "parity": bool((got == want).all()), "expected": int(want),
                      "cpu_port_1core_mslices_s": cpu["1core"], "cpu_port_all_mslices_s": cpu["all"],
-                     "strided": strided}
+                     "compact": compact, "strided": strided}
         del d, do, dl, ds
     # ipv4_parsing: the captured frame replicated at a 64-B stride (the small kernel)
     n = 1 << 24
