@@ -893,3 +893,45 @@ def test_dense_runs_of_packed_slices(seed, span, monkeypatch):
             o, ln = int(rec_off[i]), int(rec_len[i])
             assert got[i] == ofn(bytes(buf[o:o + ln]), int(skips[i]), b"", bytes(a[i, :h]), bytes(a[i, h:]),
                                  int(protos[i])), (alen, i)
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_runs_of_small_slices_vs_oracle(seed, monkeypatch):
+    """slice_run_kernel on runs whose 64 slices are all small (each summed by its
+    own lane): short slices at every alignment with the skipped word inside /
+    straddling / past the slice, empty and out-of-bounds descriptors, batch
+    sizes giving an odd run count with a ragged last run, a long slice every few
+    hundred slices (its run takes the group path), and packed 64-B runs (dense)
+    between them; 16-B and compact descriptors, against the oracle. (Written
+    for a two-runs-at-once variant, measured slower and not kept:
+    profiles/r03/slices/ab_run_pairs.txt.)"""
+    monkeypatch.setenv("PNETGPU_SLICE_KERNEL", "run")
+    rng = np.random.default_rng(900 + seed)
+    n = 64 * (201 + 2 * seed) + 13 + seed
+    buf = rng.integers(0, 256, 1 << 21, dtype=np.uint8)
+    lens = rng.integers(0, 50, n).astype(np.uint32)
+    lens[rng.random(n) < 0.02] = 0
+    offs = rng.integers(0, buf.size - 6000, n).astype(np.uint64)
+    if seed != 2:                                       # seed 2: every run qualifies
+        big = rng.choice(n, n // 400, replace=False)
+        lens[big] = rng.integers(70, 5000, big.size)
+    r = 64 * (30 + seed)                                # two packed 64-B runs: dense, not paired
+    offs[r:r + 128] = 4096 + 64 * np.arange(128, dtype=np.uint64)
+    lens[r:r + 128] = 64
+    skips = np.where(rng.random(n) < 0.7, rng.integers(0, 26, n), rng.integers(0, 3000, n)).astype(np.uint32)
+    bad = rng.choice(n, 30, replace=False)
+    offs[bad[:15]] = buf.size + rng.integers(0, 1000, 15)
+    lens[bad[15:]] = (buf.size - offs[bad[15:]] + rng.integers(1, 40, 15)).astype(np.uint32)
+    rec_off = np.where(offs > buf.size, 0, offs)
+    rec_len = np.where((offs > buf.size) | (offs + lens > buf.size), 0, lens).astype(np.uint32)
+    want = coracle.checksum_slices(buf, rec_off, rec_len, skips)
+    d = to_dev(buf)
+    got = lp.checksum_slices(d, to_dev(offs.astype(np.int64)), to_dev(lens.astype(np.int32)),
+                             to_dev(skips.astype(np.int32))).cpu().numpy().view(np.uint16)
+    assert np.array_equal(got, want)
+    co, cl, cs = offs, np.minimum(lens, 0xFFFF), np.minimum(skips, 0xFFFF)   # compact: u32 offset, u16 length
+    desc = lp.slice_descriptors(co, cl, cs, device=DEV)
+    got = lp.checksum_slices_compact(d, desc).cpu().numpy().view(np.uint16)
+    c_len = np.where((co > buf.size) | (co + cl > buf.size), 0, cl).astype(np.uint32)
+    want_c = coracle.checksum_slices(buf, np.where(co > buf.size, 0, co), c_len, cs.astype(np.uint32))
+    assert np.array_equal(got, want_c)
