@@ -9,6 +9,7 @@
 #include "pnetgpu.h"
 #include "rx_internal.h"
 #include "rx_common.h"
+#include "rx_small.h"   // small_fast (short runs)
 
 namespace pnetgpu {
 namespace {
@@ -137,6 +138,9 @@ __device__ __forceinline__ void tail_sums(const uint8_t* data, WaveLds<NW>& L, i
 // EXT: batch flags may be non-zero (VLAN / IPv6 extension dispatch) or
 // header-field columns may be requested; the plain instantiation compiles the
 // parse without those branches (half the code, SGPR spills 118 -> 14, IMIX -2 %).
+#ifndef PNET_SHORT_RUNS
+#define PNET_SHORT_RUNS 1   // A/B: short-run fast path in the mixed shape
+#endif
 template <int NW, int G, int U, bool NT, int PASS, bool DYN, bool EXT, bool TX>
 __global__ __launch_bounds__(kBlock, NW < 8 ? 5 : 4) void rx_kernel(RxArgs a) {
     // the window must hold every field the parse reads near (Ethernet + 2 VLAN
@@ -145,6 +149,10 @@ __global__ __launch_bounds__(kBlock, NW < 8 ? 5 : 4) void rx_kernel(RxArgs a) {
     static_assert(G == 2 || G == 4 || G == 8 || G == 16 || G == 32 || G == 64, "tail group");
     constexpr int kSlot = WaveLds<NW>::kSlot;
     constexpr int kWin = NW * 16;
+    // runs of short aligned frames take the small kernel's fast path (the
+    // mixed shape's plain instantiation: no dispatch flags, header-field
+    // columns or TX)
+    constexpr bool kShortRuns = PNET_SHORT_RUNS && PASS == 0 && DYN && !EXT && !TX;
 
     __shared__ WaveLds<NW> lds_all[kWavesPerBlock];
     __shared__ uint64_t blk_ctr[kWavesPerBlock][PNETGPU_NCOUNTERS];
@@ -216,6 +224,52 @@ __global__ __launch_bounds__(kBlock, NW < 8 ? 5 : 4) void rx_kernel(RxArgs a) {
         L.base[lane] = base;
         L.end[lane] = span < (uint32_t)NW ? span : (uint32_t)NW;   // granules to load into the window
         wave_sync();
+
+        // ---- short run: every frame 16-B aligned and at most 64 B ----------
+        // (descriptor batches of minimum-size frames: the AF_PACKET / ring
+        // hand-off of 64-B traffic). Four granule loads per frame instead of
+        // NW, no tail phase, and the small kernel's register fast path
+        // (small_fast: compile-time field positions) in place of parse_frame
+        // for IPv4/IHL-5 frames; the rest parse from the slot as usual.
+        if constexpr (kShortRuns) {
+            if (__ballot(in_batch && !desc_bad && (sh != 0 || len > 64u)) == 0ull) {
+                uint4 g[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int q = i * kWave + lane;
+                    const int fl = q >> 2, c = q & 3;
+                    g[i] = make_uint4(0, 0, 0, 0);
+                    if ((uint32_t)c < L.end[fl]) g[i] = load16(a.data + L.base[fl] + 16u * c);
+                }
+                fetch_desc(nrun);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int q = i * kWave + lane;
+                    uint32_t* dst = reinterpret_cast<uint32_t*>(L.win + (q >> 2) * kSlot + 16 * (q & 3));
+                    dst[0] = g[i].x; dst[1] = g[i].y; dst[2] = g[i].z; dst[3] = g[i].w;
+                }
+                wave_sync();
+                uint32_t w[16];
+#pragma unroll
+                for (int k = 0; k < 16; ++k) w[k] = reinterpret_cast<const uint32_t*>(slot)[k];
+                Parsed P{};
+                uint32_t ipc = 0, l4c = 0;
+                if (desc_bad) {
+                    P.st = PNET_ST_DESC_INVALID;
+                } else if (in_batch && small_fast(w, len, P, ipc, l4c)) {
+                    // IPv6 / IPv4 options: the frame lies whole in its slot (flags are 0)
+                    P = parse_frame(FrameBytes{slot, slot, 64}, len, 0u);
+                    uint32_t tA = 0, tB = 0;
+                    window_sums(slot, P.a_lo, P.a_hi, P.b_lo, P.b_hi, tA, tB);
+                    finalize(P, tA, tB, false, ipc, l4c);
+                }
+                store_columns(a.cols, f0, lane, in_batch, P, ipc, l4c, slot, 0);
+                if (a.cols.counters) K.add(in_batch && !desc_bad, len, P.st);
+                wave_sync();   // slots are rewritten by the next run
+                run = nrun;
+                continue;
+            }
+        }
 
         // ---- 2. window: NW*64 granule loads, all in flight before any store --
         if (PASS != 1) {

@@ -12,7 +12,7 @@ import pytest
 import torch
 
 import libpnet_amd as lp
-from libpnet_amd.engine import ALL_COLUMNS, COLUMNS
+from libpnet_amd.engine import ALL_COLUMNS, COLUMNS, RECORD_COLUMNS
 from oracle import coracle, pyoracle
 from tests import framegen, kats
 
@@ -935,3 +935,36 @@ def test_runs_of_small_slices_vs_oracle(seed, monkeypatch):
     c_len = np.where((co > buf.size) | (co + cl > buf.size), 0, cl).astype(np.uint32)
     want_c = coracle.checksum_slices(buf, np.where(co > buf.size, 0, co), c_len, cs.astype(np.uint32))
     assert np.array_equal(got, want_c)
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_descriptor_runs_of_short_aligned_frames(seed):
+    """The mixed kernel's short-run path (every frame of a run 16-B aligned and
+    at most 64 B: the small kernel's register fast path over descriptors):
+    random UDP/TCP/ICMP/IPv6 frames of 0-64 B, the <= 64-B edge frames (IHL
+    0-15, short L4, IPv6), a ragged last run; then the same batch with a few
+    frames moved off alignment, one 65-B frame and invalid descriptors (their
+    runs take the generic parse). Every record column and the counters equal
+    the oracle's."""
+    rng = np.random.default_rng(1300 + seed)
+    edge = [f for f in framegen.edge_frames(rng) if len(f) <= 64]
+    frames = framegen.random_frames(rng, 64 * 90 + 37, min_len=0, max_len=64)
+    frames[100:100 + len(edge)] = edge
+    buf, offs, lens = framegen.pack(frames, align=16)
+    rec = oracle_desc(buf, offs, lens)
+    res = run_desc(buf, offs, lens, columns=RECORD_COLUMNS)
+    compare(res, rec)
+    assert res.counter_dict() == oracle_counters(rec, lens)
+    # some runs no longer qualify: a misaligned frame, a 65-B frame, bad descriptors
+    f65 = np.frombuffer(bytes(framegen.random_frames(rng, 1, min_len=65, max_len=65)[0]), np.uint8)
+    buf2 = np.concatenate([buf, f65, np.zeros(32, np.uint8)])
+    offs2, lens2 = offs.copy(), lens.copy()
+    offs2[64 * 3 + 5] += 1
+    lens2[64 * 3 + 5] = min(int(lens2[64 * 3 + 5]), 15)
+    offs2[64 * 7 + 9], lens2[64 * 7 + 9] = buf.size, 65
+    offs2[64 * 11] = buf2.size + 64
+    lens2[64 * 13 + 63] = buf2.size
+    rec2 = oracle_desc(buf2, offs2, lens2)
+    res2 = run_desc(buf2, offs2, lens2, columns=RECORD_COLUMNS)
+    compare(res2, rec2)
+    assert res2.counter_dict() == oracle_counters(rec2, lens2)
