@@ -225,54 +225,36 @@ __global__ __launch_bounds__(kBlock, NW < 8 ? 5 : 4) void rx_kernel(RxArgs a) {
         L.end[lane] = span < (uint32_t)NW ? span : (uint32_t)NW;   // granules to load into the window
         wave_sync();
 
-        // ---- short run: every frame 16-B aligned and at most 64 B ----------
-        // (descriptor batches of minimum-size frames: the AF_PACKET / ring
-        // hand-off of 64-B traffic). Four granule loads per frame instead of
-        // NW, no tail phase, and the small kernel's register fast path
-        // (small_fast: compile-time field positions) in place of parse_frame
-        // for IPv4/IHL-5 frames; the rest parse from the slot as usual.
-        if constexpr (kShortRuns) {
-            if (__ballot(in_batch && !desc_bad && (sh != 0 || len > 64u)) == 0ull) {
-                uint4 g[4];
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const int q = i * kWave + lane;
-                    const int fl = q >> 2, c = q & 3;
-                    g[i] = make_uint4(0, 0, 0, 0);
-                    if ((uint32_t)c < L.end[fl]) g[i] = load16(a.data + L.base[fl] + 16u * c);
-                }
-                fetch_desc(nrun);
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const int q = i * kWave + lane;
-                    uint32_t* dst = reinterpret_cast<uint32_t*>(L.win + (q >> 2) * kSlot + 16 * (q & 3));
-                    dst[0] = g[i].x; dst[1] = g[i].y; dst[2] = g[i].z; dst[3] = g[i].w;
-                }
-                wave_sync();
-                uint32_t w[16];
-#pragma unroll
-                for (int k = 0; k < 16; ++k) w[k] = reinterpret_cast<const uint32_t*>(slot)[k];
-                Parsed P{};
-                uint32_t ipc = 0, l4c = 0;
-                if (desc_bad) {
-                    P.st = PNET_ST_DESC_INVALID;
-                } else if (in_batch && small_fast(w, len, P, ipc, l4c)) {
-                    // IPv6 / IPv4 options: the frame lies whole in its slot (flags are 0)
-                    P = parse_frame(FrameBytes{slot, slot, 64}, len, 0u);
-                    uint32_t tA = 0, tB = 0;
-                    window_sums(slot, P.a_lo, P.a_hi, P.b_lo, P.b_hi, tA, tB);
-                    finalize(P, tA, tB, false, ipc, l4c);
-                }
-                store_columns(a.cols, f0, lane, in_batch, P, ipc, l4c, slot, 0);
-                if (a.cols.counters) K.add(in_batch && !desc_bad, len, P.st);
-                wave_sync();   // slots are rewritten by the next run
-                run = nrun;
-                continue;
-            }
-        }
+        // short run (descriptor batches of minimum-size frames: the AF_PACKET /
+        // ring hand-off of 64- or 60-B traffic): every frame at most 64 B, so no
+        // tail phase; four granule loads per frame when none straddles a fifth
+        // granule, and step 4 runs the small kernel's register fast path
+        // (small_fast: compile-time field positions) on the frame's 64 bytes
+        // realigned from its slot, parse_frame only for the frames it leaves
+        // (IPv6, IPv4 options). Descriptor 64-B batches -16 %, IMIX even
+        // (profiles/r03/short_runs/).
+        const bool short_run = kShortRuns && __ballot(in_batch && !desc_bad && len > 64u) == 0ull;
+        const bool four = short_run && __ballot(span > 4u) == 0ull;
+
 
         // ---- 2. window: NW*64 granule loads, all in flight before any store --
-        if (PASS != 1) {
+        if (kShortRuns && four) {   // wave-uniform: 4 granules per frame
+            uint4 g[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int q = i * kWave + lane;
+                const int fl = q >> 2, c = q & 3;
+                g[i] = make_uint4(0, 0, 0, 0);
+                if ((uint32_t)c < L.end[fl]) g[i] = load16(a.data + L.base[fl] + 16u * c);
+            }
+            fetch_desc(nrun);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int q = i * kWave + lane;
+                uint32_t* dst = reinterpret_cast<uint32_t*>(L.win + (q >> 2) * kSlot + 16 * (q & 3));
+                dst[0] = g[i].x; dst[1] = g[i].y; dst[2] = g[i].z; dst[3] = g[i].w;
+            }
+        } else if (PASS != 1) {
             uint4 g[NW];
 #pragma unroll
             for (int i = 0; i < NW; ++i) {
@@ -321,26 +303,40 @@ __global__ __launch_bounds__(kBlock, NW < 8 ? 5 : 4) void rx_kernel(RxArgs a) {
         PNET_PH(1);   // probe: tail phase
         // ---- 4. parse + window sums (lane l <-> frame l) -------------------
         Parsed P{};
-        if (desc_bad) P.st = PNET_ST_DESC_INVALID;
-        else if (in_batch)
-            P = parse_frame(FrameBytes{slot + sh, a.data + off, kWin - sh}, len, EXT ? a.flags : 0u);
-        // A (<= 97 B into the frame) lies in the window unless the window is
-        // shorter than 8 granules (IPv4 options past it); B may run past it
-        const int p0 = P.a_lo + sh, p1 = P.a_hi + sh, p2 = P.b_lo + sh, p3 = P.b_hi + sh;
-        uint32_t tA = 0, tB = 0;
-        window_sums(slot, p0, min(p1, kWin), min(p2, kWin), min(p3, kWin), tA, tB);
-        if (NW < 8 && p1 > kWin) tA += lane_range_sum(a.data + base, kWin, p1);
-        if (P.l4do && p3 > kWin) {
-            // B past the window = the speculative tail minus [kWin, p2) and [p3, fend)
-            tB += L.tail[lane];
-            const uint8_t* fb = a.data + base;
-            if (p2 > kWin) tB -= lane_range_sum(fb, kWin, p2);
-            if ((uint32_t)p3 < fend) tB -= lane_range_sum(fb, p3, (int)fend);
-        }
-
-        // ---- 5. finalize + stores ------------------------------------------
         uint32_t ipc = 0, l4c = 0;
-        finalize(P, tA, tB, (off & 1) != 0, ipc, l4c);
+        bool fast_done = false;
+        if (kShortRuns && short_run && in_batch && !desc_bad) {
+            // the frame's bytes [0, 64) from slot byte sh on (sh + 68 <= kSlot)
+            const uint32_t* s32 = reinterpret_cast<const uint32_t*>(slot) + (sh >> 2);
+            uint32_t w[16];
+#pragma unroll
+            for (int k = 0; k < 16; ++k) w[k] = __builtin_amdgcn_alignbyte(s32[k + 1], s32[k], (uint32_t)(sh & 3));
+            fast_done = !small_fast(w, len, P, ipc, l4c);
+        }
+        if (!fast_done) {
+            P = Parsed{};
+            if (desc_bad) P.st = PNET_ST_DESC_INVALID;
+            else if (in_batch)
+                P = parse_frame(FrameBytes{slot + sh, a.data + off, kWin - sh}, len, EXT ? a.flags : 0u);
+            // A (<= 97 B into the frame) lies in the window unless the window is
+            // shorter than 8 granules (IPv4 options past it); B may run past it
+            const int p0 = P.a_lo + sh, p1 = P.a_hi + sh, p2 = P.b_lo + sh, p3 = P.b_hi + sh;
+            uint32_t tA = 0, tB = 0;
+            window_sums(slot, p0, min(p1, kWin), min(p2, kWin), min(p3, kWin), tA, tB);
+            if (NW < 8 && p1 > kWin) tA += lane_range_sum(a.data + base, kWin, p1);
+            if (P.l4do && p3 > kWin) {
+                // B past the window = the speculative tail minus [kWin, p2) and [p3, fend)
+                tB += L.tail[lane];
+                const uint8_t* fb = a.data + base;
+                if (p2 > kWin) tB -= lane_range_sum(fb, kWin, p2);
+                if ((uint32_t)p3 < fend) tB -= lane_range_sum(fb, p3, (int)fend);
+            }
+
+            // ---- 5. finalize + stores --------------------------------------
+            ipc = 0;
+            l4c = 0;
+            finalize(P, tA, tB, (off & 1) != 0, ipc, l4c);
+        }
         PNET_PH(2);   // probe: parse, window sums, tail trims, finalize
         if (TX && in_batch && !desc_bad) tx_write(const_cast<uint8_t*>(a.data) + off, P, ipc, l4c);
         store_columns(a.cols, f0, lane, in_batch, P, ipc, l4c, slot, sh);

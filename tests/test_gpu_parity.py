@@ -938,9 +938,9 @@ def test_runs_of_small_slices_vs_oracle(seed, monkeypatch):
 
 
 @pytest.mark.parametrize("seed", [0, 1])
-def test_descriptor_runs_of_short_aligned_frames(seed):
-    """The mixed kernel's short-run path (every frame of a run 16-B aligned and
-    at most 64 B: the small kernel's register fast path over descriptors):
+def test_descriptor_runs_of_short_frames(seed):
+    """The mixed kernel's short-run path (every frame of a run at most 64 B: the
+    small kernel's register fast path on frames realigned from their slots):
     random UDP/TCP/ICMP/IPv6 frames of 0-64 B, the <= 64-B edge frames (IHL
     0-15, short L4, IPv6), a ragged last run; then the same batch with a few
     frames moved off alignment, one 65-B frame and invalid descriptors (their
@@ -968,3 +968,10 @@ def test_descriptor_runs_of_short_aligned_frames(seed):
     res2 = run_desc(buf2, offs2, lens2, columns=RECORD_COLUMNS)
     compare(res2, rec2)
     assert res2.counter_dict() == oracle_counters(rec2, lens2)
+    # any alignment: frames straddling four or five granules, runs of both kinds
+    for align, gap in ((1, 0), (1, 7), (4, 0)):
+        buf3, offs3, lens3 = framegen.pack(frames, align=align, gap=gap, rng=rng)
+        rec3 = oracle_desc(buf3, offs3, lens3)
+        res3 = run_desc(buf3, offs3, lens3, columns=RECORD_COLUMNS)
+        compare(res3, rec3)
+        assert res3.counter_dict() == oracle_counters(rec3, lens3)
