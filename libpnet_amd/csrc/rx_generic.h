@@ -138,6 +138,9 @@ __device__ __forceinline__ void tail_sums(const uint8_t* data, WaveLds<NW>& L, i
 // EXT: batch flags may be non-zero (VLAN / IPv6 extension dispatch) or
 // header-field columns may be requested; the plain instantiation compiles the
 // parse without those branches (half the code, SGPR spills 118 -> 14, IMIX -2 %).
+#ifndef PNET_SHORT_NT
+#define PNET_SHORT_NT 1   // non-temporal granule loads in 4-granule short runs (A/B: 0)
+#endif
 #ifndef PNET_SHORT_RUNS
 #define PNET_SHORT_RUNS 1   // A/B: short-run fast path in the mixed shape
 #endif
@@ -245,7 +248,8 @@ __global__ __launch_bounds__(kBlock, NW < 8 ? 5 : 4) void rx_kernel(RxArgs a) {
                 const int q = i * kWave + lane;
                 const int fl = q >> 2, c = q & 3;
                 g[i] = make_uint4(0, 0, 0, 0);
-                if ((uint32_t)c < L.end[fl]) g[i] = load16(a.data + L.base[fl] + 16u * c);
+                if ((uint32_t)c < L.end[fl])
+                    g[i] = PNET_SHORT_NT ? load16_nt(a.data + L.base[fl] + 16u * c) : load16(a.data + L.base[fl] + 16u * c);
             }
             fetch_desc(nrun);
 #pragma unroll
