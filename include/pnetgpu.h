@@ -50,9 +50,14 @@
  *     round_up(data + data_bytes, 16). (hipMalloc'd buffers always are.)
  *   - Threading: a context is bound to one device; calls on one context may be
  *     issued from one host thread at a time. Distinct contexts are independent.
- *     Up to 64 receive / slice launches of one context may be in flight at once
- *     (on any streams): each takes one of the context's 64 run-claim counter
- *     slots by launch order (run scheduling).
+ *     Any number of launches may be in flight, on any streams: the run-claim
+ *     counters (run scheduling) are owned per stream — launches
+ *     on one stream run in stream order and reuse their stream's counter slot;
+ *     the first 64 distinct streams a context sees get a slot each, launches on
+ *     later streams use the static schedule (same results, no claims). A
+ *     stream handle must not be destroyed while its work is in flight and
+ *     then reused for another stream of the same context (a reused slot is
+ *     detected on the device and counted: pnetgpu_ctx_sched_conflicts).
  *   - Malformed input never faults: frames whose descriptor falls outside
  *     [0, data_bytes) get PNET_ST_DESC_INVALID, short frames get the
  *     *_MALFORMED bits (the reference's `new()` returning None).
@@ -228,6 +233,33 @@ int         pnetgpu_device_count(int* count);
 
 int  pnetgpu_ctx_create(int device, pnetgpu_ctx** out);
 void pnetgpu_ctx_destroy(pnetgpu_ctx* ctx);
+
+/* ---- per-context tuning -------------------------------------------------
+ * The kernels' measured defaults can be overridden per
+ * context, for tests and measurement tools. Each key is read from the
+ * environment variable PNETGPU_<NAME> once, in pnetgpu_ctx_create, and is
+ * never re-read on a call: afterwards only pnetgpu_ctx_set_tuning changes it.
+ * A value of -1 restores the default. */
+#define PNETGPU_TUNE_RX_KIND             0  /* non-small receive batches: 0 mixed, 2 MTU, 3 jumbo shape   */
+#define PNETGPU_TUNE_BLOCKS_PER_CU       1  /* receive grid: resident blocks per CU (> 0)                  */
+#define PNETGPU_TUNE_STATIC_PCT          2  /* share of runs taken in grid-stride order, 0..100 (100: no claims; default 88) */
+#define PNETGPU_TUNE_CLAIM_COUNTERS      3  /* claim counters per launch, 1..128 (default 64)              */
+#define PNETGPU_TUNE_SLICE_BLOCKS_PER_CU 4  /* slice grids: resident blocks per CU (> 0)                   */
+#define PNETGPU_TUNE_SLICE_KERNEL        5  /* descriptor slices: 1 slice_run_kernel, 2 slice_kernel       */
+#define PNETGPU_TUNE_SLICE_DENSE_SPAN    6  /* bytes a run of small slices must span to be LDS-staged (default 2048) */
+#define PNETGPU_TUNE_DEBUG               7  /* 1: log each receive call's kernel and grid to stderr        */
+#define PNETGPU_TUNE_SCHED_EPOCH         8  /* test hook: raise every stream slot's launch epoch to at least
+                                             * this (0..2^32-1), so a test reaches the epoch wrap, where the
+                                             * slot is re-zeroed in stream order                             */
+#define PNETGPU_NTUNE                    9
+int pnetgpu_ctx_set_tuning(pnetgpu_ctx* ctx, int key, int64_t value);
+int pnetgpu_ctx_get_tuning(const pnetgpu_ctx* ctx, int key, int64_t* value);
+
+/* Claims of a launch that found its stream's counter slot taken by another
+ * launch (a stream handle destroyed with work in flight and reused): the
+ * number counted on the device since the context was created, 0 when the
+ * schedule was never shared. Synchronises the context's device. */
+int pnetgpu_ctx_sched_conflicts(pnetgpu_ctx* ctx, uint64_t* count);
 
 /* Receive path: parse + verify every frame of `batch`, write `cols`. */
 int pnetgpu_rx_process(pnetgpu_ctx* ctx, const pnetgpu_batch* batch,

@@ -99,6 +99,12 @@ def _load():
     L.pnetgpu_ctx_create.argtypes = [i32, ctypes.POINTER(vp)]
     L.pnetgpu_ctx_destroy.restype = None
     L.pnetgpu_ctx_destroy.argtypes = [vp]
+    L.pnetgpu_ctx_set_tuning.restype = i32
+    L.pnetgpu_ctx_set_tuning.argtypes = [vp, i32, ctypes.c_int64]
+    L.pnetgpu_ctx_get_tuning.restype = i32
+    L.pnetgpu_ctx_get_tuning.argtypes = [vp, i32, ctypes.POINTER(ctypes.c_int64)]
+    L.pnetgpu_ctx_sched_conflicts.restype = i32
+    L.pnetgpu_ctx_sched_conflicts.argtypes = [vp, ctypes.POINTER(u64)]
     for f in (L.pnetgpu_rx_process, L.pnetgpu_tx_fill_checksums):
         f.restype = i32
         f.argtypes = [vp, ctypes.POINTER(Batch), ctypes.POINTER(RxColumns), vp]

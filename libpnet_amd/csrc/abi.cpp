@@ -17,6 +17,18 @@
 #include "pnetgpu_ring.h"
 #include "rx_internal.h"
 
+// run-claim counter slots per context: one per stream (launches on one stream
+// run in order, so they reuse its slot; slot s's count is stamped by epoch)
+constexpr uint32_t kSchedSlots = 64;
+constexpr uint32_t kMaxCtrs = 128;                                   // counters per slot
+constexpr size_t kCtrStride = 256 / sizeof(unsigned long long);      // 256 B apart
+constexpr size_t kSchedStride = kMaxCtrs * kCtrStride;
+// the slots, then one 256-B line holding the conflict count
+constexpr size_t kSchedBytes = (kSchedSlots * kSchedStride + kCtrStride) * sizeof(unsigned long long);
+// epochs of a slot must grow; the slot is re-zeroed in stream order before its
+// count would wrap
+constexpr uint32_t kEpochWrap = 0xFFFFFF00u;
+
 struct pnetgpu_ctx {
     int device;
     int cus;
@@ -24,10 +36,14 @@ struct pnetgpu_ctx {
     int per_cu[8][2] = {};
     // of each slice kernel: [strided, run, group] x pseudo {0, 4, 16} x extra
     int slice_per_cu[3][8][2] = {};
-    // run-claim counters of the receive launches (RxArgs::sched): one 128-B
-    // line per slot, slots used round robin by launch epoch
+    // run-claim counters of the launches (RunSched): kSchedSlots slots of
+    // kMaxCtrs counters, 256 B apart, owned by the stream in slot_stream
     unsigned long long* d_sched = nullptr;
-    std::atomic<uint32_t> epoch{0};
+    void* slot_stream[kSchedSlots] = {};
+    uint32_t slot_epoch[kSchedSlots] = {};
+    uint32_t nslots = 0;
+    // PNETGPU_TUNE_* (-1: default), from the environment at creation only
+    int64_t tune[PNETGPU_NTUNE];
 };
 
 namespace pnetgpu {
@@ -48,25 +64,19 @@ namespace {
 
 constexpr int kBlock = 256;
 
+int64_t tuning(const pnetgpu_ctx* ctx, int key) { return ctx->tune[key]; }
+
 // persistent slice grid: one resident wave of blocks (at most `want`)
 int slice_grid(pnetgpu_ctx* ctx, int which, int pseudo, bool extra, uint64_t want) {
     // which 0 (strided): pseudo = strided_variant() in 0..7
     const int k = which == 0 ? pseudo : (pseudo == 0 ? 0 : pseudo == 4 ? 1 : 2);
     int& c = ctx->slice_per_cu[which][k][extra ? 1 : 0];
     if (c <= 0) c = pnetgpu::slice_blocks_per_cu(which, pseudo, extra);
-    const char* env = std::getenv("PNETGPU_SLICE_BLOCKS_PER_CU");   // tuning override (tools/)
-    const int v = env ? std::atoi(env) : 0;
+    const int64_t v = tuning(ctx, PNETGPU_TUNE_SLICE_BLOCKS_PER_CU);
     const uint64_t cap = (uint64_t)ctx->cus * (uint64_t)(v > 0 ? v : c > 0 ? c : 1);
     return (int)std::max<uint64_t>(1, std::min<uint64_t>(want, cap));
 }
 constexpr int kRunFrames = 64;      // frames per wave-run
-// run-claim counter slots per context: a launch uses slot epoch % kSchedSlots,
-// so up to kSchedSlots receive launches of one context may be in flight at once
-constexpr uint32_t kSchedSlots = 64;
-constexpr uint32_t kMaxCtrs = 128;                                   // counters per slot
-constexpr size_t kCtrStride = 256 / sizeof(unsigned long long);      // 256 B apart
-constexpr size_t kSchedStride = kMaxCtrs * kCtrStride;
-constexpr size_t kSchedBytes = kSchedSlots * kSchedStride * sizeof(unsigned long long);
 #ifndef PNET_STATIC_PCT
 #define PNET_STATIC_PCT 88   // share of a batch's runs assigned statically (100: no claims)
 #endif
@@ -79,29 +89,76 @@ constexpr size_t kSchedBytes = kSchedSlots * kSchedStride * sizeof(unsigned long
 // waves of a SIMD, the slower XCDs: tools/wave_times.py) do not set the
 // kernel's end. Launches of fewer than 8 units per wave stay static (1500-B
 // frames at 4 runs per wave: claims measured even to +1 %).
-int plan_sched(pnetgpu_ctx* ctx, uint64_t nunits, uint64_t nwaves, pnetgpu::RunSched* s) {
+// The counters are the stream's own slot: launches on one stream are ordered,
+// so the next one may stamp the slot (atomicMax of its epoch) only after the
+// previous one has finished with it; a stream beyond the 64 slots runs static.
+int plan_sched(pnetgpu_ctx* ctx, uint64_t nunits, uint64_t nwaves, void* stream, pnetgpu::RunSched* s) {
     *s = pnetgpu::RunSched{};
     s->nstatic = nunits;
-    const char* static_env = std::getenv("PNETGPU_STATIC_PCT");   // tuning override (tools/)
-    const int static_pct = static_env ? std::atoi(static_env) : PNET_STATIC_PCT;
-    if (static_pct < 0 || static_pct >= 100 || nwaves == 0 || nunits < 8 * nwaves) return PNETGPU_OK;
-    s->nstatic = (nunits * (uint64_t)static_pct / 100) / nwaves * nwaves;
-    uint32_t e = ++ctx->epoch;
-    if (e >= 0xFFFFFF00u) {   // epochs must grow: re-zero the slots before the count wraps
-        if (hipDeviceSynchronize() != hipSuccess || hipMemset(ctx->d_sched, 0, kSchedBytes) != hipSuccess)
-            return pnetgpu::hip_fail(hipGetLastError());
-        ctx->epoch = 1;
-        e = 1;
+    const int64_t tp = tuning(ctx, PNETGPU_TUNE_STATIC_PCT);
+    const int64_t static_pct = tp >= 0 ? tp : PNET_STATIC_PCT;
+    if (static_pct >= 100 || nwaves == 0 || nunits < 8 * nwaves) return PNETGPU_OK;
+    uint32_t slot = 0;
+    while (slot < ctx->nslots && ctx->slot_stream[slot] != stream) ++slot;
+    if (slot == ctx->nslots) {
+        if (ctx->nslots == kSchedSlots) return PNETGPU_OK;   // no slot left for this stream: static
+        ctx->slot_stream[ctx->nslots] = stream;
+        ctx->slot_epoch[ctx->nslots++] = (uint32_t)std::max<int64_t>(0, tuning(ctx, PNETGPU_TUNE_SCHED_EPOCH));
     }
+    unsigned long long* ctr = ctx->d_sched + (size_t)slot * kSchedStride;
+    uint32_t e = ++ctx->slot_epoch[slot];
+    if (e >= kEpochWrap) {   // re-zero the slot behind the stream's earlier launches
+        const hipError_t he = hipMemsetAsync(ctr, 0, kSchedStride * sizeof(unsigned long long),
+                                             static_cast<hipStream_t>(stream));
+        if (he != hipSuccess) return pnetgpu::hip_fail(he);
+        ctx->slot_epoch[slot] = e = 1;
+    }
+    s->nstatic = (nunits * (uint64_t)static_pct / 100) / nwaves * nwaves;
     s->epoch = e;
-    s->ctr = ctx->d_sched + (size_t)(e % kSchedSlots) * kSchedStride;
-    const char* nctr_env = std::getenv("PNETGPU_CLAIM_COUNTERS");   // tuning override (tools/)
-    const int nctr = nctr_env ? std::atoi(nctr_env) : PNET_CLAIM_COUNTERS;
+    s->ctr = ctr;
+    s->conflicts = ctx->d_sched + (size_t)kSchedSlots * kSchedStride;
+    const int64_t tn = tuning(ctx, PNETGPU_TUNE_CLAIM_COUNTERS);
+    const uint64_t nctr = tn > 0 ? (uint64_t)tn : PNET_CLAIM_COUNTERS;
     // every counter needs home waves: wave ids [0, 32 nctr) cover them all
     const uint64_t homes = std::max<uint64_t>(1, nwaves / 32);
-    s->nctr = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>({(uint64_t)std::max(nctr, 1), kMaxCtrs, homes}));
+    s->nctr = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>({nctr, kMaxCtrs, homes}));
     s->ctr_stride = (uint32_t)kCtrStride;
     return PNETGPU_OK;
+}
+
+// PNETGPU_<NAME> of each tuning key, read once when a context is created
+const char* const kTuneEnv[PNETGPU_NTUNE] = {"PNETGPU_RX_KIND",        "PNETGPU_BLOCKS_PER_CU",
+                                             "PNETGPU_STATIC_PCT",     "PNETGPU_CLAIM_COUNTERS",
+                                             "PNETGPU_SLICE_BLOCKS_PER_CU", "PNETGPU_SLICE_KERNEL",
+                                             "PNETGPU_SLICE_DENSE_SPAN",    "PNETGPU_DEBUG",
+                                             "PNETGPU_SCHED_EPOCH"};
+
+bool tuning_valid(int key, int64_t v) {
+    if (v == -1) return true;   // the default
+    switch (key) {
+    case PNETGPU_TUNE_RX_KIND: return v == pnetgpu::kKindMixed || v == pnetgpu::kKindMtu || v == pnetgpu::kKindJumbo;
+    case PNETGPU_TUNE_BLOCKS_PER_CU:
+    case PNETGPU_TUNE_SLICE_BLOCKS_PER_CU: return v >= 1 && v <= 64;
+    case PNETGPU_TUNE_STATIC_PCT: return v >= 0 && v <= 100;
+    case PNETGPU_TUNE_CLAIM_COUNTERS: return v >= 1 && v <= (int64_t)kMaxCtrs;
+    case PNETGPU_TUNE_SLICE_KERNEL: return v == 1 || v == 2;
+    case PNETGPU_TUNE_SLICE_DENSE_SPAN: return v >= 0 && v <= 65536;
+    case PNETGPU_TUNE_DEBUG: return v == 0 || v == 1;
+    case PNETGPU_TUNE_SCHED_EPOCH: return v >= 0 && v <= (int64_t)UINT32_MAX;
+    default: return false;
+    }
+}
+
+void tuning_from_env(pnetgpu_ctx* c) {
+    for (int k = 0; k < PNETGPU_NTUNE; ++k) {
+        c->tune[k] = -1;
+        const char* e = std::getenv(kTuneEnv[k]);
+        if (!e || !*e) continue;
+        int64_t v;
+        if (k == PNETGPU_TUNE_SLICE_KERNEL && (e[0] == 'r' || e[0] == 'g')) v = e[0] == 'r' ? 1 : 2;
+        else v = std::strtoll(e, nullptr, 10);
+        if (tuning_valid(k, v)) c->tune[k] = v;
+    }
 }
 
 int set_device(const pnetgpu_ctx* ctx) {
@@ -167,6 +224,7 @@ int pnetgpu_ctx_create(int device, pnetgpu_ctx** out) {
     if (!c) return PNETGPU_ENOMEM;
     c->device = device;
     c->cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+    tuning_from_env(c);
     if (hipMalloc((void**)&c->d_sched, kSchedBytes) != hipSuccess) {
         delete c;
         return PNETGPU_ENOMEM;
@@ -176,6 +234,34 @@ int pnetgpu_ctx_create(int device, pnetgpu_ctx** out) {
         return PNETGPU_EHIP;
     }
     *out = c;
+    return PNETGPU_OK;
+}
+
+int pnetgpu_ctx_set_tuning(pnetgpu_ctx* ctx, int key, int64_t value) {
+    if (!ctx || key < 0 || key >= PNETGPU_NTUNE || !tuning_valid(key, value)) return PNETGPU_EINVAL;
+    ctx->tune[key] = value;
+    if (key == PNETGPU_TUNE_SCHED_EPOCH && value > 0)   // only ever upward: a stamped slot keeps growing
+        for (uint32_t i = 0; i < ctx->nslots; ++i)
+            ctx->slot_epoch[i] = std::max(ctx->slot_epoch[i], (uint32_t)value);
+    return PNETGPU_OK;
+}
+
+int pnetgpu_ctx_get_tuning(const pnetgpu_ctx* ctx, int key, int64_t* value) {
+    if (!ctx || !value || key < 0 || key >= PNETGPU_NTUNE) return PNETGPU_EINVAL;
+    *value = ctx->tune[key];
+    return PNETGPU_OK;
+}
+
+int pnetgpu_ctx_sched_conflicts(pnetgpu_ctx* ctx, uint64_t* count) {
+    pnetgpu::set_last_hip_error(0);
+    if (!ctx || !count) return PNETGPU_EINVAL;
+    if (const int rc = set_device(ctx)) return rc;
+    if (const hipError_t e = hipDeviceSynchronize(); e != hipSuccess) return pnetgpu::hip_fail(e);
+    unsigned long long v = 0;
+    const hipError_t e = hipMemcpy(&v, ctx->d_sched + (size_t)kSchedSlots * kSchedStride, sizeof(v),
+                                   hipMemcpyDeviceToHost);
+    if (e != hipSuccess) return pnetgpu::hip_fail(e);
+    *count = v;
     return PNETGPU_OK;
 }
 
@@ -240,17 +326,10 @@ static int rx_common(pnetgpu_ctx* ctx, const pnetgpu_batch* b, const pnetgpu_rx_
         else
             kind = b->frame_len >= 4096 ? pnetgpu::kKindJumbo : pnetgpu::kKindMtu;
     }
-    // tuning overrides (read per call: tests and tools flip them at run time)
-    const char* kind_env = std::getenv("PNETGPU_RX_KIND");
-    const char* per_cu_env = std::getenv("PNETGPU_BLOCKS_PER_CU");
-    const char* debug_env = std::getenv("PNETGPU_DEBUG");
-    const bool debug = debug_env && *debug_env == '1';
-    if (kind_env) {
-        const int v = std::atoi(kind_env);
-        if ((v == pnetgpu::kKindMixed || v == pnetgpu::kKindMtu || v == pnetgpu::kKindJumbo) &&
-            kind != pnetgpu::kKindSmall)
-            kind = v;
-    }
+    // the context's tuning (pnetgpu_ctx_set_tuning; never the environment per call)
+    const bool debug = tuning(ctx, PNETGPU_TUNE_DEBUG) > 0;
+    const int64_t kind_v = tuning(ctx, PNETGPU_TUNE_RX_KIND);
+    if (kind_v >= 0 && kind != pnetgpu::kKindSmall) kind = (int)kind_v;
     const int ext = rxf != 0 || a.field_cols;   // the EXT instantiations (launch_rx)
     int& per_cu_cached = ctx->per_cu[kind & 7][ext];
     if (per_cu_cached <= 0 || debug) {                             // first use of this kernel on ctx
@@ -261,13 +340,13 @@ static int rx_common(pnetgpu_ctx* ctx, const pnetgpu_batch* b, const pnetgpu_rx_
                          per_cu_cached, ctx->cus);
     }
     if (per_cu_cached <= 0) return pnetgpu::hip_fail(hipGetLastError());
-    const int per_cu_v = per_cu_env ? std::atoi(per_cu_env) : 0;
-    const int per_cu = per_cu_v > 0 ? per_cu_v : per_cu_cached;
+    const int64_t per_cu_v = tuning(ctx, PNETGPU_TUNE_BLOCKS_PER_CU);
+    const int per_cu = per_cu_v > 0 ? (int)per_cu_v : per_cu_cached;
     const uint64_t wpb = (uint64_t)pnetgpu::rx_waves_per_block(kind);
     const uint64_t want = (a.nruns + wpb - 1) / wpb;
     const uint64_t cap = (uint64_t)ctx->cus * (uint64_t)per_cu;
     const int blocks = (int)std::max<uint64_t>(1, std::min(want, cap));
-    if (const int rc = plan_sched(ctx, a.nruns, (uint64_t)blocks * wpb, &a.sched)) return rc;
+    if (const int rc = plan_sched(ctx, a.nruns, (uint64_t)blocks * wpb, stream, &a.sched)) return rc;
     if (const int e = pnetgpu::launch_rx(a, kind, blocks, tx, static_cast<hipStream_t>(stream))) {
         pnetgpu::set_last_hip_error(e);
         if (debug)
@@ -290,11 +369,18 @@ int pnetgpu_tx_fill_checksums(pnetgpu_ctx* ctx, const pnetgpu_batch* b, const pn
 // they span at least this many bytes (up to 5 KiB): coalesced loads beat the
 // per-lane gathers once the slices are >= ~32 B apart (each gather then
 // touches one cache line per lane); below, the gathers share lines and the
-// staging's latency costs more than it saves. PNETGPU_SLICE_DENSE_SPAN
+// staging's latency costs more than it saves. PNETGPU_TUNE_SLICE_DENSE_SPAN
 // overrides (0: always stage, 65536: never).
-static uint32_t dense_span() {
-    const char* env = std::getenv("PNETGPU_SLICE_DENSE_SPAN");
-    return env ? (uint32_t)std::strtoul(env, nullptr, 10) : 2048u;
+static uint32_t dense_span(const pnetgpu_ctx* ctx) {
+    const int64_t v = tuning(ctx, PNETGPU_TUNE_SLICE_DENSE_SPAN);
+    return v >= 0 ? (uint32_t)std::min<int64_t>(v, UINT32_MAX) : 2048u;
+}
+
+// slice_run_kernel for buffers of at most 512 B per slice unless the tuning
+// names the kernel (1 run, 2 group)
+static bool slice_run_choice(const pnetgpu_ctx* ctx, uint64_t data_bytes, uint64_t n) {
+    const int64_t k = tuning(ctx, PNETGPU_TUNE_SLICE_KERNEL);
+    return k == 1 ? true : k == 2 ? false : data_bytes / n <= 512;
 }
 
 static int slices_common(pnetgpu_ctx* ctx, const uint8_t* data, uint64_t data_bytes, uint64_t n,
@@ -320,7 +406,7 @@ static int slices_common(pnetgpu_ctx* ctx, const uint8_t* data, uint64_t data_by
     a.extra_offsets = extra_offsets;
     a.extra_lengths = extra_lengths;
     a.out = out;
-    a.dense_min = dense_span();
+    a.dense_min = dense_span(ctx);
     // Kernel choice. The slice lengths are device-resident, so the host decides
     // by the BUFFER bytes per slice (data_bytes / n), which equals the bytes per
     // slice only for slices that tile the buffer: slice_run_kernel (one wave per
@@ -332,15 +418,13 @@ static int slices_common(pnetgpu_ctx* ctx, const uint8_t* data, uint64_t data_by
     // batches the same way (their extra slices summed as a second range). Short
     // slices spread through a large buffer (e.g. headers of MTU frames) thus
     // take slice_kernel; callers that know their slice sizes set
-    // PNETGPU_SLICE_KERNEL=run|group, and uniform slices have
+    // PNETGPU_TUNE_SLICE_KERNEL (1 run, 2 group), and uniform slices have
     // pnetgpu_checksum_slices_strided, which decides by the slice length itself.
-    const char* kenv = std::getenv("PNETGPU_SLICE_KERNEL");
-    bool run = data_bytes / n <= 512;
-    if (kenv) run = kenv[0] == 'r' ? true : kenv[0] == 'g' ? false : run;
+    const bool run = slice_run_choice(ctx, data_bytes, n);
     const uint64_t per_block = run ? kBlock : kBlock / 16;
     const int blocks = slice_grid(ctx, run ? 1 : 2, pseudo, extra_offsets != nullptr, (n + per_block - 1) / per_block);
     // scheduled units: slice_run_kernel's runs of 64 slices, slice_kernel's 4
-    if ((rc = plan_sched(ctx, run ? (n + 63) / 64 : (n + 3) / 4, (uint64_t)blocks * 4, &a.sched))) return rc;
+    if ((rc = plan_sched(ctx, run ? (n + 63) / 64 : (n + 3) / 4, (uint64_t)blocks * 4, stream, &a.sched))) return rc;
     if (const int e = pnetgpu::launch_slices(a, pseudo, run, blocks, static_cast<hipStream_t>(stream))) {
         pnetgpu::set_last_hip_error(e);
         return PNETGPU_EHIP;
@@ -369,7 +453,7 @@ int pnetgpu_checksum_slices_strided(pnetgpu_ctx* ctx, const uint8_t* data, uint6
     a.stride = stride;
     a.slice_len = slice_len;
     a.skipword = skipword;
-    a.dense_min = dense_span();
+    a.dense_min = dense_span(ctx);
     // small uniform slices (<= 64 B at <= 64 B apart): runs staged through LDS;
     // otherwise the descriptor kernels with computed offsets (the same choice
     // as pnetgpu_checksum_slices, by the slice length the caller gave)
@@ -382,7 +466,7 @@ int pnetgpu_checksum_slices_strided(pnetgpu_ctx* ctx, const uint8_t* data, uint6
     // computes it), slice_run_kernel's runs, slice_kernel's 4 slices
     const uint64_t slices_per_unit =
         small ? 64u * (stride ? std::max(1u, std::min(16u, 4096u / (64u * stride))) : 16u) : run ? 64u : 4u;
-    if ((rc = plan_sched(ctx, (n + slices_per_unit - 1) / slices_per_unit, (uint64_t)blocks * 4, &a.sched)))
+    if ((rc = plan_sched(ctx, (n + slices_per_unit - 1) / slices_per_unit, (uint64_t)blocks * 4, stream, &a.sched)))
         return rc;
     const int e = small ? pnetgpu::launch_slices_strided_small(a, blocks, static_cast<hipStream_t>(stream))
                         : pnetgpu::launch_slices(a, 0, run, blocks, static_cast<hipStream_t>(stream));
@@ -404,14 +488,12 @@ int pnetgpu_checksum_slices_compact(pnetgpu_ctx* ctx, const uint8_t* data, uint6
     a.offsets = reinterpret_cast<const uint64_t*>(desc);
     a.compact = 1;
     a.out = out;
-    a.dense_min = dense_span();
+    a.dense_min = dense_span(ctx);
     // the same choice as pnetgpu_checksum_slices (by the buffer bytes per slice)
-    const char* kenv = std::getenv("PNETGPU_SLICE_KERNEL");
-    bool run = data_bytes / n <= 512;
-    if (kenv) run = kenv[0] == 'r' ? true : kenv[0] == 'g' ? false : run;
+    const bool run = slice_run_choice(ctx, data_bytes, n);
     const uint64_t per_block = run ? kBlock : kBlock / 16;
     const int blocks = slice_grid(ctx, run ? 1 : 2, 0, false, (n + per_block - 1) / per_block);
-    if ((rc = plan_sched(ctx, run ? (n + 63) / 64 : (n + 3) / 4, (uint64_t)blocks * 4, &a.sched))) return rc;
+    if ((rc = plan_sched(ctx, run ? (n + 63) / 64 : (n + 3) / 4, (uint64_t)blocks * 4, stream, &a.sched))) return rc;
     if (const int e = pnetgpu::launch_slices(a, 0, run, blocks, static_cast<hipStream_t>(stream))) return pnetgpu::hip_fail((hipError_t)e);
     return PNETGPU_OK;
 }

@@ -51,6 +51,10 @@ struct WaveTimer {
     uint64_t t0 = wall_clock64();
     uint64_t c0 = clock64(), last = c0;
     uint64_t ph[5] = {0, 0, 0, 0, 0};
+    // tail-phase makespan (rx_kernel's tail_sums, per run summed): group-rounds
+    // issued, group-round slots (loop iterations x groups) and the slots a
+    // perfect split of the issued rounds would need (ceil(issued / groups))
+    uint64_t tail[3] = {0, 0, 0};
     uint32_t runs = 0;
     __device__ void mark(int i) {
         const uint64_t c = clock64();
@@ -71,6 +75,7 @@ struct WaveTimer {
             p[3] = runs;
             for (int i = 0; i < 5; ++i) p[4 + i] = ph[i];
             p[9] = c1 - c0;
+            for (int i = 0; i < 3; ++i) p[10 + i] = tail[i];
         }
     }
 };
@@ -78,7 +83,9 @@ struct WaveTimer {
 #define PNET_WT_RUN ++pnet_wt_.runs
 #define PNET_WT_END(wid) pnet_wt_.end((wid), lane)
 #define PNET_PH(i) pnet_wt_.mark(i)
+#define PNET_TAIL_STAT , pnet_wt_.tail
 #else
+#define PNET_TAIL_STAT
 #define PNET_WT_BEGIN
 #define PNET_WT_RUN
 #define PNET_WT_END(wid)
@@ -119,13 +126,14 @@ __device__ __forceinline__ void rotate_prio(uint32_t step) {
 struct RunQueue {
     uint64_t next_static, stride, nstatic, nruns, lo, hi;
     unsigned long long* ctr;
+    unsigned long long* conflicts;
     uint64_t pend;          // claimed ahead (dynamic phase), nruns when none is pending
     uint32_t epoch;
     bool stamped;
 
     __device__ RunQueue(const RunSched& s, uint64_t n_units, uint64_t wave_id, uint64_t wave_stride)
         : next_static(wave_id), stride(wave_stride), nstatic(s.ctr ? s.nstatic : n_units), nruns(n_units), lo(0),
-          hi(0), ctr(s.ctr), pend(n_units), epoch(s.epoch), stamped(false) {
+          hi(0), ctr(s.ctr), conflicts(s.conflicts), pend(n_units), epoch(s.epoch), stamped(false) {
         if (ctr) {
             const uint64_t h = (wave_id >> 5) % s.nctr, d = nruns - nstatic;
             lo = nstatic + d * h / s.nctr;
@@ -143,7 +151,11 @@ struct RunQueue {
                 (void)atomicMax(ctr, (unsigned long long)epoch << 32);
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             }
-            k = (uint32_t)atomicAdd(ctr, 1ull);
+            const unsigned long long old = atomicAdd(ctr, 1ull);
+            k = (uint32_t)old;
+            // another launch stamped this stream's slot while this one runs:
+            // claims may be shared, so the host hears of it (never silent)
+            if ((uint32_t)(old >> 32) != epoch && conflicts) atomicAdd(conflicts, 1ull);
         }
         stamped = true;
         const uint64_t r = lo + (uint64_t)__builtin_amdgcn_readfirstlane(k);

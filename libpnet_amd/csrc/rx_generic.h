@@ -61,7 +61,11 @@ __device__ __forceinline__ uint32_t lane_range_sum(const uint8_t* fb, int lo, in
 // frames needing more than one round first, so mixed sizes balance across the
 // groups (the caller sets L.qhead = kWave / G).
 template <int NW, int G, int U, bool NT, bool UNI, bool DYN>
-__device__ __forceinline__ void tail_sums(const uint8_t* data, WaveLds<NW>& L, int lane, int count) {
+__device__ __forceinline__ void tail_sums(const uint8_t* data, WaveLds<NW>& L, int lane, int count
+#ifdef PNET_WAVE_TIMES
+                                          , uint64_t (&stat)[3]
+#endif
+) {
     constexpr int kGroups = kWave / G;
     constexpr int kSlot = WaveLds<NW>::kSlot;
     constexpr uint32_t c_first = UNI ? 0u : (uint32_t)NW;
@@ -78,7 +82,14 @@ __device__ __forceinline__ void tail_sums(const uint8_t* data, WaveLds<NW>& L, i
         nneed = (fe + 15u) >> 4;
         c0 = c_first + j;
     }
+#ifdef PNET_WAVE_TIMES
+    uint32_t iters = 0, issued = 0;
+#endif
     while (__ballot(idx < count)) {
+#ifdef PNET_WAVE_TIMES
+        ++iters;
+        issued += (uint32_t)__popcll(__ballot(idx < count && j == 0));
+#endif
         if (idx < count) {
             uint4 v[U];
 #pragma unroll
@@ -130,6 +141,11 @@ __device__ __forceinline__ void tail_sums(const uint8_t* data, WaveLds<NW>& L, i
             }
         }
     }
+#ifdef PNET_WAVE_TIMES
+    stat[0] += issued;
+    stat[1] += (uint64_t)iters * kGroups;
+    stat[2] += (uint64_t)((issued + kGroups - 1) / kGroups) * kGroups;
+#endif
 }
 
 // PASS: 0 = window phase for every frame, then the tails of the long ones;
@@ -156,6 +172,8 @@ __global__ __launch_bounds__(kBlock, NW < 8 ? 5 : 4) void rx_kernel(RxArgs a) {
     // mixed shape's plain instantiation: no dispatch flags, header-field
     // columns or TX)
     constexpr bool kShortRuns = PNET_SHORT_RUNS && PASS == 0 && DYN && !EXT && !TX;
+    // the short-run realignment reads slot dwords up to byte sh + 67 (sh <= 15)
+    static_assert(!kShortRuns || kSlot >= 15 + 68, "short runs need a slot of at least 83 B");
 
     __shared__ WaveLds<NW> lds_all[kWavesPerBlock];
     __shared__ uint64_t blk_ctr[kWavesPerBlock][PNETGPU_NCOUNTERS];
@@ -300,7 +318,7 @@ __global__ __launch_bounds__(kBlock, NW < 8 ? 5 : 4) void rx_kernel(RxArgs a) {
             }
             if (DYN && lane == 0) L.qhead = kWave / G;
             wave_sync();
-            tail_sums<NW, G, U, NT, (PASS != 0), DYN>(a.data, L, lane, __popcll(tmask));
+            tail_sums<NW, G, U, NT, (PASS != 0), DYN>(a.data, L, lane, __popcll(tmask) PNET_TAIL_STAT);
         }
         wave_sync();
 

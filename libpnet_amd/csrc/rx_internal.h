@@ -13,9 +13,12 @@ namespace pnetgpu {
 // at a time from nctr counters, ctr_stride u64 apart from ctr (high 32 bits of
 // a counter: the launch epoch, stamped by atomicMax; low 32 bits: claims), so
 // waves whose share ran slow do not set the kernel's end. ctr == nullptr: all
-// units static.
+// units static. The counters belong to the launch's stream (abi.cpp
+// plan_sched): a claim that returns another epoch means a concurrent launch
+// took the slot, and is counted at `conflicts`.
 struct RunSched {
     unsigned long long* ctr;
+    unsigned long long* conflicts;
     uint64_t nstatic;
     uint32_t epoch;
     uint32_t nctr;
@@ -85,8 +88,9 @@ constexpr int kKindJumbo = 3;
 constexpr int kWaveTimeSlots = 16384;
 // t_start, t_end, (xcc << 32) | HW_ID, runs, then the shader clocks (s_memtime)
 // the wave spent in each phase of its runs (PNET_PH marks: rx_kernel's window,
-// tail, parse, stores) and the wave's whole s_memtime span
-constexpr int kWaveTimeWords = 10;
+// tail, parse, stores), the wave's whole s_memtime span, then the tail phase's
+// group-rounds issued, slots used and ideal slots (WaveTimer::tail)
+constexpr int kWaveTimeWords = 13;
 
 // device index a context is bound to (abi.cpp)
 int ctx_device(const pnetgpu_ctx* ctx);

@@ -16,6 +16,7 @@ HIP kernels of libpnetgpu.so. Unsigned columns are stored in signed torch dtypes
 of the same width; RxResult.numpy() returns the unsigned views.
 """
 import ctypes
+from contextlib import contextmanager
 from contextlib import nullcontext as _nullcontext
 
 import numpy as np
@@ -91,6 +92,11 @@ def column_bytes(columns):
     return out
 
 
+#: tuning keys of pnetgpu_ctx_set_tuning (PNETGPU_TUNE_<NAME>), by lower-case name
+TUNING_KEYS = {k[len("PNETGPU_TUNE_"):].lower(): v for k, v in DEFS.items() if k.startswith("PNETGPU_TUNE_")}
+_SLICE_KERNELS = {"run": 1, "group": 2}
+
+
 class Context:
     """One pnetgpu_ctx bound to a HIP device."""
 
@@ -99,6 +105,40 @@ class Context:
         h = ctypes.c_void_p()
         check(lib.pnetgpu_ctx_create(self.device, ctypes.byref(h)), "pnetgpu_ctx_create")
         self.handle = h
+
+    def set_tuning(self, name, value):
+        """pnetgpu_ctx_set_tuning: override a kernel default on this context
+        (name: a TUNING_KEYS key, e.g. "static_pct"; value None or -1 restores
+        the default; slice_kernel also takes "run" / "group")."""
+        if name not in TUNING_KEYS:
+            raise KeyError(f"unknown tuning key {name!r} (one of {sorted(TUNING_KEYS)})")
+        v = -1 if value is None else _SLICE_KERNELS.get(value, value)
+        check(lib.pnetgpu_ctx_set_tuning(self.handle, TUNING_KEYS[name], int(v)), f"set_tuning({name}={value})")
+
+    def get_tuning(self, name):
+        """The current setting (-1: the default)."""
+        v = ctypes.c_int64()
+        check(lib.pnetgpu_ctx_get_tuning(self.handle, TUNING_KEYS[name], ctypes.byref(v)), "get_tuning")
+        return v.value
+
+    @contextmanager
+    def tuning(self, **settings):
+        """Apply settings for the duration of a with-block, then restore them."""
+        old = {k: self.get_tuning(k) for k in settings}
+        try:
+            for k, v in settings.items():
+                self.set_tuning(k, v)
+            yield self
+        finally:
+            for k, v in old.items():
+                self.set_tuning(k, v)
+
+    def sched_conflicts(self):
+        """Claims that found this context's stream slot taken by a concurrent
+        launch (pnetgpu_ctx_sched_conflicts; synchronises the device)."""
+        v = ctypes.c_uint64()
+        check(lib.pnetgpu_ctx_sched_conflicts(self.handle, ctypes.byref(v)), "pnetgpu_ctx_sched_conflicts")
+        return v.value
 
     def close(self):
         if getattr(self, "handle", None):
@@ -118,10 +158,32 @@ _contexts = {}
 def context(device=None):
     if device is None:
         device = torch.cuda.current_device()
-    device = torch.device("cuda", device).index if not isinstance(device, int) else device
+    if isinstance(device, torch.device):
+        device = device.index or 0
+    elif isinstance(device, str):
+        device = torch.device(device).index or 0
     if device not in _contexts:
         _contexts[device] = Context(device)
     return _contexts[device]
+
+
+def tuning(device=None, **settings):
+    """Context manager: tuning settings on the shared context of `device`
+    (Context.tuning), e.g. `with engine.tuning(static_pct=0, claim_counters=4):`."""
+    return context(device).tuning(**settings)
+
+
+def apply_tuning_env(settings, device=None):
+    """Measurement tools: apply {"PNETGPU_<NAME>": value} settings (named as the
+    environment variables a context reads at creation) to the shared context of
+    `device` through pnetgpu_ctx_set_tuning; "" or None restores the default."""
+    ctx = context(device)
+    for k, v in settings.items():
+        name = k[len("PNETGPU_"):].lower() if k.startswith("PNETGPU_") else k
+        if v in ("", None):
+            ctx.set_tuning(name, None)
+        else:
+            ctx.set_tuning(name, v if name == "slice_kernel" and v in _SLICE_KERNELS else int(v))
 
 
 def _stream_handle(stream, device):
@@ -192,6 +254,21 @@ class RxResult:
 def _check_u8_cuda(t, what):
     if not (isinstance(t, torch.Tensor) and t.is_cuda and t.dtype == torch.uint8 and t.is_contiguous()):
         raise TypeError(f"{what} must be a contiguous torch.uint8 CUDA tensor")
+
+
+def _check_dev(t, what, dtypes, device, numel):
+    """A device array the kernels read: contiguous, of one of `dtypes`, on the
+    data's device and holding at least `numel` elements (a host pointer or a
+    short array would fault the GPU or read past the end)."""
+    if not (isinstance(t, torch.Tensor) and t.is_cuda and t.device == device and t.is_contiguous()):
+        raise TypeError(f"{what} must be a contiguous CUDA tensor on {device}")
+    if t.dtype not in dtypes:
+        raise TypeError(f"{what} must be one of {[str(d) for d in dtypes]}, not {t.dtype}")
+    if t.numel() < numel:
+        raise ValueError(f"{what} holds {t.numel()} elements, {numel} needed")
+
+
+_I64, _I32, _U8 = (torch.int64, torch.uint64), (torch.int32, torch.uint32), (torch.uint8,)
 
 
 def last_rx_kernel():
@@ -265,9 +342,15 @@ def _rx_or_tx(fn_name, data, n_frames, stride, frame_len, first_offset, offsets,
     return out
 
 
-def _slices(fn_name, data, offsets, lengths, skipwords, addrs=None, protos=None, stream=None):
+def _slices(fn_name, data, offsets, lengths, skipwords, addrs=None, protos=None, stream=None, alen=0):
     _check_u8_cuda(data, "data")
     n = offsets.numel()
+    _check_dev(offsets, "offsets", _I64, data.device, n)
+    _check_dev(lengths, "lengths", _I32, data.device, n)
+    _check_dev(skipwords, "skipwords", _I32, data.device, n)
+    if addrs is not None:
+        _check_dev(addrs, "addrs", _U8, data.device, n * alen)
+        _check_dev(protos, "protos", _U8, data.device, n)
     out = torch.empty(n, dtype=torch.int16, device=data.device)
     ctx = context(data.device.index)
     args = [ctx.handle, _ptr(data), data.numel(), n, _ptr(offsets), _ptr(lengths), _ptr(skipwords)]
@@ -297,9 +380,14 @@ def slice_descriptors(offsets, lengths, skipwords, device=None):
 
 
 def checksum_slices_compact(data, desc, stream=None):
-    """out[i] = util::checksum over compact descriptors (slice_descriptors(...) on the
-    data's device): pnetgpu_checksum_slices_compact."""
+    """out[i] = util::checksum over compact descriptors (slice_descriptors(...)):
+    pnetgpu_checksum_slices_compact. Descriptors held elsewhere than the data's
+    device (e.g. slice_descriptors' host tensor) are copied there first."""
     _check_u8_cuda(data, "data")
+    if not isinstance(desc, torch.Tensor) or desc.dtype not in _I64:
+        raise TypeError("desc must be an int64 / uint64 tensor of packed pnetgpu_slice_desc records")
+    if not desc.is_cuda or desc.device != data.device or not desc.is_contiguous():
+        desc = desc.to(data.device).contiguous()
     n = desc.numel()
     out = torch.empty(n, dtype=torch.int16, device=data.device)
     ctx = context(data.device.index)
@@ -312,6 +400,11 @@ def checksum_slices_strided(data, n, stride, slice_len, skipword, first_offset=0
     """out[i] = util::checksum(data[first_offset + i*stride, +slice_len), skipword), i < n:
     uniform slices without descriptor arrays (pnetgpu_checksum_slices_strided)."""
     _check_u8_cuda(data, "data")
+    for v, what in ((stride, "stride"), (slice_len, "slice_len"), (skipword, "skipword")):
+        if not 0 <= int(v) < (1 << 32):   # u32 in the C-ABI: never truncated
+            raise ValueError(f"{what}={v} must be in [0, 2^32)")
+    if int(n) < 0 or int(first_offset) < 0:
+        raise ValueError("n and first_offset must be non-negative")
     out = torch.empty(n, dtype=torch.int16, device=data.device)
     ctx = context(data.device.index)
     check(lib.pnetgpu_checksum_slices_strided(ctx.handle, _ptr(data), data.numel(), n, first_offset, stride,
@@ -322,7 +415,7 @@ def checksum_slices_strided(data, n, stride, slice_len, skipword, first_offset=0
 
 def ipv4_checksum_slices(data, offsets, lengths, skipwords, addrs, protos, stream=None):
     """util::ipv4_checksum per slice; addrs uint8 [n, 8] (src||dst), protos uint8 [n]."""
-    return _slices("pnetgpu_ipv4_checksum_slices", data, offsets, lengths, skipwords, addrs, protos, stream)
+    return _slices("pnetgpu_ipv4_checksum_slices", data, offsets, lengths, skipwords, addrs, protos, stream, alen=8)
 
 
 def checksum_adv_slices(version, data, offsets, lengths, skipwords, extra_offsets, extra_lengths, addrs, protos,
@@ -331,6 +424,11 @@ def checksum_adv_slices(version, data, offsets, lengths, skipwords, extra_offset
     version 4 (addrs [n, 8]) or 6 (addrs [n, 32])."""
     _check_u8_cuda(data, "data")
     n = offsets.numel()
+    for t, what, dts, k in ((offsets, "offsets", _I64, 1), (lengths, "lengths", _I32, 1),
+                            (skipwords, "skipwords", _I32, 1), (extra_offsets, "extra_offsets", _I64, 1),
+                            (extra_lengths, "extra_lengths", _I32, 1), (addrs, "addrs", _U8, 8 if version == 4 else 32),
+                            (protos, "protos", _U8, 1)):
+        _check_dev(t, what, dts, data.device, n * k)
     out = torch.empty(n, dtype=torch.int16, device=data.device)
     ctx = context(data.device.index)
     fn = "pnetgpu_ipv4_checksum_adv_slices" if version == 4 else "pnetgpu_ipv6_checksum_adv_slices"
@@ -342,4 +440,4 @@ def checksum_adv_slices(version, data, offsets, lengths, skipwords, extra_offset
 
 def ipv6_checksum_slices(data, offsets, lengths, skipwords, addrs, protos, stream=None):
     """util::ipv6_checksum per slice; addrs uint8 [n, 32] (src||dst), protos uint8 [n]."""
-    return _slices("pnetgpu_ipv6_checksum_slices", data, offsets, lengths, skipwords, addrs, protos, stream)
+    return _slices("pnetgpu_ipv6_checksum_slices", data, offsets, lengths, skipwords, addrs, protos, stream, alen=32)

@@ -10,9 +10,11 @@ the fields the GPU extracted, and whose payload() is a zero-copy memoryview of
 the frame bytes at the bounds the GPU computed. Nothing here re-parses a frame.
 
 The rest of the trait surface (pnet_macros_support/src/packet.rs:19-89):
-`packet()` / `payload()` (Packet), `packet_mut()` / `payload_mut()` (MutablePacket:
-writable views when the frame buffer is writable — edit, then recompute the
-checksums of the whole batch with tx_fill_checksums), `packet_size()`
+`packet()` / `payload()` (Packet), `packet_mut()` / `payload_mut()` /
+`clone_from()` (MutablePacket: writable views when the frame buffer is
+writable — edit, then recompute the checksums of the whole batch with
+tx_fill_checksums), the generated `minimum_packet_size()` and
+`to_immutable()` (decorator.rs:589-632), `packet_size()`
 (PacketSize, the generated header + variable-field sizes) and `from_packet()`
 (FromPacket: an owned dict of every field). IPv4 and TCP options are decoded
 from the option bytes between the fixed header and the bounds the record
@@ -25,6 +27,7 @@ gives, by the generated Ipv4OptionIterable / TcpOptionIterable rules
     if ip and (udp := ip.udp()):                # UdpPacket::new(ip.payload())
         udp.get_source(), udp.payload(), udp.checksum_ok()
 """
+import copy
 import ipaddress
 from dataclasses import dataclass
 
@@ -55,6 +58,34 @@ def _writable(buf, what):
 
 def _be16(b, at):
     return (b[at] << 8) | b[at + 1]
+
+
+#: minimum_packet_size() of each view: the byte size of its fixed fields, the
+#: bound every generated new() checks (pnet_macros/src/decorator.rs:589-600,623-629)
+MINIMUM_PACKET_SIZE = {"ethernet": 14, "ipv4": 20, "ipv6": 40, "udp": 8, "tcp": 20, "icmp": 4, "icmpv6": 4,
+                       "echo_request": 8, "echo_reply": 8, "destination_unreachable": 8, "time_exceeded": 8}
+
+
+class _PacketTraits:
+    """The generated inherent methods and MutablePacket defaults every view shares
+    (pnet_macros/src/decorator.rs:589-632, pnet_macros_support/src/packet.rs:61-72)."""
+
+    def to_immutable(self):
+        """MutableXxxPacket::to_immutable: the same view over a read-only buffer
+        (packet_mut / payload_mut / clone_from then raise)."""
+        v = copy.copy(self)
+        v._f = memoryview(self._f).toreadonly()
+        return v
+
+    consume_to_immutable = to_immutable
+
+    def clone_from(self, other):
+        """MutablePacket::clone_from: copy other.packet() (another view, or bytes)
+        over the start of this view's packet_mut(). Like the reference, asserts
+        that this packet is at least as long as the other."""
+        src = bytes(other.packet() if hasattr(other, "packet") else other)
+        assert len(self.packet()) >= len(src), "clone_from: the destination packet is shorter than the source"
+        self.packet_mut()[:len(src)] = src
 
 
 @dataclass(frozen=True)
@@ -100,11 +131,15 @@ def _option_iter(buf, tcp):
         buf = buf[min(1 + ll + plen, len(buf)):]
 
 
-class L4View:
+class L4View(_PacketTraits):
     """UdpPacket / TcpPacket / IcmpPacket / Icmpv6Packet over the IP payload."""
 
     def __init__(self, kind, records, i, frame):
         self.kind, self._r, self._i, self._f = kind, records, i, frame
+
+    def minimum_packet_size(self):
+        """UdpPacket 8, TcpPacket 20, IcmpPacket / Icmpv6Packet 4 (their new() bounds)."""
+        return MINIMUM_PACKET_SIZE[self.kind]
 
     def _rec(self, name):
         return _field(self._r, name, self._i)
@@ -284,6 +319,18 @@ class _IcmpMessage:
     def __init__(self, icmp):
         self._icmp = icmp
 
+    def minimum_packet_size(self):
+        """8: the fixed part of every ICMP message view (icmp.rs:221-232,304-314,378-389,425-436)."""
+        return 8
+
+    def to_immutable(self):
+        return type(self)(self._icmp.to_immutable())
+
+    consume_to_immutable = to_immutable
+
+    def clone_from(self, other):
+        self._icmp.clone_from(other)
+
     def packet(self):
         return self._icmp.packet()
 
@@ -350,11 +397,15 @@ class TimeExceededView(_IcmpMessage):
                     unused=self.get_unused(), payload=bytes(self.payload()))
 
 
-class IpView:
+class IpView(_PacketTraits):
     """Ipv4Packet / Ipv6Packet over the Ethernet payload."""
 
     def __init__(self, version, records, i, frame):
         self.version, self._r, self._i, self._f = version, records, i, frame
+
+    def minimum_packet_size(self):
+        """Ipv4Packet 20, Ipv6Packet 40."""
+        return MINIMUM_PACKET_SIZE["ipv4" if self.version == 4 else "ipv6"]
 
     def _rec(self, name):
         return _field(self._r, name, self._i)
@@ -512,11 +563,16 @@ class IpView:
         return self._l4("icmpv6")
 
 
-class FrameView:
+class FrameView(_PacketTraits):
     """EthernetPacket over one processed frame."""
 
     def __init__(self, records, i, frame):
         self._r, self._i, self._f = records, i, frame
+
+    @staticmethod
+    def minimum_packet_size():
+        """EthernetPacket::minimum_packet_size: 14."""
+        return MINIMUM_PACKET_SIZE["ethernet"]
 
     def _rec(self, name):
         return _field(self._r, name, self._i)

@@ -96,3 +96,38 @@ def test_compact_slice_descriptor_packing():
     with pytest.raises(ValueError):
         lp.slice_descriptors([0], [1 << 16], [0])
     assert np.asarray(lp.slice_descriptors([], [], [])).size == 0
+
+
+def test_tuning_entry_points_without_gpu():
+    """pnetgpu_ctx_set_tuning / get_tuning / sched_conflicts refuse a NULL
+    context and unknown keys (no GPU needed); every PNETGPU_TUNE_* key has a
+    Python name."""
+    import ctypes
+
+    from libpnet_amd import engine
+    from libpnet_amd._lib import DEFS, lib
+    assert lib.pnetgpu_ctx_set_tuning(None, 0, -1) == DEFS["PNETGPU_EINVAL"]
+    v = ctypes.c_int64()
+    assert lib.pnetgpu_ctx_get_tuning(None, 0, ctypes.byref(v)) == DEFS["PNETGPU_EINVAL"]
+    c = ctypes.c_uint64()
+    assert lib.pnetgpu_ctx_sched_conflicts(None, ctypes.byref(c)) == DEFS["PNETGPU_EINVAL"]
+    keys = sorted(v for k, v in DEFS.items() if k.startswith("PNETGPU_TUNE_"))
+    assert keys == list(range(DEFS["PNETGPU_NTUNE"]))
+    assert sorted(engine.TUNING_KEYS.values()) == keys
+
+
+def test_environment_read_only_at_context_creation():
+    """The product path reads no environment variable per call: the only
+    getenv in the C++ sources is tuning_from_env (called by pnetgpu_ctx_create)."""
+    import re
+    src_dir = os.path.join(ROOT, "libpnet_amd", "csrc")
+    for f in sorted(os.listdir(src_dir)):
+        text = open(os.path.join(src_dir, f)).read()
+        hits = [m.start() for m in re.finditer(r"\bgetenv\s*\(", text)]
+        if f != "abi.cpp":
+            assert not hits, f
+            continue
+        assert len(hits) == 1
+        fn = text.rfind("\nvoid tuning_from_env(", 0, hits[0])
+        assert fn >= 0 and text.find("\n}\n", fn) > hits[0]
+        assert "tuning_from_env(c);" in text[text.index("int pnetgpu_ctx_create"):]

@@ -2,7 +2,7 @@
 lengths — SURVEY.md §8(b)'s suggested layout) vs the oracle and vs the full
 u64/u32 descriptors of the same batch: random and extension frames at any
 alignment (with and without the parse extensions), invalid descriptors, the
-full-size IMIX workload, and the pinned ring, which ships compact descriptors
+full-size IMIX workload against the oracle, and the pinned ring, which ships compact descriptors
 whenever a batch qualifies."""
 import numpy as np
 import pytest
@@ -12,7 +12,7 @@ import libpnet_amd as lp
 from libpnet_amd.engine import ALL_COLUMNS
 from oracle import coracle
 from tests import framegen
-from tests.test_gpu_parity import compare, oracle_counters, to_dev
+from tests.test_gpu_parity import NTHREADS, compare, oracle_counters, to_dev
 
 pytestmark = pytest.mark.gpu
 
@@ -57,17 +57,19 @@ def test_compact_invalid_descriptors():
     assert res.counter_dict() == oracle_counters(rec, lens)
 
 
-def test_compact_imix_full_size_equals_full_descriptors():
-    w = lp.synth.make("imix", 1 << 22, seed=5, corrupt_ppm=10000)
-    d = to_dev(w.buf)
-    full = lp.rx_process(d, offsets=to_dev(w.offsets.astype(np.int64)),
-                         lengths=to_dev(w.lengths.astype(np.int32)), columns=lp.IPV4_COLUMNS)
-    comp = run_compact(d, w.offsets, w.lengths, columns=lp.IPV4_COLUMNS)
-    a, b = full.numpy(), comp.numpy()
-    for c in lp.IPV4_COLUMNS:
-        assert np.array_equal(a[c], b[c]), c
-    assert full.counter_dict() == comp.counter_dict()
-    assert comp.counter_dict()["frames"] == 1 << 22
+def test_compact_imix_full_size_vs_oracle():
+    """The bench's IMIX form (configs[3]: compact descriptors, 2^22 frames per
+    GPU, 1 % planted corruptions) against the oracle directly: every record
+    column, the counters, and every planted corruption found — the very batch
+    `python bench.py` times at N = 1 (its default --seed 1: synth seed 1000)."""
+    w = lp.synth.make("imix", 1 << 22, seed=1000, corrupt_ppm=10000)
+    rec = coracle.rx_batch(w.buf, w.n, offsets=w.offsets, lengths=w.lengths, nthreads=NTHREADS)
+    comp = run_compact(to_dev(w.buf), w.offsets, w.lengths, columns=lp.IPV4_COLUMNS)
+    compare(comp, rec)
+    c = comp.counter_dict()
+    assert c == oracle_counters(rec, w.lengths)
+    assert c["frames"] == 1 << 22
+    assert c["ip_csum_bad"] == w.expect["ip_bad"] and c["l4_csum_bad"] == w.expect["l4_bad"]
 
 
 def test_ring_ships_compact_descriptors_and_full_ones_for_long_frames():

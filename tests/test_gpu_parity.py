@@ -297,11 +297,12 @@ def test_small_kernel_strides_and_lengths(stride):
 
 @pytest.mark.parametrize("stride,flen", [(144, 144), (150, 97), (333, 333), (1500, 1500), (1514, 1400),
                                          (4000, 3999), (9018, 9018)])
-def test_stride_mode_random_frames_every_kernel(stride, flen, monkeypatch):
+def test_stride_mode_random_frames_every_kernel(stride, flen, tune):
     """Fixed-stride batches of random/malformed frames (garbage between frames,
     L4 ranges shorter than the frame, IPv4 options, IPv6) at every first-offset
-    alignment: the streaming kernel (chosen by default for these strides) and
-    the per-frame kernel kinds (forced through PNETGPU_RX_KIND) all bit-exact."""
+    alignment: the default kernel for the stride (rx_kernel's MTU shape below
+    4 KiB, the jumbo shape from 4 KiB) and every rx_kernel shape forced through
+    the rx_kind tuning (mixed, MTU, jumbo) all bit-exact."""
     rng = np.random.default_rng(stride + flen)
     n = 700
     frames = framegen.random_frames(rng, n, max_len=min(stride + 64, 9100))
@@ -313,10 +314,7 @@ def test_stride_mode_random_frames_every_kernel(stride, flen, monkeypatch):
         rec = coracle.rx_batch(buf, n, first=first, stride=stride, frame_len=flen, nthreads=NTHREADS)
         d = to_dev(buf)
         for kind in (None, "0", "2", "3"):
-            if kind is None:
-                monkeypatch.delenv("PNETGPU_RX_KIND", raising=False)
-            else:
-                monkeypatch.setenv("PNETGPU_RX_KIND", kind)
+            tune("rx_kind", None if kind is None else int(kind))
             res = lp.rx_process(d, stride=stride, frame_len=flen, first_offset=first, n_frames=n,
                                 columns=ALL_COLUMNS)
             torch.cuda.synchronize()
@@ -420,8 +418,8 @@ def test_idempotent_and_stream_ordered():
 
 
 @pytest.mark.parametrize("kernel", ["run", "group"])
-def test_random_slices_vs_oracle(kernel, monkeypatch):
-    monkeypatch.setenv("PNETGPU_SLICE_KERNEL", kernel)   # slice_run_kernel / slice_kernel
+def test_random_slices_vs_oracle(kernel, tune):
+    tune("slice_kernel", kernel)   # slice_run_kernel / slice_kernel
     rng = np.random.default_rng(21)
     n = 20000
     buf = rng.integers(0, 256, 1 << 22, dtype=np.uint8)
@@ -448,13 +446,13 @@ def test_random_slices_vs_oracle(kernel, monkeypatch):
 
 @pytest.mark.parametrize("kernel", ["run", "group"])
 @pytest.mark.parametrize("seed", [0, 1])
-def test_small_and_large_slices_mixed_in_runs(seed, kernel, monkeypatch):
+def test_small_and_large_slices_mixed_in_runs(seed, kernel, tune):
     """slice_run_kernel: tiny slices (0-70 B, summed by their own lane) and long
     ones (group path) interleaved in the same 64-slice runs, at every alignment,
     skipwords inside / straddling / past the slice, invalid descriptors, and a
     batch size that is not a multiple of 64; pseudo-header forms with the
     address array at a 4-B-aligned and an odd address. Both slice kernels."""
-    monkeypatch.setenv("PNETGPU_SLICE_KERNEL", kernel)
+    tune("slice_kernel", kernel)
     rng = np.random.default_rng(600 + seed)
     n = 64 * 300 + 17
     buf = rng.integers(0, 256, 1 << 21, dtype=np.uint8)
@@ -490,12 +488,12 @@ def test_small_and_large_slices_mixed_in_runs(seed, kernel, monkeypatch):
 
 @pytest.mark.parametrize("kernel", ["run", "group"])
 @pytest.mark.parametrize("short", [False, True])
-def test_random_adv_slices_vs_oracle(kernel, short, monkeypatch):
+def test_random_adv_slices_vs_oracle(kernel, short, tune):
     """*_checksum_adv (extra_data) batched: main and extra slices at every byte
     alignment, odd/even/empty extras, extras longer than one 16-lane pass; short
     main and extra slices (0-100 B: own-lane, 2- and 4-lane classes of
     slice_run_kernel, its extra range a second pass), both slice kernels."""
-    monkeypatch.setenv("PNETGPU_SLICE_KERNEL", kernel)
+    tune("slice_kernel", kernel)
     rng = np.random.default_rng(23 + short)
     n = 6000
     buf = rng.integers(0, 256, 1 << 21, dtype=np.uint8)
@@ -523,11 +521,11 @@ def test_random_adv_slices_vs_oracle(kernel, short, monkeypatch):
 
 
 @pytest.mark.parametrize("kernel", ["run", "group"])
-def test_adv_slices_match_tcp_with_options_split(kernel, monkeypatch):
+def test_adv_slices_match_tcp_with_options_split(kernel, tune):
     """A TCP segment checksummed whole equals the same segment split into a
     header slice + an even-length extra (the way tcp::ipv4_checksum_adv is used
     to checksum a header and a separately held payload)."""
-    monkeypatch.setenv("PNETGPU_SLICE_KERNEL", kernel)
+    tune("slice_kernel", kernel)
     rng = np.random.default_rng(5)
     seg = rng.integers(0, 256, 1000, dtype=np.uint8)
     buf = np.concatenate([np.zeros(3, np.uint8), seg, np.zeros(64, np.uint8)])
@@ -815,11 +813,8 @@ def test_compact_slices_kats_and_random_vs_oracle():
     desc = lp.slice_descriptors(offs, lens, skips, device=DEV)
     d = to_dev(np.concatenate([buf, np.zeros(32, np.uint8)]))[: buf.size]
     for kern in ("run", "group"):
-        os.environ["PNETGPU_SLICE_KERNEL"] = kern
-        try:
+        with lp.engine.tuning(0, slice_kernel=kern):
             got = lp.checksum_slices_compact(d, desc).cpu().numpy().view(np.uint16)
-        finally:
-            del os.environ["PNETGPU_SLICE_KERNEL"]
         assert np.array_equal(got, want), kern
     big = np.full(70000, 7, np.uint8)                     # the compact maximum: 65535-B slices
     desc = lp.slice_descriptors([0, 1, 4465], [65535, 65535, 65535], [0, 3, 32767], device=DEV)
@@ -831,7 +826,7 @@ def test_compact_slices_kats_and_random_vs_oracle():
 
 @pytest.mark.parametrize("span", ["0", None])
 @pytest.mark.parametrize("seed", [0, 1, 2])
-def test_dense_runs_of_packed_slices(seed, span, monkeypatch):
+def test_dense_runs_of_packed_slices(seed, span, tune):
     """slice_run_kernel's dense-run path: runs of 64 sorted small slices packed
     in a span of at most 5 KiB arrive as coalesced loads into LDS. Packed
     slices (0..64 B, gaps 0..k), every alignment, and runs that must fall back
@@ -839,10 +834,10 @@ def test_dense_runs_of_packed_slices(seed, span, monkeypatch):
     0 or the last lane empty, a slice past the buffer, a slice ending after
     the last one's end, a final partial run. Full and compact descriptors,
     ipv4/ipv6 pseudo-header forms, against the oracle; with every eligible run
-    staged (PNETGPU_SLICE_DENSE_SPAN=0) and with the default span threshold."""
+    staged (slice_dense_span 0) and with the default span threshold."""
     if span is not None:
-        monkeypatch.setenv("PNETGPU_SLICE_DENSE_SPAN", span)
-    monkeypatch.setenv("PNETGPU_SLICE_KERNEL", "run")
+        tune("slice_dense_span", int(span))
+    tune("slice_kernel", "run")
     rng = np.random.default_rng(900 + seed)
     n = 64 * 200 + 23
     maxgap = (0, 4, 20)[seed]
@@ -896,7 +891,7 @@ def test_dense_runs_of_packed_slices(seed, span, monkeypatch):
 
 
 @pytest.mark.parametrize("seed", [0, 1, 2])
-def test_runs_of_small_slices_vs_oracle(seed, monkeypatch):
+def test_runs_of_small_slices_vs_oracle(seed, tune):
     """slice_run_kernel on runs whose 64 slices are all small (each summed by its
     own lane): short slices at every alignment with the skipped word inside /
     straddling / past the slice, empty and out-of-bounds descriptors, batch
@@ -905,7 +900,7 @@ def test_runs_of_small_slices_vs_oracle(seed, monkeypatch):
     between them; 16-B and compact descriptors, against the oracle. (Written
     for a two-runs-at-once variant, measured slower and not kept:
     profiles/r03/slices/ab_run_pairs.txt.)"""
-    monkeypatch.setenv("PNETGPU_SLICE_KERNEL", "run")
+    tune("slice_kernel", "run")
     rng = np.random.default_rng(900 + seed)
     n = 64 * (201 + 2 * seed) + 13 + seed
     buf = rng.integers(0, 256, 1 << 21, dtype=np.uint8)
@@ -937,22 +932,35 @@ def test_runs_of_small_slices_vs_oracle(seed, monkeypatch):
     assert np.array_equal(got, want_c)
 
 
+def run_desc_form(buf, offs, lens, compact, columns=RECORD_COLUMNS):
+    """rx_process over full (u64/u32) or compact (u32/u16) descriptors."""
+    if not compact:
+        return run_desc(buf, offs, lens, columns=columns)
+    res = lp.rx_process(to_dev(buf), offsets=to_dev(np.asarray(offs, np.uint32).view(np.int32)),
+                        lengths=to_dev(np.asarray(lens, np.uint16).view(np.int16)), columns=columns,
+                        flags=lp.DESC_COMPACT)
+    torch.cuda.synchronize()
+    return res
+
+
+@pytest.mark.parametrize("compact", [False, True])
 @pytest.mark.parametrize("seed", [0, 1])
-def test_descriptor_runs_of_short_frames(seed):
+def test_descriptor_runs_of_short_frames(seed, compact):
     """The mixed kernel's short-run path (every frame of a run at most 64 B: the
     small kernel's register fast path on frames realigned from their slots):
     random UDP/TCP/ICMP/IPv6 frames of 0-64 B, the <= 64-B edge frames (IHL
     0-15, short L4, IPv6), a ragged last run; then the same batch with a few
     frames moved off alignment, one 65-B frame and invalid descriptors (their
     runs take the generic parse). Every record column and the counters equal
-    the oracle's."""
+    the oracle's, with full (12-B) and compact (6-B, the ring's and the
+    bench's IMIX form) descriptors."""
     rng = np.random.default_rng(1300 + seed)
     edge = [f for f in framegen.edge_frames(rng) if len(f) <= 64]
     frames = framegen.random_frames(rng, 64 * 90 + 37, min_len=0, max_len=64)
     frames[100:100 + len(edge)] = edge
     buf, offs, lens = framegen.pack(frames, align=16)
     rec = oracle_desc(buf, offs, lens)
-    res = run_desc(buf, offs, lens, columns=RECORD_COLUMNS)
+    res = run_desc_form(buf, offs, lens, compact)
     compare(res, rec)
     assert res.counter_dict() == oracle_counters(rec, lens)
     # some runs no longer qualify: a misaligned frame, a 65-B frame, bad descriptors
@@ -963,15 +971,50 @@ def test_descriptor_runs_of_short_frames(seed):
     lens2[64 * 3 + 5] = min(int(lens2[64 * 3 + 5]), 15)
     offs2[64 * 7 + 9], lens2[64 * 7 + 9] = buf.size, 65
     offs2[64 * 11] = buf2.size + 64
-    lens2[64 * 13 + 63] = buf2.size
+    if compact:                                          # a length running past the end, in 16 bits
+        offs2[64 * 13 + 63], lens2[64 * 13 + 63] = buf2.size - 10, 65
+    else:
+        lens2[64 * 13 + 63] = buf2.size
     rec2 = oracle_desc(buf2, offs2, lens2)
-    res2 = run_desc(buf2, offs2, lens2, columns=RECORD_COLUMNS)
+    assert (rec2["status"][[64 * 11, 64 * 13 + 63]] & pyoracle.ST_DESC_INVALID).all()
+    res2 = run_desc_form(buf2, offs2, lens2, compact)
     compare(res2, rec2)
     assert res2.counter_dict() == oracle_counters(rec2, lens2)
     # any alignment: frames straddling four or five granules, runs of both kinds
     for align, gap in ((1, 0), (1, 7), (4, 0)):
         buf3, offs3, lens3 = framegen.pack(frames, align=align, gap=gap, rng=rng)
         rec3 = oracle_desc(buf3, offs3, lens3)
-        res3 = run_desc(buf3, offs3, lens3, columns=RECORD_COLUMNS)
+        res3 = run_desc_form(buf3, offs3, lens3, compact)
         compare(res3, rec3)
         assert res3.counter_dict() == oracle_counters(rec3, lens3)
+
+
+def test_slice_argument_validation():
+    """The slice entry points refuse arrays the kernels would misread (host
+    pointers, other dtypes, short arrays) and u32 arguments that would be
+    truncated, before any launch; compact descriptors on the host are copied
+    to the data's device (slice_descriptors' default) and give the same sums."""
+    rng = np.random.default_rng(31)
+    buf = rng.integers(0, 256, 4096, dtype=np.uint8)
+    d = to_dev(buf)
+    offs, lens, skips = np.arange(0, 4000, 100, dtype=np.uint64), np.full(40, 60, np.uint32), np.full(40, 2, np.uint32)
+    want = coracle.checksum_slices(buf, offs, lens, skips)
+    host_desc = lp.slice_descriptors(offs, lens, skips)                  # a CPU tensor
+    assert not host_desc.is_cuda
+    assert np.array_equal(lp.checksum_slices_compact(d, host_desc).cpu().numpy().view(np.uint16), want)
+    with pytest.raises(TypeError):
+        lp.checksum_slices_compact(d, host_desc.int())
+    do, dl, ds = to_dev(offs.astype(np.int64)), to_dev(lens.astype(np.int32)), to_dev(skips.astype(np.int32))
+    assert np.array_equal(lp.checksum_slices(d, do, dl, ds).cpu().numpy().view(np.uint16), want)
+    with pytest.raises(TypeError):
+        lp.checksum_slices(d, do.cpu(), dl, ds)
+    with pytest.raises(TypeError):
+        lp.checksum_slices(d, do, dl.long(), ds)
+    with pytest.raises(ValueError):
+        lp.checksum_slices(d, do, dl[:10], ds)
+    with pytest.raises(ValueError):
+        lp.ipv4_checksum_slices(d, do, dl, ds, to_dev(np.zeros((40, 4), np.uint8)), to_dev(np.zeros(40, np.uint8)))
+    for kw in ({"stride": 1 << 32}, {"slice_len": 1 << 32}, {"skipword": -1}):
+        args = {"stride": 20, "slice_len": 20, "skipword": 5, **kw}
+        with pytest.raises(ValueError):
+            lp.checksum_slices_strided(d, 10, args["stride"], args["slice_len"], args["skipword"])

@@ -4,12 +4,10 @@ A launch hands each persistent wave a static grid-stride share of the batch's
 runs and lets the waves claim the rest from per-launch counters. These tests
 check that every run is processed exactly once whatever the static share and
 the counter count, across ragged batch ends, every kernel kind that claims
-(small, MTU, mixed), counter-slot reuse over many launches (epochs), and
-launches of one context interleaved on two streams. Results are compared with
+(small, MTU, mixed), counter-slot reuse over many launches (epochs), the
+epoch wrap, and launches of one context interleaved on three streams. Results are compared with
 the oracle (bit-exact) and the per-launch counters with the oracle's counts.
 """
-import os
-
 import numpy as np
 import pytest
 import torch
@@ -54,71 +52,136 @@ def _oracle(w, n):
     return coracle.rx_batch(w.buf, n, offsets=w.offsets, lengths=w.lengths, nthreads=NTHREADS), w.lengths
 
 
-@pytest.fixture
-def sched_env():
-    keys = ("PNETGPU_STATIC_PCT", "PNETGPU_CLAIM_COUNTERS", "PNETGPU_BLOCKS_PER_CU")
-    old = {k: os.environ.get(k) for k in keys}
-
-    def set_(pct, nctr):
-        os.environ["PNETGPU_STATIC_PCT"] = str(pct)
-        os.environ["PNETGPU_CLAIM_COUNTERS"] = str(nctr)
-    yield set_
-    for k, v in old.items():
-        if v is None:
-            os.environ.pop(k, None)
-        else:
-            os.environ[k] = v
-
-
 @pytest.mark.parametrize("name", list(SIZES))
-def test_every_run_once_any_static_share(name, sched_env):
+def test_every_run_once_any_static_share(name, tune):
     n = SIZES[name]
     w = lp.synth.make(name, n, seed=11, corrupt_ppm=10000)
     rec, lens = _oracle(w, n)
     want = oracle_counters(rec, lens)
     dv = _Dev(w)
     if name in BLOCKS_PER_CU:
-        os.environ["PNETGPU_BLOCKS_PER_CU"] = BLOCKS_PER_CU[name]
+        tune("blocks_per_cu", BLOCKS_PER_CU[name])
     for pct, nctr in [(100, 1), (92, 32), (50, 7), (0, 64), (0, 1), (99, 3)]:
-        sched_env(pct, nctr)
+        tune("static_pct", pct)
+        tune("claim_counters", nctr)
         res = dv.run(n)
         torch.cuda.synchronize()
         compare(res, rec)
         assert res.counter_dict() == want, (pct, nctr)
 
 
-def test_counter_slots_reused_across_many_launches(sched_env):
-    """More launches than the context has counter slots: each slot is taken
-    again by a later epoch and must start from zero claims for it."""
+def test_counter_slot_reused_across_many_launches(tune):
+    """Many launches on one stream: each stamps the stream's counter slot with
+    the next epoch and must start from zero claims."""
     n = SIZES["udp64"]
     w = lp.synth.make("udp64", n, seed=12, corrupt_ppm=10000)
     rec, lens = _oracle(w, n)
     want = oracle_counters(rec, lens)
     dv = _Dev(w)
-    sched_env(90, 16)
+    tune("static_pct", 90)
+    tune("claim_counters", 16)
     results = [dv.run(n) for _ in range(150)]
     torch.cuda.synchronize()
     for i in (0, 63, 64, 65, 127, 128, 149):
         compare(results[i], rec)
     for r in results:
         assert r.counter_dict() == want
+    assert lp.engine.context(0).sched_conflicts() == 0
 
 
-def test_two_streams_one_context(sched_env):
-    """Launches of one context on two streams in flight together use distinct
-    counter slots (one per epoch)."""
-    n = SIZES["imix"]
-    w = lp.synth.make("imix", n, seed=13, corrupt_ppm=10000)
+def test_epoch_wrap_rezeroes_the_slot_in_stream_order(tune):
+    """A stream slot whose launch epoch reaches the wrap threshold is re-zeroed
+    with an async memset on the launch's own stream (no device-wide sync):
+    launches across the wrap, with no host synchronization between them,
+    every one bit-exact, and no claim ever sees a foreign epoch."""
+    n = SIZES["udp64"]
+    w = lp.synth.make("udp64", n, seed=14, corrupt_ppm=10000)
     rec, lens = _oracle(w, n)
     want = oracle_counters(rec, lens)
     dv = _Dev(w)
-    sched_env(80, 32)
-    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
-    results = []
-    for i in range(40):
-        results.append(dv.run(n, stream=s1 if i % 2 else s2))
+    tune("static_pct", 50)
+    s = torch.cuda.Stream()
+    dv.run(n, stream=s)                       # the stream owns a slot from here on
+    tune("sched_epoch", 0xFFFFFF00 - 4)       # its next epochs: ...FC, FD, FE, FF, then wrap to 1
+    results = [dv.run(n, stream=s) for _ in range(10)]
     torch.cuda.synchronize()
     for r in results:
         assert r.counter_dict() == want
+    compare(results[4], rec)
     compare(results[-1], rec)
-    compare(results[-2], rec)
+    assert lp.engine.context(0).sched_conflicts() == 0
+
+
+def test_three_streams_no_host_sync(tune):
+    """150 launches of one context spread over three streams with no host
+    synchronization in between (more launches in flight than the context
+    has counter slots): every stream claims from its own slot, every record
+    equals the oracle and no claim saw another launch's epoch. The batch has
+    exactly 8 runs per resident wave at one block per CU, so each launch
+    claims runs."""
+    n = 8 * 1024 * 64                         # 8 runs x 256 CUs x 4 waves x 64 frames
+    w = lp.synth.make("udp64", n, seed=15, corrupt_ppm=10000)
+    rec, lens = _oracle(w, n)
+    want = oracle_counters(rec, lens)
+    dv = _Dev(w)
+    tune("blocks_per_cu", 1)
+    tune("static_pct", 25)
+    tune("claim_counters", 8)
+    streams = [torch.cuda.Stream() for _ in range(3)]
+    results = [dv.run(n, stream=streams[i % 3]) for i in range(150)]
+    torch.cuda.synchronize()
+    compare(results[0], rec)
+    for i, r in enumerate(results):
+        for c, col in r.columns.items():              # the same records as the oracle-checked launch
+            assert torch.equal(col, results[0].columns[c]), (i, c)
+        assert r.counter_dict() == want, i
+    assert lp.engine.context(0).sched_conflicts() == 0
+
+
+@pytest.mark.parametrize("pct,nctr", [(0, 64), (50, 7), (92, 1)])
+def test_slice_kernels_claim_path(pct, nctr, tune):
+    """The slice kernels' claimed units (slice_run_kernel's runs of 64 slices,
+    slice_kernel's groups of 4, slice_strided_kernel's blocks of runs): one
+    resident block per CU (1024 waves) and batches of more than 8 units per
+    wave, so every launch claims; util::checksum through both descriptor
+    kernels, the compact and strided entry points and ipv4_checksum_adv,
+    bit-exact with the oracle at static shares 0, 50 and 92 %."""
+    tune("slice_blocks_per_cu", 1)
+    tune("static_pct", pct)
+    tune("claim_counters", nctr)
+    rng = np.random.default_rng(40 + pct)
+    n = 8192 * 64 + 29                        # 8 runs of 64 slices per wave, a ragged last run
+    buf = rng.integers(0, 256, 1 << 24, dtype=np.uint8)
+    lens = rng.integers(0, 120, n).astype(np.uint32)
+    big = rng.random(n) < 0.05
+    lens[big] = rng.integers(120, 1500, int(big.sum()))
+    offs = rng.integers(0, buf.size - 1600, n).astype(np.uint64)
+    skips = np.where(rng.random(n) < 0.8, rng.integers(0, 30, n), rng.integers(0, 900, n)).astype(np.uint32)
+    want = coracle.checksum_slices(buf, offs, lens, skips)
+    d = to_dev(buf)
+    do, dl, ds = to_dev(offs.astype(np.int64)), to_dev(lens.astype(np.int32)), to_dev(skips.astype(np.int32))
+    desc = lp.slice_descriptors(offs, lens, skips, device="cuda:0")
+    for kern in ("run", "group"):
+        tune("slice_kernel", kern)
+        got = lp.checksum_slices(d, do, dl, ds).cpu().numpy().view(np.uint16)
+        assert np.array_equal(got, want), kern
+        got = lp.checksum_slices_compact(d, desc).cpu().numpy().view(np.uint16)
+        assert np.array_equal(got, want), ("compact", kern)
+        eo = rng.integers(0, buf.size - 700, n).astype(np.uint64)
+        el = rng.integers(0, 600, n).astype(np.uint32)
+        addrs = rng.integers(0, 256, (n, 8), dtype=np.uint8)
+        protos = rng.integers(0, 256, n, dtype=np.uint8)
+        got = lp.checksum_adv_slices(4, d, do, dl, ds, to_dev(eo.astype(np.int64)), to_dev(el.astype(np.int32)),
+                                     to_dev(addrs), to_dev(protos)).cpu().numpy().view(np.uint16)
+        for i in list(range(0, n, 509)) + [n - 1]:
+            o, ln, e0, e1 = int(offs[i]), int(lens[i]), int(eo[i]), int(el[i])
+            assert got[i] == coracle.ipv4_checksum(bytes(buf[o:o + ln]), int(skips[i]), bytes(buf[e0:e0 + e1]),
+                                                   bytes(addrs[i, :4]), bytes(addrs[i, 4:]), int(protos[i])), i
+    tune("slice_kernel", None)
+    # uniform 20-B slices: blocks of 3 runs (192 slices) per unit, 8 units per wave
+    ns = 8 * 1024 * 192 + 77
+    sbuf = rng.integers(0, 256, ns * 20 + 3, dtype=np.uint8)
+    got = lp.checksum_slices_strided(to_dev(sbuf), ns, 20, 20, 5, first_offset=3).cpu().numpy().view(np.uint16)
+    so = 3 + 20 * np.arange(ns, dtype=np.uint64)
+    swant = coracle.checksum_slices(sbuf, so, np.full(ns, 20, np.uint32), np.full(ns, 5, np.uint32))
+    assert np.array_equal(got, swant)

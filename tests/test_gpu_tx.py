@@ -58,9 +58,9 @@ def test_tx_then_rx_all_verify_and_idempotent():
 
 
 @pytest.mark.parametrize("stride,flen", [(64, 64), (64, 60), (1514, 1514), (1500, 1400), (9018, 9018)])
-def test_tx_fill_stride_every_kernel(stride, flen, monkeypatch):
+def test_tx_fill_stride_every_kernel(stride, flen, tune):
     """Fixed-stride TX fill of random/corrupted frames through the default kernel
-    for the shape and every forced rx_kernel kind (PNETGPU_RX_KIND)."""
+    for the shape and every forced rx_kernel kind (the rx_kind tuning)."""
     rng = np.random.default_rng(stride * 7 + flen)
     n = 300
     frames = framegen.random_frames(rng, n, max_len=min(stride, 9100))
@@ -70,10 +70,7 @@ def test_tx_fill_stride_every_kernel(stride, flen, monkeypatch):
         buf[i * stride:i * stride + len(f)] = f
     want_buf, want_rec = coracle.tx_fill(buf, n, stride=stride, frame_len=flen)
     for kind in (None, "0", "2", "3"):
-        if kind is None:
-            monkeypatch.delenv("PNETGPU_RX_KIND", raising=False)
-        else:
-            monkeypatch.setenv("PNETGPU_RX_KIND", kind)
+        tune("rx_kind", None if kind is None else int(kind))
         d = to_dev(buf.copy())
         res = lp.tx_fill_checksums(d, stride=stride, frame_len=flen, n_frames=n, columns=ALL_COLUMNS)
         torch.cuda.synchronize()

@@ -293,3 +293,78 @@ def test_icmp_message_views():
                 assert view.get_unused() == int.from_bytes(p[4:8], "big")
                 assert view.from_packet()["payload"] == p[8:]
     assert seen == {"echo_request", "echo_reply", "destination_unreachable", "time_exceeded"}
+
+
+def test_minimum_packet_size_is_the_new_bound():
+    """minimum_packet_size() (decorator.rs:589-600,623-629) is the length at
+    which each view's constructor starts answering: frames cut so that the
+    Ethernet / IP / L4 buffer holds minimum - 1 and minimum bytes, through the
+    oracle's records (the reference's new() bounds)."""
+    rng = np.random.default_rng(41)
+    assert lp.views.FrameView.minimum_packet_size() == 14
+    for cut in (13, 14):
+        f = framegen.build_frame(rng, "udp", 20)[:cut]
+        assert lp.frame_view(_records([f]), 0, f).valid() == (cut >= 14)
+    for kind, version in (("udp", 4), ("udp6", 6)):
+        full = framegen.build_frame(rng, kind, 20)
+        ipmin = 20 if version == 4 else 40
+        for cut in (ipmin - 1, ipmin):
+            f = full[:14 + cut]
+            fv = lp.frame_view(_records([f]), 0, f)
+            ip = fv.ipv4() if version == 4 else fv.ipv6()
+            assert (ip is not None) == (cut >= ipmin), (kind, cut)
+            if ip is not None:
+                assert ip.minimum_packet_size() == ipmin == lp.views.MINIMUM_PACKET_SIZE[f"ipv{version}"]
+    for kind, l4min in (("udp", 8), ("tcp", 20), ("icmp", 4), ("icmp6", 4)):
+        full = framegen.build_frame(rng, kind, 40)
+        l3 = 14 + (40 if kind == "icmp6" else 20)
+        for cut in (l4min - 1, l4min):
+            f = full[:l3 + cut]                   # the L4 slice: bounded by the buffer
+            fv = lp.frame_view(_records([f]), 0, f)
+            ip = fv.ipv4() or fv.ipv6()
+            l4 = getattr(ip, kind.rstrip("6") + ("v6" if kind == "icmp6" else ""))()
+            assert (l4 is not None) == (cut >= l4min), (kind, cut)
+            if l4 is not None:
+                assert l4.minimum_packet_size() == l4min
+                assert len(l4.packet()) == cut
+
+
+def test_clone_from_and_to_immutable():
+    """MutablePacket::clone_from (packet.rs:61-72): copies the other packet's
+    bytes over the start of this one, asserting this one is at least as long;
+    to_immutable (decorator.rs:630-632): the same view, read-only."""
+    rng = np.random.default_rng(42)
+    a = bytearray(framegen.build_frame(rng, "udp", 40))
+    b = framegen.build_frame(rng, "udp", 30)
+    ra, rb = _records([bytes(a)]), _records([b])
+    ua = lp.frame_view(ra, 0, a).ipv4().udp()
+    ub = lp.frame_view(rb, 0, b).ipv4().udp()
+    before = bytes(a)
+    ua.clone_from(ub)                                       # 38 B over 48
+    off = int(ra["l4_offset"][0])
+    assert bytes(a[off:off + len(bytes(ub.packet()))]) == bytes(ub.packet())
+    assert bytes(a[off + len(bytes(ub.packet())):]) == before[off + len(bytes(ub.packet())):]
+    with pytest.raises(AssertionError):
+        ub_w = lp.frame_view(rb, 0, bytearray(b)).ipv4().udp()
+        ub_w.clone_from(ua)                                 # 48 B into 38: the reference's assert
+    fv = lp.frame_view(ra, 0, a)
+    fv.clone_from(bytes(10))                                # raw bytes as the source
+    assert bytes(a[:10]) == bytes(10)
+    imm = fv.ipv4().udp().to_immutable()
+    assert bytes(imm.packet()) == bytes(ua.packet()) and imm.get_source() == ua.get_source()
+    for call in (imm.packet_mut, imm.payload_mut, lambda: imm.clone_from(b"x")):
+        with pytest.raises(TypeError):
+            call()
+    assert fv.to_immutable().minimum_packet_size() == 14
+    frames, _ = framegen.icmp_type_frames(np.random.default_rng(31))
+    for i, f in enumerate(frames):
+        ic = lp.frame_view(_records(frames), i, bytearray(f)).ipv4()
+        ic = ic and ic.icmp()
+        echo = ic and ic.echo_request()
+        if echo:
+            assert echo.minimum_packet_size() == 8
+            with pytest.raises(TypeError):
+                echo.to_immutable().packet_mut()
+            break
+    else:
+        raise AssertionError("no echo request frame")

@@ -53,7 +53,7 @@ def main():
         times = {v: [] for v in vals}
         for _ in range(a.rounds):
             for v in vals:
-                os.environ.update(envs[v])
+                lp.engine.apply_tuning_env(envs[v], dev)   # the context reads no env per call
                 for _ in range(2):
                     sh.step(s)
                 evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.reps)]

@@ -41,7 +41,7 @@ def main():
     for _ in range(3):
         for name, n, size, fn, v in cases:
             if v is not None:
-                os.environ[env[0]] = v
+                lp.engine.apply_tuning_env({env[0]: v}, dev)
             for _ in range(2):
                 fn()
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

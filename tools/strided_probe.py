@@ -33,9 +33,8 @@ sizes = [int(x) for x in os.environ.get("PROBE_SIZES", "20,64,1024").split(",")]
 for size, n in ((z, 1 << 24 if z <= 32 else (1 << 29) // z) for z in sizes):
     for bpc, dspan in ((b, ds) for b in os.environ.get("PROBE_BPC", "0").split(",")
                        for ds in os.environ.get("PROBE_DENSE", "").split(",")):
-        os.environ["PNETGPU_SLICE_BLOCKS_PER_CU"] = bpc
-        if dspan:
-            os.environ["PNETGPU_SLICE_DENSE_SPAN"] = dspan
+        lp.engine.apply_tuning_env({"PNETGPU_SLICE_BLOCKS_PER_CU": None if bpc == "0" else bpc,
+                                    "PNETGPU_SLICE_DENSE_SPAN": dspan or None}, dev)
         print(f"blocks/CU {bpc} (0 = occupancy) dense span {dspan or 'default'}")
         d = torch.full((n * size + 32,), 99, dtype=torch.uint8, device=dev)
         offs = torch.arange(n, dtype=torch.int64, device=dev) * size

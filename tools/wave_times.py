@@ -26,7 +26,7 @@ from bench import Shard, WORKLOADS  # noqa: E402
 from libpnet_amd import _lib  # noqa: E402
 
 EXTRA = {"imix": 1 << 22, "udp6_jumbo": 1 << 17}
-SLOTS, WORDS = 16384, 10
+SLOTS, WORDS = 16384, 13
 TICK_US = 0.01   # wall_clock64: 100 MHz
 
 
@@ -76,7 +76,7 @@ def main():
         s.synchronize()
         for v, rep in [(v, r) for v in vals for r in range(a.reps)]:
             if key:
-                os.environ[key] = v
+                lp.engine.apply_tuning_env({key: v}, dev)
                 if rep == 0:
                     print(f"-- {key}={v}", flush=True)
                     sh.step(s)
@@ -120,6 +120,11 @@ def main():
                     print(f"{'':10s} per run (us, mean over waves; s_memtime {np.median(mhz):.0f} MHz): " +
                           "  ".join(f"{nm} {ph[:, i].mean():.2f}" for i, nm in enumerate(names)) +
                           f"  total {ph.sum(1).mean():.2f} ({dur.mean() / runs.mean():.2f} wall)", flush=True)
+                tu, tsl, tid = (int(t[:, k].astype(np.int64).sum()) for k in (10, 11, 12))
+                if tsl:
+                    print(f"{'':10s} tail makespan: group-rounds issued {tu}, slots {tsl} (used {tu / tsl:.1%}); "
+                          f"a perfect split needs {tid} slots ({tid / tsl:.1%} of the rounds), "
+                          f"{tu / runs.sum():.1f} group-rounds per run", flush=True)
                 per = []
                 for x in range(8):
                     m = xcc == x
