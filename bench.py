@@ -278,17 +278,29 @@ def config0_block(steps, warmup, device):
     return out
 
 
-def e2e_rate(sh, device, chunks=16, reps=3):
+def _link(frames, el, up, down):
+    """The PCIe link's share of an e2e line: bytes each frame moves up (frame +
+    descriptors) and down (its record columns), and the link rate that implies,
+    so lines with different records compare on the same link."""
+    return {"link_bytes_per_frame": {"up": round(up, 2), "down": round(down, 2), "total": round(up + down, 2)},
+            "link_gb_s": round(frames * (up + down) / el / 1e9, 2)}
+
+
+VERIFY_COLUMNS = ("status", "ip_csum", "l4_csum")
+
+
+def e2e_rate(sh, device, chunks=16, reps=3, columns=None):
     """PCIe-inclusive rate: pinned host frames -> H2D -> kernel -> D2H of the results,
     double-buffered on two streams. Reported beside `value`, never as `value`."""
     if not sh.w.stride:
         return None
+    columns = columns or lp.IPV4_COLUMNS
     n, stride = sh.n, sh.w.stride
     host = torch.from_numpy(sh.w.buf[: n * stride]).pin_memory()
     per = n // chunks
     streams = [torch.cuda.Stream(device), torch.cuda.Stream(device)]
     dbuf = [torch.empty(per * stride + 32, dtype=torch.uint8, device=device) for _ in range(2)]
-    res = [lp.RxResult(per, device, lp.IPV4_COLUMNS, counters=False) for _ in range(2)]
+    res = [lp.RxResult(per, device, columns, counters=False) for _ in range(2)]
     hout = [torch.empty(r.nbytes, dtype=torch.uint8).pin_memory() for r in res]
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -302,15 +314,25 @@ def e2e_rate(sh, device, chunks=16, reps=3):
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     frames = reps * chunks * per
+    rb = lp.engine.column_bytes(columns)
     return {"mpkts_s": round(frames / el / 1e6, 1), "gb_s": round(frames * stride / el / 1e9, 2),
-            "note": "pinned host batch -> hipMemcpyAsync H2D -> rx kernel -> one D2H of the packed IPV4 record "
-                    f"columns (26 B/frame), {chunks} chunks double-buffered on 2 streams"}
+            **_link(frames, el, stride, res[0].nbytes / per),
+            "note": "pinned host batch -> hipMemcpyAsync H2D -> rx kernel -> one D2H of the packed record "
+                    f"columns ({rb} B/frame: {', '.join(columns)}), {chunks} chunks double-buffered on 2 streams"}
 
 
-def e2e_ring_rate(sh, seconds=3.0):
+def _ring_link(frames, nbytes, el, rb, nbatches):
+    # up: the frames plus their descriptors (compact, 6 B, for these batches:
+    # ring.cpp ships them whenever a batch qualifies); down: the record
+    # columns plus 64 B of counters per batch
+    return _link(frames, el, nbytes / frames + 6, rb + 64 * nbatches / frames)
+
+
+def e2e_ring_rate(sh, seconds=3.0, columns=None):
     """Producer-inclusive rate: frames copied into the pinned ring
     (pnetgpu_ring_push_many: the DataLinkReceiver::next() consumer), shipped,
-    verified and every record column copied back (three rotating slots)."""
+    verified and the record columns copied back (three rotating slots)."""
+    columns = columns or lp.IPV4_COLUMNS
     w = sh.w
     n = min(sh.n, 1 << 22)
     if w.stride:
@@ -318,31 +340,35 @@ def e2e_ring_rate(sh, seconds=3.0):
         lens = np.full(n, w.frame_len, dtype=np.uint32)
     else:
         offs, lens = w.offsets[:n], w.lengths[:n]
-    ring = lp.Ring(batch_bytes=64 << 20, batch_frames=1 << 20, copy=False)
-    frames = 0
-    nbytes = 0
+    ring = lp.Ring(batch_bytes=64 << 20, batch_frames=1 << 20, copy=False, columns=columns)
+    frames = nbytes = nb = 0
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < seconds:
         for b in ring.feed_many(w.buf, offs, lens):
             frames += b.n
             nbytes += int(b.lengths.sum())
+            nb += 1
             del b
     for b in ring.drain():
         frames += b.n
         nbytes += int(b.lengths.sum())
+        nb += 1
     el = time.perf_counter() - t0
     ring.close()
+    rb = lp.engine.column_bytes(columns)
     return {"mpkts_s": round(frames / el / 1e6, 1), "gb_s": round(nbytes / el / 1e9, 2),
+            **_ring_link(frames, nbytes, el, rb, nb),
             "note": "host frames pushed into the pinned ring with pnetgpu_ring_push_many (descriptors and "
-                    "source-adjacent frame copies split over up to 8 host threads), async H2D -> rx kernel -> D2H of all 16 result "
-                    "columns, 3 rotating slots of 1 Mi frames"}
+                    "source-adjacent frame copies split over up to 8 host threads), async H2D -> rx kernel -> D2H of "
+                    f"the record columns ({rb} B/frame: {', '.join(columns)}), 3 rotating slots of 1 Mi frames"}
 
 
-def e2e_zero_copy_rate(sh, seconds=3.0):
+def e2e_zero_copy_rate(sh, seconds=3.0, columns=None):
     """Zero-copy producer: the host frames stay where they are (a registered
     buffer, as an mmap'd pcap file or AF_PACKET ring would be) and each batch is
     one DMA of their span (pnetgpu_ring_submit_region), verified, and every
     record column copied back (three rotating slots)."""
+    columns = columns or lp.IPV4_COLUMNS
     w = sh.w
     n = min(sh.n, 1 << 22)
     if w.stride:
@@ -354,25 +380,29 @@ def e2e_zero_copy_rate(sh, seconds=3.0):
         span = int(offs[-1] + lens[-1])
     buf = w.buf[:span]
     reg = lp.HostRegistration(buf)
-    ring = lp.Ring(batch_bytes=64 << 20, batch_frames=1 << 20, copy=False, columns=lp.IPV4_COLUMNS)
-    frames = nbytes = 0
+    ring = lp.Ring(batch_bytes=64 << 20, batch_frames=1 << 20, copy=False, columns=columns)
+    frames = nbytes = nb = 0
     t0 = time.perf_counter()
     try:
         while time.perf_counter() - t0 < seconds:
             for b in ring.feed_region(buf, offs, lens):
                 frames += b.n
                 nbytes += int(b.lengths.sum())
+                nb += 1
                 del b
         for b in ring.drain():
             frames += b.n
             nbytes += int(b.lengths.sum())
+            nb += 1
         el = time.perf_counter() - t0
     finally:
         ring.close()
         reg.close()
+    rb = lp.engine.column_bytes(columns)
     return {"mpkts_s": round(frames / el / 1e6, 1), "gb_s": round(nbytes / el / 1e9, 2),
+            **_ring_link(frames, nbytes, el, rb, nb),
             "note": "frames DMA'd straight from a registered host buffer (pnetgpu_ring_submit_region, no copy into "
-                    "the ring), rx kernel, D2H of the 12 IPv4 record columns (26 B/frame, "
+                    f"the ring), rx kernel, D2H of the record columns ({rb} B/frame: {', '.join(columns)}; "
                     "pnetgpu_ring_set_columns), 3 rotating slots of 1 Mi frames"}
 
 
@@ -818,9 +848,13 @@ def main():
                 line["workloads"]["tcp1500"]["ipv4_checksum_slices"] = slices_rate(results["tcp1500"]["sh"], args.steps,
                                                                                    args.warmup, device)
         if world == 1 and not args.no_e2e:
+            # every e2e line ships the same 26-B IPv4 record, so they differ only
+            # in the producer; the verify-only line (status + both checksums,
+            # 6 B/frame back) shows the H2D-bound rate
             line["e2e_pcie"] = e2e_rate(sh, device)
             line["e2e_ring"] = e2e_ring_rate(sh)
             line["e2e_zero_copy"] = e2e_zero_copy_rate(sh)
+            line["e2e_pcie_verify"] = e2e_rate(sh, device, columns=VERIFY_COLUMNS)
         print(json.dumps(line), flush=True)
     if dist_on:
         torch.distributed.barrier()
