@@ -413,7 +413,8 @@ __global__ __launch_bounds__(kBlock, NW < 8 ? 5 : 4) void rx_kernel(RxArgs a) {
             uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, kWave - 1);
             uint32_t per = 1, mine = rounds;
             if (total > (uint32_t)kMaxItems) {
-                per = (total + kMaxItems - 1) / kMaxItems;
+                // sum of ceil(rounds / per) <= total / per + 64 <= kMaxItems
+                per = (total + (kMaxItems - kWave) - 1) / (kMaxItems - kWave);
                 mine = (rounds + per - 1) / per;
                 incl = wave_incl_scan(mine);
                 total = (uint32_t)__builtin_amdgcn_readlane((int)incl, kWave - 1);
