@@ -122,18 +122,22 @@ __device__ __forceinline__ void rotate_prio(uint32_t step) {
 // [nstatic, nruns); 32 consecutive wave ids are 8 blocks, which the dispatcher
 // spreads over the 8 XCDs, so every counter balances work across them),
 // one claim kept in flight ahead of its use so the atomic's round trip
-// overlaps a whole run. take() returns the next run; >= nruns ends the loop.
+// overlaps a whole run: claim() issues the atomic, and its value is read
+// (and waited for) only at the next take(). take() returns the next run;
+// >= nruns ends the loop.
 struct RunQueue {
     uint64_t next_static, stride, nstatic, nruns, lo, hi;
     unsigned long long* ctr;
     unsigned long long* conflicts;
     uint64_t pend;          // claimed ahead (dynamic phase), nruns when none is pending
     uint32_t epoch;
-    bool stamped;
+    uint32_t kraw, kepoch;  // lane 0: the in-flight claim's count and epoch
+    bool stamped, inflight;
 
     __device__ RunQueue(const RunSched& s, uint64_t n_units, uint64_t wave_id, uint64_t wave_stride)
         : next_static(wave_id), stride(wave_stride), nstatic(s.ctr ? s.nstatic : n_units), nruns(n_units), lo(0),
-          hi(0), ctr(s.ctr), conflicts(s.conflicts), pend(n_units), epoch(s.epoch), stamped(false) {
+          hi(0), ctr(s.ctr), conflicts(s.conflicts), pend(n_units), epoch(s.epoch), kraw(0), kepoch(0),
+          stamped(false), inflight(false) {
         if (ctr) {
             const uint64_t h = (wave_id >> 5) % s.nctr, d = nruns - nstatic;
             lo = nstatic + d * h / s.nctr;
@@ -143,7 +147,6 @@ struct RunQueue {
         }
     }
     __device__ void claim() {
-        uint32_t k = 0;
         if (__lane_id() == 0) {
             if (!stamped) {
                 // the slot may hold an earlier launch's count: lift it to this
@@ -152,13 +155,20 @@ struct RunQueue {
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             }
             const unsigned long long old = atomicAdd(ctr, 1ull);
-            k = (uint32_t)old;
-            // another launch stamped this stream's slot while this one runs:
-            // claims may be shared, so the host hears of it (never silent)
-            if ((uint32_t)(old >> 32) != epoch && conflicts) atomicAdd(conflicts, 1ull);
+            kraw = (uint32_t)old;
+            kepoch = (uint32_t)(old >> 32);
         }
         stamped = true;
-        const uint64_t r = lo + (uint64_t)__builtin_amdgcn_readfirstlane(k);
+        inflight = true;
+    }
+    // the in-flight claim's run (waits for the atomic's return)
+    __device__ void resolve() {
+        if (!inflight) return;
+        inflight = false;
+        // another launch stamped this stream's slot while this one runs:
+        // claims may be shared, so the host hears of it (never silent)
+        if (__lane_id() == 0 && kepoch != epoch && conflicts) atomicAdd(conflicts, 1ull);
+        const uint64_t r = lo + (uint64_t)__builtin_amdgcn_readfirstlane(kraw);
         pend = r < hi ? r : nruns;
     }
     __device__ uint64_t take() {
@@ -168,6 +178,7 @@ struct RunQueue {
             if (ctr && next_static >= nstatic) claim();   // last static run: the first claim goes out
             return r;
         }
+        resolve();
         const uint64_t r = pend;
         if (r < nruns) claim();
         return r;
