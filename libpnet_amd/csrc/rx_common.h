@@ -477,6 +477,47 @@ __device__ __forceinline__ void tx_write(uint8_t* frame, const Parsed& P, uint32
     }
 }
 
+// TX through the frame's LDS window (rx_kernel): the window copy is patched,
+// then each aligned 16-B granule holding a checksum field is stored whole
+// (one dwordx4 store) when it lies inside the frame and the window; a field
+// outside that (short frames, fields straddling a granule, fields past the
+// window) gets byte stores. A granule inside the frame holds only this frame's
+// bytes (frames of a TX batch do not overlap), unchanged since the window was
+// loaded except for the patched field. `fb` is the frame's aligned base
+// (granule 0 of the window), `sh` the frame's offset in it.
+#ifndef PNET_TX_GRANULES
+#define PNET_TX_GRANULES 0   // A/B: 1 = granule stores from the window, 0 = byte stores (tx_write)
+#endif
+__device__ __forceinline__ void tx_write_window(uint8_t* fb, uint8_t* slot, int sh, uint32_t len, int kwin,
+                                                const Parsed& P, uint32_t ipc, uint32_t l4c) {
+    int pos[2];
+    uint32_t val[2];
+    int nf = 0;
+    if (P.is_v4) { pos[nf] = sh + (int)P.l3 + 10; val[nf++] = ipc; }
+    if (P.st & PNET_ST_L4_CSUM_DONE) { pos[nf] = sh + P.l4csum_at; val[nf++] = l4c; }
+    for (int k = 0; k < nf; ++k) {
+        if (pos[k] + 2 <= kwin) {
+            slot[pos[k]] = (uint8_t)(val[k] >> 8);
+            slot[pos[k] + 1] = (uint8_t)val[k];
+        }
+    }
+    int stored = -1;
+    for (int k = 0; k < nf; ++k) {
+        const int p = pos[k], g = p >> 4;
+        const bool whole = ((p + 1) >> 4) == g && 16 * g >= sh && 16 * g + 16 <= sh + (int)len && 16 * g + 16 <= kwin;
+        if (whole) {
+            if (g != stored) {
+                const uint32_t* s32 = reinterpret_cast<const uint32_t*>(slot + 16 * g);
+                *reinterpret_cast<uint4*>(fb + 16 * g) = make_uint4(s32[0], s32[1], s32[2], s32[3]);
+                stored = g;
+            }
+        } else {
+            fb[p] = (uint8_t)(val[k] >> 8);
+            fb[p + 1] = (uint8_t)val[k];
+        }
+    }
+}
+
 // Per-wave counters (ballots: wave-uniform) and coalesced column stores.
 struct Counters {
     uint32_t frames = 0, v4 = 0, v6 = 0, ipbad = 0, l4bad = 0, malf = 0, unk = 0;

@@ -482,7 +482,12 @@ __global__ __launch_bounds__(kBlock, NW < 8 ? 5 : 4) void rx_kernel(RxArgs a) {
             finalize(P, tA, tB, (off & 1) != 0, ipc, l4c);
         }
         PNET_PH(2);   // probe: parse, window sums, tail trims, finalize
-        if (TX && in_batch && !desc_bad) tx_write(const_cast<uint8_t*>(a.data) + off, P, ipc, l4c);
+        if (TX && in_batch && !desc_bad) {
+            if (PNET_TX_GRANULES)
+                tx_write_window(const_cast<uint8_t*>(a.data) + base, slot, sh, len, kWin, P, ipc, l4c);
+            else
+                tx_write(const_cast<uint8_t*>(a.data) + off, P, ipc, l4c);
+        }
         store_columns(a.cols, f0, lane, in_batch, P, ipc, l4c, slot, sh);
 #ifndef PNET_NO_FIELD_COLUMNS   // A/B: the header-field stores compiled out
         if (EXT && a.field_cols && in_batch)   // header-field columns: EXT instantiations only

@@ -242,13 +242,25 @@ __global__ __launch_bounds__(kBlock, PNET_SMALL_WAVES) void rx_small_kernel(RxAr
             // lines instead of four scattered byte stores per frame, which left
             // every line of the batch partially dirty (0.63 ms -> see DESIGN.md)
             if (in_batch) tx_write(slot, P, ipc, l4c);
+#ifdef PNET_SMALL_TX_PARTIAL
+            // A/B: write back only the granules holding a patched field
+            // (granule 1: the IPv4 checksum; the L4 field's granule)
+            __shared__ uint8_t txm[kWavesPerBlock][kWave];
+            txm[wv][lane] = (uint8_t)((P.is_v4 ? 1u << ((P.l3 + 10) >> 4) | 1u << ((P.l3 + 11) >> 4) : 0u) |
+                                      ((P.st & PNET_ST_L4_CSUM_DONE) ? 1u << (P.l4csum_at >> 4) |
+                                                                      1u << ((P.l4csum_at + 1) >> 4) : 0u));
+#endif
             wave_sync();
             const uint32_t span = (a.frame_len + 15u) >> 4;
             const uint32_t c = (uint32_t)(lane & 3);
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 const uint64_t f = f0 + 16 * i + (lane >> 2);
+#ifdef PNET_SMALL_TX_PARTIAL
+                if (f < a.n && c < span && ((txm[wv][16 * i + (lane >> 2)] >> c) & 1u)) {
+#else
                 if (f < a.n && c < span) {
+#endif
                     const uint4 v = *reinterpret_cast<const uint4*>(lds_slots[wv] + (16 * i + (lane >> 2)) * kSmallSlot +
                                                                     16 * c);
                     __builtin_nontemporal_store(u32x4_t{v.x, v.y, v.z, v.w},
