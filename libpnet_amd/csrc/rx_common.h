@@ -160,6 +160,9 @@ struct RunQueue {
         }
         stamped = true;
         inflight = true;
+#ifdef PNET_CLAIM_EAGER   // A/B: the round-3 claim, waited for where it is made
+        resolve();
+#endif
     }
     // the in-flight claim's run (waits for the atomic's return)
     __device__ void resolve() {
