@@ -251,9 +251,7 @@ void pnetgpu_ctx_destroy(pnetgpu_ctx* ctx);
 #define PNETGPU_TUNE_SCHED_EPOCH         8  /* test hook: raise every stream slot's launch epoch to at least
                                              * this (0..2^32-1), so a test reaches the epoch wrap, where the
                                              * slot is re-zeroed in stream order                             */
-#define PNETGPU_TUNE_SMALL_DMA           9  /* 64-B-class batches: 1 stage frames by LDS-DMA
-                                             * (rx_small_dma_kernel), 0 register-staged (rx_small_kernel) */
-#define PNETGPU_NTUNE                    10
+#define PNETGPU_NTUNE                    9
 int pnetgpu_ctx_set_tuning(pnetgpu_ctx* ctx, int key, int64_t value);
 int pnetgpu_ctx_get_tuning(const pnetgpu_ctx* ctx, int key, int64_t* value);
 

@@ -83,9 +83,6 @@ constexpr int kRunFrames = 64;      // frames per wave-run
 #ifndef PNET_CLAIM_COUNTERS
 #define PNET_CLAIM_COUNTERS 64
 #endif
-#ifndef PNET_SMALL_DMA_DEFAULT
-#define PNET_SMALL_DMA_DEFAULT 0   // rx_small_dma_kernel for plain 64-B-class records (A/B: tuning SMALL_DMA)
-#endif
 
 // Run scheduling of a persistent-grid launch (RunSched): a static grid-stride
 // share, then claimed units, so that waves whose share ran slow (the younger
@@ -134,7 +131,7 @@ const char* const kTuneEnv[PNETGPU_NTUNE] = {"PNETGPU_RX_KIND",        "PNETGPU_
                                              "PNETGPU_STATIC_PCT",     "PNETGPU_CLAIM_COUNTERS",
                                              "PNETGPU_SLICE_BLOCKS_PER_CU", "PNETGPU_SLICE_KERNEL",
                                              "PNETGPU_SLICE_DENSE_SPAN",    "PNETGPU_DEBUG",
-                                             "PNETGPU_SCHED_EPOCH",         "PNETGPU_SMALL_DMA"};
+                                             "PNETGPU_SCHED_EPOCH"};
 
 bool tuning_valid(int key, int64_t v) {
     if (v == -1) return true;   // the default
@@ -148,7 +145,6 @@ bool tuning_valid(int key, int64_t v) {
     case PNETGPU_TUNE_SLICE_DENSE_SPAN: return v >= 0 && v <= 65536;
     case PNETGPU_TUNE_DEBUG: return v == 0 || v == 1;
     case PNETGPU_TUNE_SCHED_EPOCH: return v >= 0 && v <= (int64_t)UINT32_MAX;
-    case PNETGPU_TUNE_SMALL_DMA: return v == 0 || v == 1;
     default: return false;
     }
 }
@@ -334,13 +330,6 @@ static int rx_common(pnetgpu_ctx* ctx, const pnetgpu_batch* b, const pnetgpu_rx_
     const bool debug = tuning(ctx, PNETGPU_TUNE_DEBUG) > 0;
     const int64_t kind_v = tuning(ctx, PNETGPU_TUNE_RX_KIND);
     if (kind_v >= 0 && kind != pnetgpu::kKindSmall) kind = (int)kind_v;
-    // the small batches' LDS-DMA kernel: plain records only (the slot stays
-    // rotated: no TX write-back, header fields or IPv6 addresses)
-    if (kind == pnetgpu::kKindSmall && !tx && !a.field_cols && !cols->src_ipv6 && !cols->dst_ipv6 &&
-        b->frame_len >= 1) {
-        const int64_t dma = tuning(ctx, PNETGPU_TUNE_SMALL_DMA);
-        if (dma >= 0 ? dma == 1 : PNET_SMALL_DMA_DEFAULT) kind = pnetgpu::kKindSmallDma;
-    }
     const int ext = rxf != 0 || a.field_cols;   // the EXT instantiations (launch_rx)
     int& per_cu_cached = ctx->per_cu[kind & 7][ext];
     if (per_cu_cached <= 0 || debug) {                             // first use of this kernel on ctx

@@ -17,9 +17,6 @@ namespace {
 // ============================================================================
 // rx_kernel: generic (descriptor mode, any alignment, any length).
 // ============================================================================
-#ifndef PNET_HYBRID
-#define PNET_HYBRID 0   // A/B: long frames streamed whole by the tail items (no window loads for them)
-#endif
 #ifndef PNET_TAIL_SPLIT
 #define PNET_TAIL_SPLIT 1   // the mixed shape's tail cut into round-sized items (A/B: 0, whole frames)
 #endif
@@ -169,11 +166,7 @@ __device__ __forceinline__ void tail_sums(const uint8_t* data, WaveLds<NW, IT>& 
 // over several groups and the phase ends after about ceil(rounds / groups)
 // rounds instead of the longest frame's rounds (whole frames per group used
 // 58.5 % of the group-round slots on IMIX, tools/wave_times.py).
-// HYB (A/B): a frame longer than the window is streamed whole by the items
-// (from granule 0, its first NW granules dropped into its slot, not summed):
-// the window phase loads only the short frames, so the line a long frame's
-// window shares with its tail is fetched once.
-template <int NW, int G, int U, bool NT, bool HYB>
+template <int NW, int G, int U, bool NT>
 __device__ __forceinline__ void tail_items(const uint8_t* data, WaveLds<NW, true>& L, int lane, int count,
                                            uint32_t round_granules
 #ifdef PNET_WAVE_TIMES
@@ -191,7 +184,7 @@ __device__ __forceinline__ void tail_items(const uint8_t* data, WaveLds<NW, true
         fl = (int)(it & 63u);
         fe = L.end[fl];
         fb = data + L.base[fl];
-        const uint32_t cbeg = (HYB ? 0u : (uint32_t)NW) + (it >> 6) * round_granules;
+        const uint32_t cbeg = (uint32_t)NW + (it >> 6) * round_granules;
         cend = min(cbeg + round_granules, (fe + 15u) >> 4);
         c0 = cbeg + (uint32_t)j;
     };
@@ -215,13 +208,6 @@ __device__ __forceinline__ void tail_items(const uint8_t* data, WaveLds<NW, true
             for (int u = 0; u < U; ++u) {
                 const uint32_t c = c0 + u * G;
                 uint32_t x = v[u].x, y = v[u].y, z = v[u].z, w = v[u].w;
-                if (HYB && c < (uint32_t)NW) {                   // window granule -> the frame's slot
-                    if (c < cend) {
-                        uint32_t* dst = reinterpret_cast<uint32_t*>(L.win + fl * WaveLds<NW, true>::kSlot + 16 * c);
-                        dst[0] = x; dst[1] = y; dst[2] = z; dst[3] = w;
-                    }
-                    continue;
-                }
                 const int hi = (int)fe - (int)(16u * c);
                 if (hi < 16) {                                   // the frame's last granule
                     x &= first_bytes(clamp04(hi));
@@ -276,7 +262,6 @@ __global__ __launch_bounds__(kBlock, NW < 8 ? 5 : 4) void rx_kernel(RxArgs a) {
     static_assert(G == 2 || G == 4 || G == 8 || G == 16 || G == 32 || G == 64, "tail group");
     // the mixed shape splits its tail into round-sized items (tail_items)
     constexpr bool kItems = PNET_TAIL_SPLIT && PASS == 0 && DYN;
-    constexpr bool kHybrid = kItems && PNET_HYBRID;
     constexpr int kSlot = WaveLds<NW, kItems>::kSlot;
     constexpr int kWin = NW * 16;
     // runs of short aligned frames take the small kernel's fast path (the
@@ -355,7 +340,6 @@ __global__ __launch_bounds__(kBlock, NW < 8 ? 5 : 4) void rx_kernel(RxArgs a) {
         const bool long_frame = fend > (uint32_t)kWin;
         L.base[lane] = base;
         L.end[lane] = span < (uint32_t)NW ? span : (uint32_t)NW;   // granules to load into the window
-        if (kHybrid && long_frame) L.end[lane] = 0;                 // streamed whole by the tail items
         wave_sync();
 
         // short run (descriptor batches of minimum-size frames: the AF_PACKET /
@@ -424,7 +408,7 @@ __global__ __launch_bounds__(kBlock, NW < 8 ? 5 : 4) void rx_kernel(RxArgs a) {
             // frame order; a run with more than kMaxItems rounds takes R rounds
             // per item (wave-uniform)
             constexpr uint32_t kRound = (uint32_t)(G * U);
-            const uint32_t rounds = has_tail ? (span - (kHybrid ? 0u : (uint32_t)NW) + kRound - 1) / kRound : 0u;
+            const uint32_t rounds = has_tail ? (span - (uint32_t)NW + kRound - 1) / kRound : 0u;
             uint32_t incl = wave_incl_scan(rounds);
             uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, kWave - 1);
             uint32_t per = 1, mine = rounds;
@@ -442,7 +426,7 @@ __global__ __launch_bounds__(kBlock, NW < 8 ? 5 : 4) void rx_kernel(RxArgs a) {
             }
             if (lane == 0) L.qhead = kWave / G;
             wave_sync();
-            tail_items<NW, G, U, NT, kHybrid>(a.data, L, lane, (int)total, per * kRound PNET_TAIL_STAT);
+            tail_items<NW, G, U, NT>(a.data, L, lane, (int)total, per * kRound PNET_TAIL_STAT);
           }
         } else if (tmask) {
             // DYN: frames needing more than one group round go first

@@ -81,9 +81,6 @@ constexpr int kKindMixed = 0;
 constexpr int kKindSmall = 1;
 constexpr int kKindMtu = 2;
 constexpr int kKindJumbo = 3;
-// the small kernel's batches with frames staged by LDS-DMA (rx_small_dma_kernel):
-// plain records (no TX, header-field or IPv6-address columns), frame_len >= 1
-constexpr int kKindSmallDma = 4;
 
 // Tuning probe (tools/wave_times.py; built only as a variant library with
 // -DPNET_WAVE_TIMES, never in the shipped one): every wave of a receive launch

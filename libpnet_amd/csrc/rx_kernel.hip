@@ -114,7 +114,6 @@ template <bool EXT, bool TX>
 const void* pick_fn(int kind) {
     switch (kind) {
     case kKindSmall: return reinterpret_cast<const void*>(rx_small_kernel<TX, EXT>);
-    case kKindSmallDma: return reinterpret_cast<const void*>(rx_small_dma_kernel<PNET_DMA_STEPS>);
     case kKindMtu: return reinterpret_cast<const void*>(rx_kernel<8, PNET_MTU_CFG, EXT, TX>);
     case kKindJumbo: return reinterpret_cast<const void*>(PNET_JUMBO_FN(EXT, TX));
     default: return reinterpret_cast<const void*>(PNET_MIXED_FN(EXT, TX));
@@ -126,9 +125,6 @@ void launch_t(const RxArgs& args, int kind, int blocks, hipStream_t stream) {
     switch (kind) {
     case kKindSmall:
         hipLaunchKernelGGL((rx_small_kernel<TX, EXT>), dim3(blocks), dim3(kBlock), 0, stream, args);
-        break;
-    case kKindSmallDma:   // plain records only (abi.cpp): never TX / EXT
-        hipLaunchKernelGGL((rx_small_dma_kernel<PNET_DMA_STEPS>), dim3(blocks), dim3(kBlock), 0, stream, args);
         break;
     case kKindMtu:
         hipLaunchKernelGGL((rx_kernel<8, PNET_MTU_CFG, EXT, TX>), dim3(blocks), dim3(kBlock), 0, stream, args);
@@ -177,12 +173,10 @@ const char* rx_kernel_name(int kind, bool ext, bool tx) {
     static const char* const jumbo[4] = PNET_NAMES("rx_kernel<8, " PNET_STR(PNET_JUMBO_CFG));
     static const char* const small[4] = {"rx_small_kernel<false, false>", "rx_small_kernel<true, false>",
                                          "rx_small_kernel<false, true>", "rx_small_kernel<true, true>"};
-    static const char* const small_dma = "rx_small_dma_kernel<" PNET_STR(PNET_DMA_STEPS) ">";
 #undef PNET_NAMES
     const int i = (ext ? 2 : 0) + (tx ? 1 : 0);
     switch (kind) {
     case kKindSmall: return small[i];
-    case kKindSmallDma: return small_dma;
     case kKindMtu: return mtu[i];
     case kKindJumbo: return jumbo[i];
     default: return mixed[i];

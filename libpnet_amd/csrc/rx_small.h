@@ -285,165 +285,5 @@ __global__ __launch_bounds__(kBlock, PNET_SMALL_WAVES) void rx_small_kernel(RxAr
     PNET_WT_END((uint64_t)blockIdx.x * kWavesPerBlock + wv);
 }
 
-// ============================================================================
-// rx_small_dma_kernel: the small kernel's batches, frames staged by LDS-DMA.
-// ============================================================================
-// Each wave keeps S runs of 64 frames in flight as LDS-DMA transfers
-// (global_load_lds_dwordx4, non-temporal: no VGPR holds a frame until it is
-// read), into an S-slot ring of the small kernel's rotated 64-B slots: lane L
-// of DMA instruction i stages granule ((L & 3) - (L >> 4)) & 3 of frame
-// 16 i + L / 4 into slot granule L & 3 — the DMA writes LDS lane-linearly, so
-// the rotation is done on the source address. A run is read once a counted
-// vmcnt shows its four transfers landed (loads, stores and atomics retire in
-// issue order; MI355X_MICROARCH.md), then processed exactly as in
-// rx_small_kernel. Plain records only (no TX, header-field or IPv6-address
-// columns, which need the linear slot). Speed-of-light skeleton of this shape
-// with the 6-B verify-only record: 196 us vs 205 us register-staged
-// (profiles/r03/sol/sol5_r6_vs_small_kernel_same_box.txt).
-#ifndef PNET_DMA_STEPS
-#define PNET_DMA_STEPS 3
-#endif
-#ifndef PNET_DMA_WAVES
-#define PNET_DMA_WAVES (PNET_DMA_STEPS == 3 ? 3 : 4)   // the ring bounds residency by LDS
-#endif
-__device__ __forceinline__ void glds16_nt(const void* sbase, uint32_t voff, uint32_t lds_addr) {
-    uint32_t keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2 nt\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep)
-                 : "v"(voff), "s"(sbase), "s"(lds_addr)
-                 : "memory");
-}
-// s_waitcnt vmcnt(n) for a wave-uniform n (clamped to the counter's 6 bits)
-__device__ __forceinline__ void wait_vm(uint32_t n) {
-    switch (n < 63u ? n : 63u) {
-#define PNET_VMC(k) case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
-        PNET_VMC(0) PNET_VMC(1) PNET_VMC(2) PNET_VMC(3) PNET_VMC(4) PNET_VMC(5) PNET_VMC(6) PNET_VMC(7)
-        PNET_VMC(8) PNET_VMC(9) PNET_VMC(10) PNET_VMC(11) PNET_VMC(12) PNET_VMC(13) PNET_VMC(14) PNET_VMC(15)
-        PNET_VMC(16) PNET_VMC(17) PNET_VMC(18) PNET_VMC(19) PNET_VMC(20) PNET_VMC(21) PNET_VMC(22) PNET_VMC(23)
-        PNET_VMC(24) PNET_VMC(25) PNET_VMC(26) PNET_VMC(27) PNET_VMC(28) PNET_VMC(29) PNET_VMC(30) PNET_VMC(31)
-        PNET_VMC(32) PNET_VMC(33) PNET_VMC(34) PNET_VMC(35) PNET_VMC(36) PNET_VMC(37) PNET_VMC(38) PNET_VMC(39)
-        PNET_VMC(40) PNET_VMC(41) PNET_VMC(42) PNET_VMC(43) PNET_VMC(44) PNET_VMC(45) PNET_VMC(46) PNET_VMC(47)
-#undef PNET_VMC
-        default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-}
-
-// column stores a run issues (store_columns: one wave instruction per
-// requested column); the DMA kernel's waits count them
-__device__ __forceinline__ uint32_t record_stores(const pnetgpu_rx_columns& C) {
-    return (C.status != nullptr) + (C.ip_csum != nullptr) + (C.l4_csum != nullptr) + (C.ethertype != nullptr) +
-           (C.ip_proto != nullptr) + (C.ttl != nullptr) + (C.l4_offset != nullptr) + (C.l4_length != nullptr) +
-           (C.src_port != nullptr) + (C.dst_port != nullptr) + (C.src_ipv4 != nullptr) + (C.dst_ipv4 != nullptr) +
-           (C.vlan_tci != nullptr) + (C.l3_offset != nullptr);
-}
-
-template <int S>
-__global__ __launch_bounds__(kBlock, PNET_DMA_WAVES) void rx_small_dma_kernel(RxArgs a) {
-    static_assert(S == 2 || S == 3, "ring steps");
-    __shared__ __attribute__((aligned(16))) uint8_t ring[kWavesPerBlock][S][kWave * kSmallSlot];
-    __shared__ uint64_t blk_ctr[kWavesPerBlock][PNETGPU_NCOUNTERS];
-    const int lane = threadIdx.x & (kWave - 1);
-    const int wv = threadIdx.x / kWave;
-    Counters K;
-    const uint32_t span = (a.frame_len + 15u) >> 4;
-    const uint32_t kst = record_stores(a.cols);            // stores per run
-    // this lane's DMA source within a run: frame 16 i + L / 4, granule cdma
-    const uint32_t fsub = (uint32_t)lane >> 2;
-    const uint32_t cdma = (uint32_t)(((lane & 3) - (lane >> 4)) & 3);
-    const bool cok = cdma < span;
-    const uint32_t voff0 = fsub * a.stride + 16u * cdma;
-    const uint8_t* base = a.data + (a.first + a.delta);
-    // every run issues exactly four transfers (the waits count them): a lane
-    // with nothing to stage (granule past the frame, frame past the batch)
-    // re-reads the run's first granule, inside the buffer since frame_len >= 1
-    // (the host's condition for this kernel), and its slot bytes are ignored
-    auto issue = [&](uint64_t run, int slot) {
-        // wave-uniform by construction; readfirstlane puts them in SGPRs
-        const uint64_t sa = reinterpret_cast<uint64_t>(base + run * kWave * (uint64_t)a.stride);
-        const uint8_t* sb = reinterpret_cast<const uint8_t*>(
-            ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(sa >> 32)) << 32) |
-            (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)sa));
-        const uint32_t l0 = (uint32_t)__builtin_amdgcn_readfirstlane(
-            (int)(uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)&ring[wv][slot][0]);
-        const uint64_t f0 = run * kWave;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const bool ok = cok && f0 + 16 * i + fsub < a.n;
-            glds16_nt(sb, ok ? voff0 + 16u * (uint32_t)i * a.stride : 0u, l0 + 1024u * i);
-        }
-    };
-
-    const uint64_t wave_stride = (uint64_t)gridDim.x * kWavesPerBlock;
-    PNET_WT_BEGIN;
-    RunQueue q(a.sched, a.nruns, (uint64_t)blockIdx.x * kWavesPerBlock + wv, wave_stride);
-    // the ring: runs[k] in slot (cs + k) % S, k < S - 1 issued ahead
-    uint64_t runs[S];
-    runs[0] = q.take();
-#pragma unroll
-    for (int k = 1; k < S; ++k) runs[k] = runs[k - 1] < a.nruns ? q.take() : a.nruns;
-#pragma unroll
-    for (int k = 0; k < S - 1; ++k)
-        if (runs[k] < a.nruns) issue(runs[k], k);
-    int cs = 0;
-    uint32_t iter = 0;
-    while (runs[0] < a.nruns) {
-        PNET_WT_RUN;
-        const uint64_t run = runs[0];
-        // the newest run of the ring goes out now
-        if (runs[S - 1] < a.nruns) issue(runs[S - 1], (cs + S - 1) % S);
-        // vector-memory ops issued after this run's four transfers: four per
-        // later run in the ring, and each earlier iteration's column stores
-        // (up to S - 1 of them); claims issued in between only add to it
-        uint32_t later = 0;
-#pragma unroll
-        for (int k = 1; k < S; ++k) later += runs[k] < a.nruns ? 4u : 0u;
-        later += kst * min(iter, (uint32_t)(S - 1));
-        wait_vm(later);
-
-        const uint64_t f0 = run * kWave;
-        const bool in_batch = f0 + lane < a.n;
-        const uint32_t len = in_batch ? a.frame_len : 0u;
-        uint8_t* rs = &ring[wv][cs][0];
-        uint4 g[4];
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            g[c] = *reinterpret_cast<const uint4*>(rs + small_gpos(lane, c));
-            if ((uint32_t)c >= span) g[c] = make_uint4(0, 0, 0, 0);
-        }
-        Parsed P{};
-        uint32_t ipc = 0, l4c = 0;
-        const uint32_t wv16[16] = {g[0].x, g[0].y, g[0].z, g[0].w, g[1].x, g[1].y, g[1].z, g[1].w,
-                                   g[2].x, g[2].y, g[2].z, g[2].w, g[3].x, g[3].y, g[3].z, g[3].w};
-        PNET_PH(0);
-        const bool slow = in_batch && small_fast(wv16, len, P, ipc, l4c);
-        if (__ballot(slow)) {
-            // the generic parse on the frame's bytes, rewritten linearly into
-            // its own 64 B of the slot (no DMA targets this slot until the
-            // next iteration issues into it)
-            uint8_t* slot = rs + lane * kSmallSlot;
-#pragma unroll
-            for (int c = 0; c < 4; ++c) *reinterpret_cast<uint4*>(slot + 16 * c) = g[c];
-            if (slow) {
-                P = parse_frame(FrameBytes{slot, slot, 64}, len, 0u);
-                uint32_t tA = 0, tB = 0;
-                window_sums(slot, P.a_lo, P.a_hi, P.b_lo, P.b_hi, tA, tB);
-                finalize(P, tA, tB, false, ipc, l4c);
-            }
-        }
-        PNET_PH(2);
-        store_columns(a.cols, f0, lane, in_batch, P, ipc, l4c, nullptr, 0);
-        if (a.cols.counters) K.add(in_batch, len, P.st);
-        PNET_PH(3);
-        // advance the ring; the next run's claim goes out here
-#pragma unroll
-        for (int k = 0; k < S - 1; ++k) runs[k] = runs[k + 1];
-        runs[S - 1] = runs[S - 2] < a.nruns ? q.take() : a.nruns;
-        cs = cs + 1 == S ? 0 : cs + 1;
-        ++iter;
-    }
-    if (a.cols.counters) K.flush(a.cols.counters, blk_ctr, wv, lane);
-    PNET_WT_END((uint64_t)blockIdx.x * kWavesPerBlock + wv);
-}
-
 }  // namespace
 }  // namespace pnetgpu
