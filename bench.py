@@ -452,6 +452,13 @@ def tx_fill_rate(sh, steps, warmup, device):
            "cpu_port_1core_mpkts_s": round(cpu, 2), "traffic": load_traffic(f"tx_{sh.name}"),
            "note": "device-resident tx_fill_checksums (IPv4 header + L4 checksum patched in place), kernel time; "
                    f"CPU: oracle_tx_fill, 1 core, first {n1} frames"}
+    # what the writes cost in HBM: PMC WRITE_SIZE per frame against the 4 B of
+    # checksum fields that change (profiles/pmc_tx_<workload>.json; the sector
+    # floor of two fields in two 32-B sectors is 64 B: profiles/r04/tx_writes/)
+    wb = load_traffic(f"tx_{sh.name}", "write_bytes_per_launch")
+    if wb:
+        out["pmc_write_bytes_per_frame"] = round(wb / sh.n, 1)
+        out["write_over_alg_writes"] = round(wb / (sh.n * 4), 2)
     if small:
         # the small kernel writes every patched frame back whole (coalesced 1-KiB stores:
         # 2-B patches at scattered offsets ran 1.7x slower), so it moves ~2x the frame bytes
@@ -600,7 +607,7 @@ def refshapes_block(steps, warmup, device):
     return out
 
 
-def load_traffic(workload):
+def load_traffic(workload, key="hbm_bytes_per_launch"):
     """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/), if present."""
     p = os.path.join(ROOT, "profiles", f"pmc_{workload}.json")
     if not os.path.exists(p):
@@ -608,7 +615,7 @@ def load_traffic(workload):
     try:
         with open(p) as fh:
             d = json.load(fh)
-        return d.get("hbm_bytes_per_launch")
+        return d.get(key)
     except Exception:
         return None
 

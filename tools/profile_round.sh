@@ -26,7 +26,8 @@ for W in udp64 tcp1500 imix udp6_jumbo; do
   KN[$W]=$(python3 -c "import json; print(json.load(open('$F'))['workloads']['$W']['kernel'])")
 done
 KN[tx_tcp1500]="${KN[tcp1500]%, false>}, true>"
-for W in udp64 tcp1500 imix udp6_jumbo tx_tcp1500; do
+KN[tx_udp64]="rx_small_kernel<true, false>"
+for W in udp64 tcp1500 imix udp6_jumbo tx_tcp1500 tx_udp64; do
   WL=${W#tx_}; TX=""; [ "$W" != "$WL" ] && TX="--tx"
   for C in FETCH_SIZE WRITE_SIZE; do
     timeout -s KILL 120 rocprofv3 --pmc $C --kernel-trace --output-format csv -d $O/pmc_${W}_$C -o run -- \
@@ -34,6 +35,8 @@ for W in udp64 tcp1500 imix udp6_jumbo tx_tcp1500; do
   done
   if [ "$W" = tx_tcp1500 ]; then
     ALG=$(python3 -c "print(1500 * 2**20 + 6 * 2**20)")
+  elif [ "$W" = tx_udp64 ]; then
+    ALG=$(python3 -c "print(64 * 2**24 + 6 * 2**24)")
   elif [ "$W" = udp64 ]; then
     ALG=$(python3 -c "import json; print(json.load(open('$O/bench_udp64_under_rocprof.json'))['workloads']['$W']['alg_bytes_per_launch'])" || true)
   else
