@@ -17,14 +17,7 @@ namespace {
 // ============================================================================
 // rx_kernel: generic (descriptor mode, any alignment, any length).
 // ============================================================================
-#ifndef PNET_TAIL_SPLIT
-#define PNET_TAIL_SPLIT 1   // the mixed shape's tail cut into round-sized items (A/B: 0, whole frames)
-#endif
-// tail items a run may list (the mixed shape): 64 frames of up to 4 rounds each
-// at one round per item; runs with more rounds make their items longer
-constexpr int kMaxItems = 256;
-
-template <int NW, bool ITEMS = false>
+template <int NW>
 struct WaveLds {
     static constexpr int kSlot = NW * 16 + 4;   // +4 B pad: conflict-free parse reads
     uint8_t win[kWave * kSlot];
@@ -33,8 +26,6 @@ struct WaveLds {
     uint32_t tail[kWave];     // weighted sum of the frame's bytes past the window
     uint8_t list[kWave];      // frames with bytes past the window (longest class first)
     uint32_t qhead;           // next list entry for a group that runs out of work
-    // the split tail (tail_items): item = chunk << 6 | frame, in frame order
-    uint16_t items[ITEMS ? kMaxItems : 1];
 };
 
 // Weighted sum of slot bytes [lo, hi) of a frame whose granule 0 is at fb, read
@@ -69,14 +60,14 @@ __device__ __forceinline__ uint32_t lane_range_sum(const uint8_t* fb, int lo, in
 // LDS counter instead of a fixed stride of the list, and the list holds the
 // frames needing more than one round first, so mixed sizes balance across the
 // groups (the caller sets L.qhead = kWave / G).
-template <int NW, int G, int U, bool NT, bool UNI, bool DYN, bool IT>
-__device__ __forceinline__ void tail_sums(const uint8_t* data, WaveLds<NW, IT>& L, int lane, int count
+template <int NW, int G, int U, bool NT, bool UNI, bool DYN>
+__device__ __forceinline__ void tail_sums(const uint8_t* data, WaveLds<NW>& L, int lane, int count
 #ifdef PNET_WAVE_TIMES
                                           , uint64_t (&stat)[3]
 #endif
 ) {
     constexpr int kGroups = kWave / G;
-    constexpr int kSlot = WaveLds<NW, IT>::kSlot;
+    constexpr int kSlot = WaveLds<NW>::kSlot;
     constexpr uint32_t c_first = UNI ? 0u : (uint32_t)NW;
     static_assert(!UNI || G * U >= NW, "the first round must cover the window");
     const int j = lane % G;
@@ -157,91 +148,6 @@ __device__ __forceinline__ void tail_sums(const uint8_t* data, WaveLds<NW, IT>& 
 #endif
 }
 
-// The split tail (the mixed shape, PNET_TAIL_SPLIT): every frame's bytes past
-// its window, [kWin, end), cut into items of R group rounds (R * G * U
-// granules; R = 1 unless the run has more than kMaxItems rounds), listed in
-// L.items by the caller and handed to the groups from the LDS counter L.qhead.
-// A group sums its item's granules and adds the sum into L.tail[frame] (zeroed
-// by the caller) with an LDS atomic, so the rounds of one long frame spread
-// over several groups and the phase ends after about ceil(rounds / groups)
-// rounds instead of the longest frame's rounds (whole frames per group used
-// 58.5 % of the group-round slots on IMIX, tools/wave_times.py).
-template <int NW, int G, int U, bool NT>
-__device__ __forceinline__ void tail_items(const uint8_t* data, WaveLds<NW, true>& L, int lane, int count,
-                                           uint32_t round_granules
-#ifdef PNET_WAVE_TIMES
-                                           , uint64_t (&stat)[3]
-#endif
-) {
-    [[maybe_unused]] constexpr int kGroups = kWave / G;
-    const int j = lane % G;
-    int idx = lane / G;
-    int fl = 0;
-    uint32_t fe = 0, cend = 0, c0 = 0, acc = 0;
-    const uint8_t* fb = data;
-    auto start = [&]() {
-        const uint32_t it = L.items[idx];
-        fl = (int)(it & 63u);
-        fe = L.end[fl];
-        fb = data + L.base[fl];
-        const uint32_t cbeg = (uint32_t)NW + (it >> 6) * round_granules;
-        cend = min(cbeg + round_granules, (fe + 15u) >> 4);
-        c0 = cbeg + (uint32_t)j;
-    };
-    if (idx < count) start();
-#ifdef PNET_WAVE_TIMES
-    uint32_t iters = 0, issued = 0;
-#endif
-    while (__ballot(idx < count)) {
-#ifdef PNET_WAVE_TIMES
-        ++iters;
-        issued += (uint32_t)__popcll(__ballot(idx < count && j == 0));
-#endif
-        if (idx < count) {
-            uint4 v[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const uint32_t c = c0 + u * G;
-                v[u] = c < cend ? (NT ? load16_nt(fb + 16u * c) : load16(fb + 16u * c)) : make_uint4(0, 0, 0, 0);
-            }
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const uint32_t c = c0 + u * G;
-                uint32_t x = v[u].x, y = v[u].y, z = v[u].z, w = v[u].w;
-                const int hi = (int)fe - (int)(16u * c);
-                if (hi < 16) {                                   // the frame's last granule
-                    x &= first_bytes(clamp04(hi));
-                    y &= first_bytes(clamp04(hi - 4));
-                    z &= first_bytes(clamp04(hi - 8));
-                    w &= first_bytes(clamp04(hi - 12));
-                }
-                acc = sad(x, acc);
-                acc = sad(y, acc);
-                acc = sad(z, acc);
-                acc = sad(w, acc);
-            }
-            c0 += U * G;
-            if (c0 - j >= cend) {                                // group-uniform: item done
-#pragma unroll
-                for (int o = G / 2; o >= 1; o >>= 1) acc += __shfl_xor(acc, o);
-                uint32_t nidx = 0;
-                if (j == 0) {
-                    atomicAdd(&L.tail[fl], acc);
-                    nidx = atomicAdd(&L.qhead, 1u);
-                }
-                acc = 0;
-                idx = __shfl((int)nidx, lane - j);
-                if (idx < count) start();
-            }
-        }
-    }
-#ifdef PNET_WAVE_TIMES
-    stat[0] += issued;
-    stat[1] += (uint64_t)iters * kGroups;
-    stat[2] += (uint64_t)((issued + kGroups - 1) / kGroups) * kGroups;
-#endif
-}
-
 // PASS: 0 = window phase for every frame, then the tails of the long ones;
 // 1 = unified: every frame streamed once by the group loop (a hybrid - windows
 // of short frames first, long frames unified - measured 5-15 % slower on IMIX).
@@ -260,9 +166,7 @@ __global__ __launch_bounds__(kBlock, NW < 8 ? 5 : 4) void rx_kernel(RxArgs a) {
     // tags + the fixed IPv4 header / IPv6 addresses: 82 B) after a 15-B shift
     static_assert(NW >= 7 || NW == 6, "window granules");
     static_assert(G == 2 || G == 4 || G == 8 || G == 16 || G == 32 || G == 64, "tail group");
-    // the mixed shape splits its tail into round-sized items (tail_items)
-    constexpr bool kItems = PNET_TAIL_SPLIT && PASS == 0 && DYN;
-    constexpr int kSlot = WaveLds<NW, kItems>::kSlot;
+    constexpr int kSlot = WaveLds<NW>::kSlot;
     constexpr int kWin = NW * 16;
     // runs of short aligned frames take the small kernel's fast path (the
     // mixed shape's plain instantiation: no dispatch flags, header-field
@@ -271,12 +175,12 @@ __global__ __launch_bounds__(kBlock, NW < 8 ? 5 : 4) void rx_kernel(RxArgs a) {
     // the short-run realignment reads slot dwords up to byte sh + 67 (sh <= 15)
     static_assert(!kShortRuns || kSlot >= 15 + 68, "short runs need a slot of at least 83 B");
 
-    __shared__ WaveLds<NW, kItems> lds_all[kWavesPerBlock];
+    __shared__ WaveLds<NW> lds_all[kWavesPerBlock];
     __shared__ uint64_t blk_ctr[kWavesPerBlock][PNETGPU_NCOUNTERS];
 
     const int lane = threadIdx.x & (kWave - 1);
     const int wv = threadIdx.x / kWave;
-    WaveLds<NW, kItems>& L = lds_all[wv];
+    WaveLds<NW>& L = lds_all[wv];
     uint8_t* slot = L.win + lane * kSlot;
     Counters K;
 
@@ -402,33 +306,7 @@ __global__ __launch_bounds__(kBlock, NW < 8 ? 5 : 4) void rx_kernel(RxArgs a) {
         // the group loop also fills the window of every frame.
         const bool has_tail = PASS == 1 ? in_batch : long_frame;
         const uint64_t tmask = __ballot(has_tail);
-        if constexpr (kItems) {
-          if (tmask) {
-            // items of one round (G * U granules) per frame past the window, in
-            // frame order; a run with more than kMaxItems rounds takes R rounds
-            // per item (wave-uniform)
-            constexpr uint32_t kRound = (uint32_t)(G * U);
-            const uint32_t rounds = has_tail ? (span - (uint32_t)NW + kRound - 1) / kRound : 0u;
-            uint32_t incl = wave_incl_scan(rounds);
-            uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, kWave - 1);
-            uint32_t per = 1, mine = rounds;
-            if (total > (uint32_t)kMaxItems) {
-                // sum of ceil(rounds / per) <= total / per + 64 <= kMaxItems
-                per = (total + (kMaxItems - kWave) - 1) / (kMaxItems - kWave);
-                mine = (rounds + per - 1) / per;
-                incl = wave_incl_scan(mine);
-                total = (uint32_t)__builtin_amdgcn_readlane((int)incl, kWave - 1);
-            }
-            for (uint32_t k = 0; k < mine; ++k) L.items[incl - mine + k] = (uint16_t)((k << 6) | (uint32_t)lane);
-            if (has_tail) {
-                L.end[lane] = fend;
-                L.tail[lane] = 0;
-            }
-            if (lane == 0) L.qhead = kWave / G;
-            wave_sync();
-            tail_items<NW, G, U, NT>(a.data, L, lane, (int)total, per * kRound PNET_TAIL_STAT);
-          }
-        } else if (tmask) {
+        if (tmask) {
             // DYN: frames needing more than one group round go first
             const bool big = DYN && has_tail && span > (uint32_t)(NW + G * U);
             const uint64_t bmask = __ballot(big);
@@ -440,7 +318,7 @@ __global__ __launch_bounds__(kBlock, NW < 8 ? 5 : 4) void rx_kernel(RxArgs a) {
             }
             if (DYN && lane == 0) L.qhead = kWave / G;
             wave_sync();
-            tail_sums<NW, G, U, NT, (PASS != 0), DYN, kItems>(a.data, L, lane, __popcll(tmask) PNET_TAIL_STAT);
+            tail_sums<NW, G, U, NT, (PASS != 0), DYN>(a.data, L, lane, __popcll(tmask) PNET_TAIL_STAT);
         }
         wave_sync();
 
