@@ -17,6 +17,9 @@ namespace {
 // ============================================================================
 // rx_kernel: generic (descriptor mode, any alignment, any length).
 // ============================================================================
+#ifndef PNET_MTU_ALT
+#define PNET_MTU_ALT 0   // A/B: the MTU shape streams odd frames backward (below)
+#endif
 #ifndef PNET_LINE_EDGES
 #define PNET_LINE_EDGES 0   // A/B: the mixed shape's lanes sum their frames' edge lines (below)
 #endif
@@ -66,7 +69,12 @@ __device__ __forceinline__ uint32_t lane_range_sum(const uint8_t* fb, int lo, in
 // LDS counter instead of a fixed stride of the list, and the list holds the
 // frames needing more than one round first, so mixed sizes balance across the
 // groups (the caller sets L.qhead = kWave / G).
-template <int NW, int G, int U, bool NT, bool UNI, bool DYN, bool EDG>
+// ALT (the unified MTU shape, PNET_MTU_ALT): odd frames are streamed from
+// their last granule backward, so the line a frame's end shares with the next
+// frame's start is read by both groups in the same round (even frame: its
+// last round; odd frame: its last round, which then covers its start), instead
+// of rounds apart (the second read then comes from L2, not HBM).
+template <int NW, int G, int U, bool NT, bool UNI, bool DYN, bool EDG, bool ALT = false>
 __device__ __forceinline__ void tail_sums(const uint8_t* data, WaveLds<NW, EDG>& L, int lane, int count
 #ifdef PNET_WAVE_TIMES
                                           , uint64_t (&stat)[3]
@@ -98,14 +106,19 @@ __device__ __forceinline__ void tail_sums(const uint8_t* data, WaveLds<NW, EDG>&
 #endif
         if (idx < count) {
             uint4 v[U];
+            // ALT: odd frames' granule order reversed (UNI: c_first = 0)
+            const bool rev = ALT && (fl & 1);
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-                const uint32_t c = c0 + u * G;
-                v[u] = c < nneed ? (NT ? load16_nt(fb + 16u * c) : load16(fb + 16u * c)) : make_uint4(0, 0, 0, 0);
+                const uint32_t cs = c0 + u * G;
+                const uint32_t c = rev && cs < nneed ? nneed - 1u - cs : cs;
+                v[u] = cs < nneed ? (NT ? load16_nt(fb + 16u * c) : load16(fb + 16u * c)) : make_uint4(0, 0, 0, 0);
             }
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-                const uint32_t c = c0 + u * G;
+                const uint32_t cs = c0 + u * G;
+                // past the frame (cs >= nneed): the same zero granule either way
+                const uint32_t c = rev && cs < nneed ? nneed - 1u - cs : cs;
                 uint32_t x = v[u].x, y = v[u].y, z = v[u].z, w = v[u].w;
                 if (UNI && c < (uint32_t)NW) {                   // window granule -> the frame's slot
                     uint32_t* dst = reinterpret_cast<uint32_t*>(L.win + fl * kSlot + 16 * c);
@@ -372,7 +385,8 @@ __global__ __launch_bounds__(kBlock, NW < 8 ? 5 : 4) void rx_kernel(RxArgs a) {
             }
             if (DYN && lane == 0) L.qhead = kWave / G;
             wave_sync();
-            tail_sums<NW, G, U, NT, (PASS != 0), DYN, kEdges>(a.data, L, lane, __popcll(tmask) PNET_TAIL_STAT);
+            tail_sums<NW, G, U, NT, (PASS != 0), DYN, kEdges, (PNET_MTU_ALT && PASS == 1 && !DYN)>(
+                a.data, L, lane, __popcll(tmask) PNET_TAIL_STAT);
         }
         wave_sync();
 
