@@ -18,12 +18,9 @@ namespace {
 // rx_kernel: generic (descriptor mode, any alignment, any length).
 // ============================================================================
 #ifndef PNET_MTU_ALT
-#define PNET_MTU_ALT 0   // A/B: the MTU shape streams odd frames backward (below)
+#define PNET_MTU_ALT 1   // the MTU shape streams odd frames backward (below; A/B: 0)
 #endif
-#ifndef PNET_LINE_EDGES
-#define PNET_LINE_EDGES 0   // A/B: the mixed shape's lanes sum their frames' edge lines (below)
-#endif
-template <int NW, bool EDG = false>
+template <int NW>
 struct WaveLds {
     static constexpr int kSlot = NW * 16 + 4;   // +4 B pad: conflict-free parse reads
     uint8_t win[kWave * kSlot];
@@ -32,9 +29,6 @@ struct WaveLds {
     uint32_t tail[kWave];     // weighted sum of the frame's bytes past the window
     uint8_t list[kWave];      // frames with bytes past the window (longest class first)
     uint32_t qhead;           // next list entry for a group that runs out of work
-    // EDG: the granule range [g0, g1) the tail groups stream (the frame's own
-    // lane sums the rest of its bytes past the window: its edge lines)
-    uint16_t g0[EDG ? kWave : 1], g1[EDG ? kWave : 1];
 };
 
 // Weighted sum of slot bytes [lo, hi) of a frame whose granule 0 is at fb, read
@@ -74,14 +68,14 @@ __device__ __forceinline__ uint32_t lane_range_sum(const uint8_t* fb, int lo, in
 // frame's start is read by both groups in the same round (even frame: its
 // last round; odd frame: its last round, which then covers its start), instead
 // of rounds apart (the second read then comes from L2, not HBM).
-template <int NW, int G, int U, bool NT, bool UNI, bool DYN, bool EDG, bool ALT = false>
-__device__ __forceinline__ void tail_sums(const uint8_t* data, WaveLds<NW, EDG>& L, int lane, int count
+template <int NW, int G, int U, bool NT, bool UNI, bool DYN, bool ALT = false>
+__device__ __forceinline__ void tail_sums(const uint8_t* data, WaveLds<NW>& L, int lane, int count
 #ifdef PNET_WAVE_TIMES
                                           , uint64_t (&stat)[3]
 #endif
 ) {
     constexpr int kGroups = kWave / G;
-    constexpr int kSlot = WaveLds<NW, EDG>::kSlot;
+    constexpr int kSlot = WaveLds<NW>::kSlot;
     constexpr uint32_t c_first = UNI ? 0u : (uint32_t)NW;
     static_assert(!UNI || G * U >= NW, "the first round must cover the window");
     const int j = lane % G;
@@ -93,8 +87,8 @@ __device__ __forceinline__ void tail_sums(const uint8_t* data, WaveLds<NW, EDG>&
         fl = L.list[idx];
         fe = L.end[fl];
         fb = data + L.base[fl];
-        nneed = EDG ? (uint32_t)L.g1[fl] : (fe + 15u) >> 4;
-        c0 = (EDG ? (uint32_t)L.g0[fl] : c_first) + j;
+        nneed = (fe + 15u) >> 4;
+        c0 = c_first + j;
     }
 #ifdef PNET_WAVE_TIMES
     uint32_t iters = 0, issued = 0;
@@ -141,7 +135,7 @@ __device__ __forceinline__ void tail_sums(const uint8_t* data, WaveLds<NW, EDG>&
             if (c0 - j >= (nneed > c_first ? nneed : c_first + 1u)) {   // group-uniform: frame done
 #pragma unroll
                 for (int o = G / 2; o >= 1; o >>= 1) acc += __shfl_xor(acc, o);
-                if (j == 0) L.tail[fl] = EDG ? L.tail[fl] + acc : acc;   // EDG: the lane's edge sum is in it
+                if (j == 0) L.tail[fl] = acc;
                 acc = 0;
                 if (DYN) {
                     uint32_t nidx = 0;
@@ -154,8 +148,8 @@ __device__ __forceinline__ void tail_sums(const uint8_t* data, WaveLds<NW, EDG>&
                     fl = L.list[idx];
                     fe = L.end[fl];
                     fb = data + L.base[fl];
-                    nneed = EDG ? (uint32_t)L.g1[fl] : (fe + 15u) >> 4;
-                    c0 = (EDG ? (uint32_t)L.g0[fl] : c_first) + j;
+                    nneed = (fe + 15u) >> 4;
+                    c0 = c_first + j;
                 }
             }
         }
@@ -185,13 +179,7 @@ __global__ __launch_bounds__(kBlock, NW < 8 ? 5 : 4) void rx_kernel(RxArgs a) {
     // tags + the fixed IPv4 header / IPv6 addresses: 82 B) after a 15-B shift
     static_assert(NW >= 7 || NW == 6, "window granules");
     static_assert(G == 2 || G == 4 || G == 8 || G == 16 || G == 32 || G == 64, "tail group");
-    // the mixed shape's edge lines (PNET_LINE_EDGES): each long frame's lane
-    // sums the granules of the line its window ends in and of the line its
-    // last byte is in, right after the window phase (both lines are then
-    // still in L2: the first one this wave just read, the other one usually
-    // the next frame's window); the tail groups stream the whole lines between
-    constexpr bool kEdges = PNET_LINE_EDGES && PASS == 0 && DYN;
-    constexpr int kSlot = WaveLds<NW, kEdges>::kSlot;
+    constexpr int kSlot = WaveLds<NW>::kSlot;
     constexpr int kWin = NW * 16;
     // runs of short aligned frames take the small kernel's fast path (the
     // mixed shape's plain instantiation: no dispatch flags, header-field
@@ -200,12 +188,12 @@ __global__ __launch_bounds__(kBlock, NW < 8 ? 5 : 4) void rx_kernel(RxArgs a) {
     // the short-run realignment reads slot dwords up to byte sh + 67 (sh <= 15)
     static_assert(!kShortRuns || kSlot >= 15 + 68, "short runs need a slot of at least 83 B");
 
-    __shared__ WaveLds<NW, kEdges> lds_all[kWavesPerBlock];
+    __shared__ WaveLds<NW> lds_all[kWavesPerBlock];
     __shared__ uint64_t blk_ctr[kWavesPerBlock][PNETGPU_NCOUNTERS];
 
     const int lane = threadIdx.x & (kWave - 1);
     const int wv = threadIdx.x / kWave;
-    WaveLds<NW, kEdges>& L = lds_all[wv];
+    WaveLds<NW>& L = lds_all[wv];
     uint8_t* slot = L.win + lane * kSlot;
     Counters K;
 
@@ -323,59 +311,17 @@ __global__ __launch_bounds__(kBlock, NW < 8 ? 5 : 4) void rx_kernel(RxArgs a) {
             fetch_desc(nrun);
         }
 
-        // ---- 2b. edge lines (kEdges): [NW, e1) and [e2, span) summed by the
-        // frame's own lane; [e1, e2) left to the tail groups
-        uint32_t eg0 = NW, eg1 = NW;
-        if constexpr (kEdges) {
-            uint32_t edge = 0;
-            if (long_frame) {
-                const uint32_t lo = (uint32_t)(base >> 4) & 7u;                 // granule of base in its 128-B line
-                const uint32_t e1 = min((uint32_t)NW + ((8u - ((lo + NW) & 7u)) & 7u), span);
-                const uint32_t last = span - 1u;
-                const uint32_t e2 = max(last - ((lo + last) & 7u), e1);
-                eg0 = e1;
-                eg1 = e2;
-                const uint8_t* fb = a.data + base;
-                uint4 v[15];
-#pragma unroll
-                for (int k = 0; k < 7; ++k) {
-                    const uint32_t c = (uint32_t)NW + k;
-                    v[k] = c < e1 ? load16(fb + 16u * c) : make_uint4(0, 0, 0, 0);
-                }
-#pragma unroll
-                for (int k = 0; k < 8; ++k) {
-                    const uint32_t c = e2 + k;
-                    v[7 + k] = c < span ? load16(fb + 16u * c) : make_uint4(0, 0, 0, 0);
-                }
-#pragma unroll
-                for (int k = 0; k < 15; ++k) {
-                    const uint32_t c = k < 7 ? (uint32_t)NW + k : e2 + (k - 7);
-                    uint32_t x = v[k].x, y = v[k].y, z = v[k].z, w = v[k].w;
-                    const int hi = (int)fend - (int)(16u * c);
-                    if (hi < 16) {                               // the frame's last granule (or past it: zeros)
-                        x &= first_bytes(clamp04(hi));
-                        y &= first_bytes(clamp04(hi - 4));
-                        z &= first_bytes(clamp04(hi - 8));
-                        w &= first_bytes(clamp04(hi - 12));
-                    }
-                    edge = sad(x, sad(y, sad(z, sad(w, edge))));
-                }
-            }
-            L.tail[lane] = edge;
-            L.g0[lane] = (uint16_t)eg0;
-            L.g1[lane] = (uint16_t)eg1;
-        }
         PNET_PH(0);   // probe: descriptors + window (its loads complete at the LDS stores)
         // ---- 3. speculative tail: all frame bytes past the window ----------
         // Summed before the parse (no parse state is live, so more loads fit in
         // flight); the parse then trims it to the L4 range B, which in every
         // well-formed frame already runs to the end of the frame. Unified pass:
         // the group loop also fills the window of every frame.
-        const bool has_tail = PASS == 1 ? in_batch : (kEdges ? long_frame && eg1 > eg0 : long_frame);
+        const bool has_tail = PASS == 1 ? in_batch : long_frame;
         const uint64_t tmask = __ballot(has_tail);
         if (tmask) {
             // DYN: frames needing more than one group round go first
-            const bool big = DYN && has_tail && (kEdges ? eg1 - eg0 : span - (uint32_t)NW) > (uint32_t)(G * U);
+            const bool big = DYN && has_tail && span > (uint32_t)(NW + G * U);
             const uint64_t bmask = __ballot(big);
             const uint64_t below = (1ull << lane) - 1ull;
             if (has_tail) {
@@ -385,7 +331,7 @@ __global__ __launch_bounds__(kBlock, NW < 8 ? 5 : 4) void rx_kernel(RxArgs a) {
             }
             if (DYN && lane == 0) L.qhead = kWave / G;
             wave_sync();
-            tail_sums<NW, G, U, NT, (PASS != 0), DYN, kEdges, (PNET_MTU_ALT && PASS == 1 && !DYN)>(
+            tail_sums<NW, G, U, NT, (PASS != 0), DYN, (PNET_MTU_ALT && PASS == 1 && !DYN)>(
                 a.data, L, lane, __popcll(tmask) PNET_TAIL_STAT);
         }
         wave_sync();
