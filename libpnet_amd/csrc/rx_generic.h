@@ -17,6 +17,9 @@ namespace {
 // ============================================================================
 // rx_kernel: generic (descriptor mode, any alignment, any length).
 // ============================================================================
+#ifndef PNET_LINE_ALIGN
+#define PNET_LINE_ALIGN 0   // A/B: the MTU shape's groups stream whole 128-B lines (tail_sums LA)
+#endif
 #ifndef PNET_MTU_ALT
 #define PNET_MTU_ALT 1   // the MTU shape streams odd frames backward (below; A/B: 0)
 #endif
@@ -68,7 +71,14 @@ __device__ __forceinline__ uint32_t lane_range_sum(const uint8_t* fb, int lo, in
 // frame's start is read by both groups in the same round (even frame: its
 // last round; odd frame: its last round, which then covers its start), instead
 // of rounds apart (the second read then comes from L2, not HBM).
-template <int NW, int G, int U, bool NT, bool UNI, bool DYN, bool ALT = false>
+// LA (line-aligned, PNET_LINE_ALIGN; groups of 8 lanes): the group streams
+// whole 128-B lines — granule c = A + stream index, A the first granule of
+// the line holding the stream's start — so that each wave load instruction
+// asks the L1 for one line per group instead of straddling two (lanes outside
+// the frame's range are predicated off: no extra line is requested). The
+// vector memory path (TA/TD/L1) is the kernels' bound (profiles/r04/pmc_mem/),
+// so the number of L1->L2 requests per byte is what the stream pays for.
+template <int NW, int G, int U, bool NT, bool UNI, bool DYN, bool ALT = false, bool LA = false>
 __device__ __forceinline__ void tail_sums(const uint8_t* data, WaveLds<NW>& L, int lane, int count
 #ifdef PNET_WAVE_TIMES
                                           , uint64_t (&stat)[3]
@@ -78,18 +88,31 @@ __device__ __forceinline__ void tail_sums(const uint8_t* data, WaveLds<NW>& L, i
     constexpr int kSlot = WaveLds<NW>::kSlot;
     constexpr uint32_t c_first = UNI ? 0u : (uint32_t)NW;
     static_assert(!UNI || G * U >= NW, "the first round must cover the window");
+    static_assert(!LA || G % 8 == 0, "line-aligned groups cover whole 8-granule lines");
     const int j = lane % G;
     int idx = lane / G;
     int fl = 0;
     uint32_t fe = 0, nneed = 0, c0 = 0, acc = 0;
+    int la0 = 0;          // LA: first granule (frame-relative, may be < 0) of the stream's first line
+    uint32_t lalen = 0;   // LA: stream length in granules (whole lines)
     const uint8_t* fb = data;
-    if (idx < count) {
+    auto start = [&]() {
         fl = L.list[idx];
         fe = L.end[fl];
         fb = data + L.base[fl];
         nneed = (fe + 15u) >> 4;
-        c0 = c_first + j;
-    }
+        if (LA) {
+            const uint32_t lo = (uint32_t)(L.base[fl] >> 4) & 7u;          // granule of base in its line
+            const uint32_t nend = UNI ? max(nneed, (uint32_t)NW) : nneed;   // UNI: the whole window too
+            la0 = (int)c_first - (int)((lo + c_first) & 7u);
+            const int lend = (int)nend + (int)((8u - ((lo + nend) & 7u)) & 7u);
+            lalen = (uint32_t)(lend - la0);
+            c0 = (uint32_t)j;
+        } else {
+            c0 = c_first + j;
+        }
+    };
+    if (idx < count) start();
 #ifdef PNET_WAVE_TIMES
     uint32_t iters = 0, issued = 0;
 #endif
@@ -102,17 +125,30 @@ __device__ __forceinline__ void tail_sums(const uint8_t* data, WaveLds<NW>& L, i
             uint4 v[U];
             // ALT: odd frames' granule order reversed (UNI: c_first = 0)
             const bool rev = ALT && (fl & 1);
+            // the granule stream index cs maps to (LA: whole lines, reversed by line)
+            auto gran = [&](uint32_t cs) -> int {
+                if (LA) {
+                    const int k = (int)(cs >> 3), t = (int)(cs & 7u);
+                    return rev ? la0 + (int)lalen - 8 * (k + 1) + t : la0 + (int)cs;
+                }
+                return (int)(rev && cs < nneed ? nneed - 1u - cs : cs);
+            };
+            auto live = [&](uint32_t cs, int c) {
+                return LA ? (c >= (int)c_first && c < (int)nneed) : cs < nneed;
+            };
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const uint32_t cs = c0 + u * G;
-                const uint32_t c = rev && cs < nneed ? nneed - 1u - cs : cs;
-                v[u] = cs < nneed ? (NT ? load16_nt(fb + 16u * c) : load16(fb + 16u * c)) : make_uint4(0, 0, 0, 0);
+                const int c = gran(cs);
+                v[u] = live(cs, c) ? (NT ? load16_nt(fb + 16 * c) : load16(fb + 16 * c)) : make_uint4(0, 0, 0, 0);
             }
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const uint32_t cs = c0 + u * G;
                 // past the frame (cs >= nneed): the same zero granule either way
-                const uint32_t c = rev && cs < nneed ? nneed - 1u - cs : cs;
+                const int ci = gran(cs);
+                if (LA && (ci < 0 || ci >= (int)(UNI ? max(nneed, (uint32_t)NW) : nneed))) continue;   // outside the frame's lines
+                const uint32_t c = (uint32_t)ci;
                 uint32_t x = v[u].x, y = v[u].y, z = v[u].z, w = v[u].w;
                 if (UNI && c < (uint32_t)NW) {                   // window granule -> the frame's slot
                     uint32_t* dst = reinterpret_cast<uint32_t*>(L.win + fl * kSlot + 16 * c);
@@ -132,7 +168,7 @@ __device__ __forceinline__ void tail_sums(const uint8_t* data, WaveLds<NW>& L, i
                 acc = sad(w, acc);
             }
             c0 += U * G;
-            if (c0 - j >= (nneed > c_first ? nneed : c_first + 1u)) {   // group-uniform: frame done
+            if (c0 - j >= (LA ? lalen : (nneed > c_first ? nneed : c_first + 1u))) {   // group-uniform: frame done
 #pragma unroll
                 for (int o = G / 2; o >= 1; o >>= 1) acc += __shfl_xor(acc, o);
                 if (j == 0) L.tail[fl] = acc;
@@ -144,13 +180,7 @@ __device__ __forceinline__ void tail_sums(const uint8_t* data, WaveLds<NW>& L, i
                 } else {
                     idx += kGroups;
                 }
-                if (idx < count) {
-                    fl = L.list[idx];
-                    fe = L.end[fl];
-                    fb = data + L.base[fl];
-                    nneed = (fe + 15u) >> 4;
-                    c0 = c_first + j;
-                }
+                if (idx < count) start();
             }
         }
     }
@@ -331,7 +361,8 @@ __global__ __launch_bounds__(kBlock, NW < 8 ? 5 : 4) void rx_kernel(RxArgs a) {
             }
             if (DYN && lane == 0) L.qhead = kWave / G;
             wave_sync();
-            tail_sums<NW, G, U, NT, (PASS != 0), DYN, (PNET_MTU_ALT && PASS == 1 && !DYN)>(
+            tail_sums<NW, G, U, NT, (PASS != 0), DYN, (PNET_MTU_ALT && PASS == 1 && !DYN),
+                      (PNET_LINE_ALIGN && PASS == 1 && !DYN && G % 8 == 0)>(
                 a.data, L, lane, __popcll(tmask) PNET_TAIL_STAT);
         }
         wave_sync();
