@@ -17,6 +17,9 @@ namespace {
 // ============================================================================
 // rx_kernel: generic (descriptor mode, any alignment, any length).
 // ============================================================================
+#ifndef PNET_MIXED_LA
+#define PNET_MIXED_LA 0   // A/B: the mixed shape's window = the frame's first two whole lines
+#endif
 #ifndef PNET_LINE_ALIGN
 #define PNET_LINE_ALIGN 0   // A/B: the MTU shape's groups stream whole 128-B lines (tail_sums LA)
 #endif
@@ -78,7 +81,11 @@ __device__ __forceinline__ uint32_t lane_range_sum(const uint8_t* fb, int lo, in
 // the frame's range are predicated off: no extra line is requested). The
 // vector memory path (TA/TD/L1) is the kernels' bound (profiles/r04/pmc_mem/),
 // so the number of L1->L2 requests per byte is what the stream pays for.
-template <int NW, int G, int U, bool NT, bool UNI, bool DYN, bool ALT = false, bool LA = false>
+// MLA (the mixed shape's line-aligned window, PNET_MIXED_LA): the window
+// phase read the frame's first two whole lines and summed their bytes past
+// the window into L.tail; the groups start at the third line (granule
+// 16 - lo) and add their sums.
+template <int NW, int G, int U, bool NT, bool UNI, bool DYN, bool ALT = false, bool LA = false, bool MLA = false>
 __device__ __forceinline__ void tail_sums(const uint8_t* data, WaveLds<NW>& L, int lane, int count
 #ifdef PNET_WAVE_TIMES
                                           , uint64_t (&stat)[3]
@@ -108,6 +115,8 @@ __device__ __forceinline__ void tail_sums(const uint8_t* data, WaveLds<NW>& L, i
             const int lend = (int)nend + (int)((8u - ((lo + nend) & 7u)) & 7u);
             lalen = (uint32_t)(lend - la0);
             c0 = (uint32_t)j;
+        } else if (MLA) {
+            c0 = 16u - ((uint32_t)(L.base[fl] >> 4) & 7u) + j;
         } else {
             c0 = c_first + j;
         }
@@ -171,7 +180,7 @@ __device__ __forceinline__ void tail_sums(const uint8_t* data, WaveLds<NW>& L, i
             if (c0 - j >= (LA ? lalen : (nneed > c_first ? nneed : c_first + 1u))) {   // group-uniform: frame done
 #pragma unroll
                 for (int o = G / 2; o >= 1; o >>= 1) acc += __shfl_xor(acc, o);
-                if (j == 0) L.tail[fl] = acc;
+                if (j == 0) L.tail[fl] = MLA ? L.tail[fl] + acc : acc;
                 acc = 0;
                 if (DYN) {
                     uint32_t nidx = 0;
@@ -215,6 +224,11 @@ __global__ __launch_bounds__(kBlock, NW < 8 ? 5 : 4) void rx_kernel(RxArgs a) {
     // mixed shape's plain instantiation: no dispatch flags, header-field
     // columns or TX)
     constexpr bool kShortRuns = PNET_SHORT_RUNS && PASS == 0 && DYN && !EXT && !TX;
+    // the mixed shape's line-aligned window (PNET_MIXED_LA): granules [-lo, 16 - lo)
+    // of each frame (its first two whole 128-B lines, lo = base's granule in
+    // its line), the slot's NW granules stored, the rest summed into L.tail by
+    // a 16-lane row reduction; the tail groups start at the third line
+    constexpr bool kMixedLA = PNET_MIXED_LA && PASS == 0 && DYN && NW == 8;
     // the short-run realignment reads slot dwords up to byte sh + 67 (sh <= 15)
     static_assert(!kShortRuns || kSlot >= 15 + 68, "short runs need a slot of at least 83 B");
 
@@ -286,7 +300,8 @@ __global__ __launch_bounds__(kBlock, NW < 8 ? 5 : 4) void rx_kernel(RxArgs a) {
         const uint32_t span = (fend + 15u) >> 4;
         const bool long_frame = fend > (uint32_t)kWin;
         L.base[lane] = base;
-        L.end[lane] = span < (uint32_t)NW ? span : (uint32_t)NW;   // granules to load into the window
+        L.end[lane] = kMixedLA ? fend : span < (uint32_t)NW ? span : (uint32_t)NW;   // granules to load into the window
+        const uint32_t lo_g = (uint32_t)(base >> 4) & 7u;     // base's granule in its 128-B line (kMixedLA)
         wave_sync();
 
         // short run (descriptor batches of minimum-size frames: the AF_PACKET /
@@ -319,6 +334,41 @@ __global__ __launch_bounds__(kBlock, NW < 8 ? 5 : 4) void rx_kernel(RxArgs a) {
                 uint32_t* dst = reinterpret_cast<uint32_t*>(L.win + (q >> 2) * kSlot + 16 * (q & 3));
                 dst[0] = g[i].x; dst[1] = g[i].y; dst[2] = g[i].z; dst[3] = g[i].w;
             }
+        } else if (kMixedLA) {
+            uint4 g[16];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int q = i * kWave + lane;
+                const int fl = q >> 4;
+                const int c = (q & 15) - (int)((L.base[fl] >> 4) & 7u);
+                g[i] = make_uint4(0, 0, 0, 0);
+                if (c >= 0 && (uint32_t)(16 * c) < L.end[fl]) g[i] = load16(a.data + L.base[fl] + 16 * c);
+            }
+            fetch_desc(nrun);
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int q = i * kWave + lane;
+                const int fl = q >> 4;
+                const int c = (q & 15) - (int)((L.base[fl] >> 4) & 7u);
+                if (c >= 0 && c < NW) {
+                    uint32_t* dst = reinterpret_cast<uint32_t*>(L.win + fl * kSlot + 16 * c);
+                    dst[0] = g[i].x; dst[1] = g[i].y; dst[2] = g[i].z; dst[3] = g[i].w;
+                }
+                // bytes past the window: summed, masked at the frame's end
+                uint32_t part = 0;
+                if (c >= NW) {
+                    const int hi = (int)L.end[fl] - 16 * c;
+                    part = sad(g[i].x & first_bytes(clamp04(hi)), part);
+                    part = sad(g[i].y & first_bytes(clamp04(hi - 4)), part);
+                    part = sad(g[i].z & first_bytes(clamp04(hi - 8)), part);
+                    part = sad(g[i].w & first_bytes(clamp04(hi - 12)), part);
+                }
+                if (__ballot(part != 0u)) {       // a 16-lane row = one frame
+#pragma unroll
+                    for (int o = 8; o >= 1; o >>= 1) part += __shfl_xor(part, o);
+                }
+                if ((q & 15) == 0) L.tail[fl] = part;
+            }
         } else if (PASS != 1) {
             uint4 g[NW];
 #pragma unroll
@@ -347,11 +397,11 @@ __global__ __launch_bounds__(kBlock, NW < 8 ? 5 : 4) void rx_kernel(RxArgs a) {
         // flight); the parse then trims it to the L4 range B, which in every
         // well-formed frame already runs to the end of the frame. Unified pass:
         // the group loop also fills the window of every frame.
-        const bool has_tail = PASS == 1 ? in_batch : long_frame;
+        const bool has_tail = PASS == 1 ? in_batch : kMixedLA ? span > 16u - lo_g : long_frame;
         const uint64_t tmask = __ballot(has_tail);
         if (tmask) {
             // DYN: frames needing more than one group round go first
-            const bool big = DYN && has_tail && span > (uint32_t)(NW + G * U);
+            const bool big = DYN && has_tail && span > (kMixedLA ? 16u - lo_g : (uint32_t)NW) + (uint32_t)(G * U);
             const uint64_t bmask = __ballot(big);
             const uint64_t below = (1ull << lane) - 1ull;
             if (has_tail) {
@@ -362,7 +412,7 @@ __global__ __launch_bounds__(kBlock, NW < 8 ? 5 : 4) void rx_kernel(RxArgs a) {
             if (DYN && lane == 0) L.qhead = kWave / G;
             wave_sync();
             tail_sums<NW, G, U, NT, (PASS != 0), DYN, (PNET_MTU_ALT && PASS == 1 && !DYN),
-                      (PNET_LINE_ALIGN && PASS == 1 && !DYN && G % 8 == 0)>(
+                      (PNET_LINE_ALIGN && PASS == 1 && !DYN && G % 8 == 0), kMixedLA>(
                 a.data, L, lane, __popcll(tmask) PNET_TAIL_STAT);
         }
         wave_sync();
