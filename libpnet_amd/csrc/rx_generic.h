@@ -20,6 +20,9 @@ namespace {
 #ifndef PNET_MIXED_LA
 #define PNET_MIXED_LA 0   // A/B: the mixed shape's window = the frame's first two whole lines
 #endif
+#ifndef PNET_MLA_INFLIGHT
+#define PNET_MLA_INFLIGHT 12   // of its 16 load instructions in flight at once (VGPR budget)
+#endif
 #ifndef PNET_LINE_ALIGN
 #define PNET_LINE_ALIGN 0   // A/B: the MTU shape's groups stream whole 128-B lines (tail_sums LA)
 #endif
@@ -335,40 +338,51 @@ __global__ __launch_bounds__(kBlock, NW < 8 ? 5 : 4) void rx_kernel(RxArgs a) {
                 dst[0] = g[i].x; dst[1] = g[i].y; dst[2] = g[i].z; dst[3] = g[i].w;
             }
         } else if (kMixedLA) {
-            uint4 g[16];
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
+            // 16 instructions (4 frames x 2 lines each), 12 in flight: the last
+            // four reuse the registers of the first four once those are consumed
+            uint4 g[PNET_MLA_INFLIGHT];
+            auto issue = [&](int i, uint4& dst) {
                 const int q = i * kWave + lane;
                 const int fl = q >> 4;
                 const int c = (q & 15) - (int)((L.base[fl] >> 4) & 7u);
-                g[i] = make_uint4(0, 0, 0, 0);
-                if (c >= 0 && (uint32_t)(16 * c) < L.end[fl]) g[i] = load16(a.data + L.base[fl] + 16 * c);
-            }
-            fetch_desc(nrun);
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
+                dst = make_uint4(0, 0, 0, 0);
+                if (c >= 0 && (uint32_t)(16 * c) < L.end[fl]) dst = load16(a.data + L.base[fl] + 16 * c);
+            };
+            auto consume = [&](int i, const uint4& v) {
                 const int q = i * kWave + lane;
                 const int fl = q >> 4;
                 const int c = (q & 15) - (int)((L.base[fl] >> 4) & 7u);
                 if (c >= 0 && c < NW) {
                     uint32_t* dst = reinterpret_cast<uint32_t*>(L.win + fl * kSlot + 16 * c);
-                    dst[0] = g[i].x; dst[1] = g[i].y; dst[2] = g[i].z; dst[3] = g[i].w;
+                    dst[0] = v.x; dst[1] = v.y; dst[2] = v.z; dst[3] = v.w;
                 }
-                // bytes past the window: summed, masked at the frame's end
-                uint32_t part = 0;
+                uint32_t part = 0;                           // bytes past the window, masked at the frame's end
                 if (c >= NW) {
                     const int hi = (int)L.end[fl] - 16 * c;
-                    part = sad(g[i].x & first_bytes(clamp04(hi)), part);
-                    part = sad(g[i].y & first_bytes(clamp04(hi - 4)), part);
-                    part = sad(g[i].z & first_bytes(clamp04(hi - 8)), part);
-                    part = sad(g[i].w & first_bytes(clamp04(hi - 12)), part);
+                    part = sad(v.x & first_bytes(clamp04(hi)), part);
+                    part = sad(v.y & first_bytes(clamp04(hi - 4)), part);
+                    part = sad(v.z & first_bytes(clamp04(hi - 8)), part);
+                    part = sad(v.w & first_bytes(clamp04(hi - 12)), part);
                 }
-                if (__ballot(part != 0u)) {       // a 16-lane row = one frame
+                if (__ballot(part != 0u)) {                  // a 16-lane row = one frame
 #pragma unroll
                     for (int o = 8; o >= 1; o >>= 1) part += __shfl_xor(part, o);
                 }
                 if ((q & 15) == 0) L.tail[fl] = part;
+            };
+#pragma unroll
+            for (int i = 0; i < PNET_MLA_INFLIGHT; ++i) issue(i, g[i]);
+            fetch_desc(nrun);
+            constexpr int kRe = 16 - PNET_MLA_INFLIGHT;   // instructions issued late
+#pragma unroll
+            for (int i = 0; i < kRe; ++i) {
+                consume(i, g[i]);
+                issue(PNET_MLA_INFLIGHT + i, g[i]);
             }
+#pragma unroll
+            for (int i = kRe; i < PNET_MLA_INFLIGHT; ++i) consume(i, g[i]);
+#pragma unroll
+            for (int i = 0; i < kRe; ++i) consume(PNET_MLA_INFLIGHT + i, g[i]);
         } else if (PASS != 1) {
             uint4 g[NW];
 #pragma unroll
