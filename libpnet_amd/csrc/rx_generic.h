@@ -17,15 +17,6 @@ namespace {
 // ============================================================================
 // rx_kernel: generic (descriptor mode, any alignment, any length).
 // ============================================================================
-#ifndef PNET_MIXED_LA
-#define PNET_MIXED_LA 0   // A/B: the mixed shape's window = the frame's first two whole lines
-#endif
-#ifndef PNET_MLA_INFLIGHT
-#define PNET_MLA_INFLIGHT 12   // of its 16 load instructions in flight at once (VGPR budget)
-#endif
-#ifndef PNET_LINE_ALIGN
-#define PNET_LINE_ALIGN 0   // A/B: the MTU shape's groups stream whole 128-B lines (tail_sums LA)
-#endif
 #ifndef PNET_MTU_ALT
 #define PNET_MTU_ALT 1   // the MTU shape streams odd frames backward (below; A/B: 0)
 #endif
@@ -77,18 +68,7 @@ __device__ __forceinline__ uint32_t lane_range_sum(const uint8_t* fb, int lo, in
 // frame's start is read by both groups in the same round (even frame: its
 // last round; odd frame: its last round, which then covers its start), instead
 // of rounds apart (the second read then comes from L2, not HBM).
-// LA (line-aligned, PNET_LINE_ALIGN; groups of 8 lanes): the group streams
-// whole 128-B lines — granule c = A + stream index, A the first granule of
-// the line holding the stream's start — so that each wave load instruction
-// asks the L1 for one line per group instead of straddling two (lanes outside
-// the frame's range are predicated off: no extra line is requested). The
-// vector memory path (TA/TD/L1) is the kernels' bound (profiles/r04/pmc_mem/),
-// so the number of L1->L2 requests per byte is what the stream pays for.
-// MLA (the mixed shape's line-aligned window, PNET_MIXED_LA): the window
-// phase read the frame's first two whole lines and summed their bytes past
-// the window into L.tail; the groups start at the third line (granule
-// 16 - lo) and add their sums.
-template <int NW, int G, int U, bool NT, bool UNI, bool DYN, bool ALT = false, bool LA = false, bool MLA = false>
+template <int NW, int G, int U, bool NT, bool UNI, bool DYN, bool ALT = false>
 __device__ __forceinline__ void tail_sums(const uint8_t* data, WaveLds<NW>& L, int lane, int count
 #ifdef PNET_WAVE_TIMES
                                           , uint64_t (&stat)[3]
@@ -98,33 +78,18 @@ __device__ __forceinline__ void tail_sums(const uint8_t* data, WaveLds<NW>& L, i
     constexpr int kSlot = WaveLds<NW>::kSlot;
     constexpr uint32_t c_first = UNI ? 0u : (uint32_t)NW;
     static_assert(!UNI || G * U >= NW, "the first round must cover the window");
-    static_assert(!LA || G % 8 == 0, "line-aligned groups cover whole 8-granule lines");
     const int j = lane % G;
     int idx = lane / G;
     int fl = 0;
     uint32_t fe = 0, nneed = 0, c0 = 0, acc = 0;
-    int la0 = 0;          // LA: first granule (frame-relative, may be < 0) of the stream's first line
-    uint32_t lalen = 0;   // LA: stream length in granules (whole lines)
     const uint8_t* fb = data;
-    auto start = [&]() {
+    if (idx < count) {
         fl = L.list[idx];
         fe = L.end[fl];
         fb = data + L.base[fl];
         nneed = (fe + 15u) >> 4;
-        if (LA) {
-            const uint32_t lo = (uint32_t)(L.base[fl] >> 4) & 7u;          // granule of base in its line
-            const uint32_t nend = UNI ? max(nneed, (uint32_t)NW) : nneed;   // UNI: the whole window too
-            la0 = (int)c_first - (int)((lo + c_first) & 7u);
-            const int lend = (int)nend + (int)((8u - ((lo + nend) & 7u)) & 7u);
-            lalen = (uint32_t)(lend - la0);
-            c0 = (uint32_t)j;
-        } else if (MLA) {
-            c0 = 16u - ((uint32_t)(L.base[fl] >> 4) & 7u) + j;
-        } else {
-            c0 = c_first + j;
-        }
-    };
-    if (idx < count) start();
+        c0 = c_first + j;
+    }
 #ifdef PNET_WAVE_TIMES
     uint32_t iters = 0, issued = 0;
 #endif
@@ -137,30 +102,17 @@ __device__ __forceinline__ void tail_sums(const uint8_t* data, WaveLds<NW>& L, i
             uint4 v[U];
             // ALT: odd frames' granule order reversed (UNI: c_first = 0)
             const bool rev = ALT && (fl & 1);
-            // the granule stream index cs maps to (LA: whole lines, reversed by line)
-            auto gran = [&](uint32_t cs) -> int {
-                if (LA) {
-                    const int k = (int)(cs >> 3), t = (int)(cs & 7u);
-                    return rev ? la0 + (int)lalen - 8 * (k + 1) + t : la0 + (int)cs;
-                }
-                return (int)(rev && cs < nneed ? nneed - 1u - cs : cs);
-            };
-            auto live = [&](uint32_t cs, int c) {
-                return LA ? (c >= (int)c_first && c < (int)nneed) : cs < nneed;
-            };
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const uint32_t cs = c0 + u * G;
-                const int c = gran(cs);
-                v[u] = live(cs, c) ? (NT ? load16_nt(fb + 16 * c) : load16(fb + 16 * c)) : make_uint4(0, 0, 0, 0);
+                const uint32_t c = rev && cs < nneed ? nneed - 1u - cs : cs;
+                v[u] = cs < nneed ? (NT ? load16_nt(fb + 16u * c) : load16(fb + 16u * c)) : make_uint4(0, 0, 0, 0);
             }
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const uint32_t cs = c0 + u * G;
                 // past the frame (cs >= nneed): the same zero granule either way
-                const int ci = gran(cs);
-                if (LA && (ci < 0 || ci >= (int)(UNI ? max(nneed, (uint32_t)NW) : nneed))) continue;   // outside the frame's lines
-                const uint32_t c = (uint32_t)ci;
+                const uint32_t c = rev && cs < nneed ? nneed - 1u - cs : cs;
                 uint32_t x = v[u].x, y = v[u].y, z = v[u].z, w = v[u].w;
                 if (UNI && c < (uint32_t)NW) {                   // window granule -> the frame's slot
                     uint32_t* dst = reinterpret_cast<uint32_t*>(L.win + fl * kSlot + 16 * c);
@@ -180,10 +132,10 @@ __device__ __forceinline__ void tail_sums(const uint8_t* data, WaveLds<NW>& L, i
                 acc = sad(w, acc);
             }
             c0 += U * G;
-            if (c0 - j >= (LA ? lalen : (nneed > c_first ? nneed : c_first + 1u))) {   // group-uniform: frame done
+            if (c0 - j >= (nneed > c_first ? nneed : c_first + 1u)) {   // group-uniform: frame done
 #pragma unroll
                 for (int o = G / 2; o >= 1; o >>= 1) acc += __shfl_xor(acc, o);
-                if (j == 0) L.tail[fl] = MLA ? L.tail[fl] + acc : acc;
+                if (j == 0) L.tail[fl] = acc;
                 acc = 0;
                 if (DYN) {
                     uint32_t nidx = 0;
@@ -192,7 +144,13 @@ __device__ __forceinline__ void tail_sums(const uint8_t* data, WaveLds<NW>& L, i
                 } else {
                     idx += kGroups;
                 }
-                if (idx < count) start();
+                if (idx < count) {
+                    fl = L.list[idx];
+                    fe = L.end[fl];
+                    fb = data + L.base[fl];
+                    nneed = (fe + 15u) >> 4;
+                    c0 = c_first + j;
+                }
             }
         }
     }
@@ -227,11 +185,6 @@ __global__ __launch_bounds__(kBlock, NW < 8 ? 5 : 4) void rx_kernel(RxArgs a) {
     // mixed shape's plain instantiation: no dispatch flags, header-field
     // columns or TX)
     constexpr bool kShortRuns = PNET_SHORT_RUNS && PASS == 0 && DYN && !EXT && !TX;
-    // the mixed shape's line-aligned window (PNET_MIXED_LA): granules [-lo, 16 - lo)
-    // of each frame (its first two whole 128-B lines, lo = base's granule in
-    // its line), the slot's NW granules stored, the rest summed into L.tail by
-    // a 16-lane row reduction; the tail groups start at the third line
-    constexpr bool kMixedLA = PNET_MIXED_LA && PASS == 0 && DYN && NW == 8;
     // the short-run realignment reads slot dwords up to byte sh + 67 (sh <= 15)
     static_assert(!kShortRuns || kSlot >= 15 + 68, "short runs need a slot of at least 83 B");
 
@@ -303,8 +256,7 @@ __global__ __launch_bounds__(kBlock, NW < 8 ? 5 : 4) void rx_kernel(RxArgs a) {
         const uint32_t span = (fend + 15u) >> 4;
         const bool long_frame = fend > (uint32_t)kWin;
         L.base[lane] = base;
-        L.end[lane] = kMixedLA ? fend : span < (uint32_t)NW ? span : (uint32_t)NW;   // granules to load into the window
-        const uint32_t lo_g = (uint32_t)(base >> 4) & 7u;     // base's granule in its 128-B line (kMixedLA)
+        L.end[lane] = span < (uint32_t)NW ? span : (uint32_t)NW;   // granules to load into the window
         wave_sync();
 
         // short run (descriptor batches of minimum-size frames: the AF_PACKET /
@@ -337,52 +289,6 @@ __global__ __launch_bounds__(kBlock, NW < 8 ? 5 : 4) void rx_kernel(RxArgs a) {
                 uint32_t* dst = reinterpret_cast<uint32_t*>(L.win + (q >> 2) * kSlot + 16 * (q & 3));
                 dst[0] = g[i].x; dst[1] = g[i].y; dst[2] = g[i].z; dst[3] = g[i].w;
             }
-        } else if (kMixedLA) {
-            // 16 instructions (4 frames x 2 lines each), 12 in flight: the last
-            // four reuse the registers of the first four once those are consumed
-            uint4 g[PNET_MLA_INFLIGHT];
-            auto issue = [&](int i, uint4& dst) {
-                const int q = i * kWave + lane;
-                const int fl = q >> 4;
-                const int c = (q & 15) - (int)((L.base[fl] >> 4) & 7u);
-                dst = make_uint4(0, 0, 0, 0);
-                if (c >= 0 && (uint32_t)(16 * c) < L.end[fl]) dst = load16(a.data + L.base[fl] + 16 * c);
-            };
-            auto consume = [&](int i, const uint4& v) {
-                const int q = i * kWave + lane;
-                const int fl = q >> 4;
-                const int c = (q & 15) - (int)((L.base[fl] >> 4) & 7u);
-                if (c >= 0 && c < NW) {
-                    uint32_t* dst = reinterpret_cast<uint32_t*>(L.win + fl * kSlot + 16 * c);
-                    dst[0] = v.x; dst[1] = v.y; dst[2] = v.z; dst[3] = v.w;
-                }
-                uint32_t part = 0;                           // bytes past the window, masked at the frame's end
-                if (c >= NW) {
-                    const int hi = (int)L.end[fl] - 16 * c;
-                    part = sad(v.x & first_bytes(clamp04(hi)), part);
-                    part = sad(v.y & first_bytes(clamp04(hi - 4)), part);
-                    part = sad(v.z & first_bytes(clamp04(hi - 8)), part);
-                    part = sad(v.w & first_bytes(clamp04(hi - 12)), part);
-                }
-                if (__ballot(part != 0u)) {                  // a 16-lane row = one frame
-#pragma unroll
-                    for (int o = 8; o >= 1; o >>= 1) part += __shfl_xor(part, o);
-                }
-                if ((q & 15) == 0) L.tail[fl] = part;
-            };
-#pragma unroll
-            for (int i = 0; i < PNET_MLA_INFLIGHT; ++i) issue(i, g[i]);
-            fetch_desc(nrun);
-            constexpr int kRe = 16 - PNET_MLA_INFLIGHT;   // instructions issued late
-#pragma unroll
-            for (int i = 0; i < kRe; ++i) {
-                consume(i, g[i]);
-                issue(PNET_MLA_INFLIGHT + i, g[i]);
-            }
-#pragma unroll
-            for (int i = kRe; i < PNET_MLA_INFLIGHT; ++i) consume(i, g[i]);
-#pragma unroll
-            for (int i = 0; i < kRe; ++i) consume(PNET_MLA_INFLIGHT + i, g[i]);
         } else if (PASS != 1) {
             uint4 g[NW];
 #pragma unroll
@@ -411,11 +317,11 @@ __global__ __launch_bounds__(kBlock, NW < 8 ? 5 : 4) void rx_kernel(RxArgs a) {
         // flight); the parse then trims it to the L4 range B, which in every
         // well-formed frame already runs to the end of the frame. Unified pass:
         // the group loop also fills the window of every frame.
-        const bool has_tail = PASS == 1 ? in_batch : kMixedLA ? span > 16u - lo_g : long_frame;
+        const bool has_tail = PASS == 1 ? in_batch : long_frame;
         const uint64_t tmask = __ballot(has_tail);
         if (tmask) {
             // DYN: frames needing more than one group round go first
-            const bool big = DYN && has_tail && span > (kMixedLA ? 16u - lo_g : (uint32_t)NW) + (uint32_t)(G * U);
+            const bool big = DYN && has_tail && span > (uint32_t)(NW + G * U);
             const uint64_t bmask = __ballot(big);
             const uint64_t below = (1ull << lane) - 1ull;
             if (has_tail) {
@@ -425,8 +331,7 @@ __global__ __launch_bounds__(kBlock, NW < 8 ? 5 : 4) void rx_kernel(RxArgs a) {
             }
             if (DYN && lane == 0) L.qhead = kWave / G;
             wave_sync();
-            tail_sums<NW, G, U, NT, (PASS != 0), DYN, (PNET_MTU_ALT && PASS == 1 && !DYN),
-                      (PNET_LINE_ALIGN && PASS == 1 && !DYN && G % 8 == 0), kMixedLA>(
+            tail_sums<NW, G, U, NT, (PASS != 0), DYN, (PNET_MTU_ALT && PASS == 1 && !DYN)>(
                 a.data, L, lane, __popcll(tmask) PNET_TAIL_STAT);
         }
         wave_sync();
