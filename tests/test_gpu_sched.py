@@ -185,3 +185,26 @@ def test_slice_kernels_claim_path(pct, nctr, tune):
     so = 3 + 20 * np.arange(ns, dtype=np.uint64)
     swant = coracle.checksum_slices(sbuf, so, np.full(ns, 20, np.uint32), np.full(ns, 5, np.uint32))
     assert np.array_equal(got, swant)
+
+
+def test_more_streams_than_slots(tune):
+    """A context gives its first 64 distinct streams a counter slot each; a
+    launch on any further stream runs the static schedule. 70 streams, two
+    launches each with no host synchronization: every record equal to the
+    oracle-checked one and no claim ever saw a foreign epoch."""
+    n = 8 * 1024 * 64
+    w = lp.synth.make("udp64", n, seed=16, corrupt_ppm=10000)
+    rec, lens = _oracle(w, n)
+    want = oracle_counters(rec, lens)
+    dv = _Dev(w)
+    tune("blocks_per_cu", 1)
+    tune("static_pct", 25)
+    streams = [torch.cuda.Stream() for _ in range(70)]
+    results = [dv.run(n, stream=streams[i % 70], cols=("status", "l4_csum")) for i in range(140)]
+    torch.cuda.synchronize()
+    compare(results[0], rec)
+    for i, r in enumerate(results):
+        for c, col in r.columns.items():
+            assert torch.equal(col, results[0].columns[c]), (i, c)
+        assert r.counter_dict() == want, i
+    assert lp.engine.context(0).sched_conflicts() == 0
