@@ -28,6 +28,19 @@ def main():
                lp.ipv4_checksum_slices(b, o, ln, k, ad, pr, stream=s)) if pseudo else
               (lambda b=buf, o=offs, ln=lens, k=skips: lp.checksum_slices(b, o, ln, k, stream=s)))
         cases.append((name, n, size, fn))
+    # the 20-B shape through 8-B compact descriptors, and descriptor slices of 64 / 256 B
+    cbuf = torch.randint(0, 256, ((1 << 24) * 20 + 32,), dtype=torch.uint8, device=dev)
+    n = 1 << 24
+    cdesc = lp.slice_descriptors(np.arange(n, dtype=np.uint64) * 20, np.full(n, 20, np.uint32),
+                                 np.full(n, 5, np.uint32), device=dev)
+    cases.append(("small20_compact", n, 20, lambda b=cbuf, dc=cdesc: lp.checksum_slices_compact(b, dc, stream=s)))
+    for size, n in ((64, 1 << 23), (256, 1 << 22)):
+        buf = torch.randint(0, 256, (n * size + 32,), dtype=torch.uint8, device=dev)
+        offs = torch.arange(n, dtype=torch.int64, device=dev) * size
+        lens = torch.full((n,), size, dtype=torch.int32, device=dev)
+        skips = torch.full((n,), 5, dtype=torch.int32, device=dev)
+        cases.append((f"d{size}", n, size, lambda b=buf, o=offs, ln=lens, k=skips: lp.checksum_slices(b, o, ln, k,
+                                                                                                   stream=s)))
     # the reference's 20-B shape as uniform slices (no descriptors)
     sbuf = torch.randint(0, 256, ((1 << 24) * 20 + 32,), dtype=torch.uint8, device=dev)
     cases.append(("strided20", 1 << 24, 20,
