@@ -50,14 +50,15 @@
  *     round_up(data + data_bytes, 16). (hipMalloc'd buffers always are.)
  *   - Threading: a context is bound to one device; calls on one context may be
  *     issued from one host thread at a time. Distinct contexts are independent.
- *     Any number of launches may be in flight, on any streams: the run-claim
- *     counters (run scheduling) are owned per stream — launches
- *     on one stream run in stream order and reuse their stream's counter slot;
- *     the first 64 distinct streams a context sees get a slot each, launches on
- *     later streams use the static schedule (same results, no claims). A
- *     stream handle must not be destroyed while its work is in flight and
- *     then reused for another stream of the same context (a reused slot is
- *     detected on the device and counted: pnetgpu_ctx_sched_conflicts).
+ *     Any number of launches may be in flight, on any streams, and launches
+ *     may be captured into HIP graphs and replayed: a launch that balances its
+ *     runs by claims (run scheduling) holds a counter block of
+ *     the context's pool that no unfinished launch holds, whatever the streams
+ *     (its last wave hands the block back, zeroed, through pinned host
+ *     memory); with all 64 blocks held, and for every launch captured into a
+ *     graph, the launch runs the static schedule — the same results without
+ *     claims (pnetgpu_ctx_sched_stats counts each case). No launch can see
+ *     another's counters, so destroyed and reused stream handles need no care.
  *   - Malformed input never faults: frames whose descriptor falls outside
  *     [0, data_bytes) get PNET_ST_DESC_INVALID, short frames get the
  *     *_MALFORMED bits (the reference's `new()` returning None).
@@ -248,18 +249,31 @@ void pnetgpu_ctx_destroy(pnetgpu_ctx* ctx);
 #define PNETGPU_TUNE_SLICE_KERNEL        5  /* descriptor slices: 1 slice_run_kernel, 2 slice_kernel       */
 #define PNETGPU_TUNE_SLICE_DENSE_SPAN    6  /* bytes a run of small slices must span to be LDS-staged (default 2048) */
 #define PNETGPU_TUNE_DEBUG               7  /* 1: log each receive call's kernel and grid to stderr        */
-#define PNETGPU_TUNE_SCHED_EPOCH         8  /* test hook: raise every stream slot's launch epoch to at least
-                                             * this (0..2^32-1), so a test reaches the epoch wrap, where the
-                                             * slot is re-zeroed in stream order                             */
+#define PNETGPU_TUNE_SCHED_EPOCH         8  /* retired (per-stream epochs, ABI v3 before the counter pool):
+                                             * 0..2^32-1 accepted and ignored                                 */
 #define PNETGPU_NTUNE                    9
 int pnetgpu_ctx_set_tuning(pnetgpu_ctx* ctx, int key, int64_t value);
 int pnetgpu_ctx_get_tuning(const pnetgpu_ctx* ctx, int key, int64_t* value);
 
-/* Claims of a launch that found its stream's counter slot taken by another
- * launch (a stream handle destroyed with work in flight and reused): the
- * number counted on the device since the context was created, 0 when the
- * schedule was never shared. Synchronises the context's device. */
+/* Kept for ABI v3 callers: claims that saw another launch's counters. Launches
+ * never share counters (each holds its own pool block), so *count is always 0;
+ * no device synchronisation. */
 int pnetgpu_ctx_sched_conflicts(pnetgpu_ctx* ctx, uint64_t* count);
+
+/* Run-scheduling counts of a context since its creation (host-side, no
+ * synchronisation): stats[PNETGPU_SCHED_CLAIMED] launches that took a counter
+ * block; [PNETGPU_SCHED_STATIC_BUSY] launches that ran static because every
+ * block was held by an unfinished launch; [PNETGPU_SCHED_STATIC_CAPTURED]
+ * launches captured into a graph (static by design); [PNETGPU_SCHED_BLOCKS_HELD]
+ * blocks held right now; [PNETGPU_SCHED_BLOCKS] the pool size. Launches too
+ * short to claim (fewer than 8 runs per wave, or STATIC_PCT 100) are in none. */
+#define PNETGPU_SCHED_CLAIMED          0
+#define PNETGPU_SCHED_STATIC_BUSY      1
+#define PNETGPU_SCHED_STATIC_CAPTURED  2
+#define PNETGPU_SCHED_BLOCKS_HELD      3
+#define PNETGPU_SCHED_BLOCKS           4
+#define PNETGPU_NSCHED_STATS           5
+int pnetgpu_ctx_sched_stats(const pnetgpu_ctx* ctx, uint64_t stats[PNETGPU_NSCHED_STATS]);
 
 /* Receive path: parse + verify every frame of `batch`, write `cols`. */
 int pnetgpu_rx_process(pnetgpu_ctx* ctx, const pnetgpu_batch* batch,

@@ -9,12 +9,14 @@
  * mode: offsets + lengths), pnetgpu_ring_submit() ships a full batch
  * asynchronously (hipMemcpyAsync H2D -> pnetgpu_rx_process -> D2H of every
  * result column) on the slot's own stream, and pnetgpu_ring_wait() hands back the
- * oldest finished batch's records in pinned host memory. Three slots rotate
- * (one filling, one in flight, one held by the application), so copies, kernel
- * and host work overlap.
+ * oldest finished batch's records in pinned host memory. Slots rotate (default
+ * PNETGPU_RING_DEFAULT_SLOTS: one filling, one held by the application, the
+ * rest in flight, each on its own stream), so the H2D of one batch overlaps the
+ * kernel and D2H of the previous ones and the application's host work.
  *
  * Validity: a waited batch (its frames and records) stays valid until the next
- * pnetgpu_ring_wait() on the same ring. Single-threaded use per ring.
+ * pnetgpu_ring_wait() or pnetgpu_ring_release() on the same ring.
+ * Single-threaded use per ring.
  */
 #ifndef PNETGPU_RING_H
 #define PNETGPU_RING_H
@@ -45,9 +47,22 @@ typedef struct pnetgpu_ring_batch {
     pnetgpu_rx_columns  cols;       /* host pointers; counters has PNETGPU_NCOUNTERS  */
 } pnetgpu_ring_batch;
 
-/* flags: PNETGPU_RX_* dispatch extensions applied to every batch */
+#define PNETGPU_RING_MIN_SLOTS      2   /* one held + one filling: no batch in flight while held */
+#define PNETGPU_RING_DEFAULT_SLOTS  4   /* held + filling + two in flight                         */
+#define PNETGPU_RING_MAX_SLOTS     16
+
+/* flags: PNETGPU_RX_* dispatch extensions applied to every batch;
+ * PNETGPU_RING_DEFAULT_SLOTS slots of batch_bytes / batch_frames each */
 int  pnetgpu_ring_create(pnetgpu_ctx* ctx, uint64_t batch_bytes, uint32_t batch_frames, uint32_t flags,
                          pnetgpu_ring** out);
+/* The same with nslots slots (PNETGPU_RING_MIN_SLOTS..PNETGPU_RING_MAX_SLOTS,
+ * else PNETGPU_EINVAL): nslots - 2 batches stay in flight while the application
+ * holds one and fills another. Each slot pins batch_bytes of host memory and
+ * allocates as much device memory. */
+int  pnetgpu_ring_create_ex(pnetgpu_ctx* ctx, uint64_t batch_bytes, uint32_t batch_frames, uint32_t flags,
+                            uint32_t nslots, pnetgpu_ring** out);
+/* Slot count of a ring (0 for NULL). */
+uint32_t pnetgpu_ring_slots(const pnetgpu_ring* ring);
 void pnetgpu_ring_destroy(pnetgpu_ring* ring);
 
 /* Copy one frame into the filling batch: 0, PNETGPU_EFULL or PNETGPU_EBUSY. */
@@ -110,8 +125,14 @@ int pnetgpu_ring_set_columns(pnetgpu_ring* ring, uint64_t column_mask);
 /* Page-lock existing host memory for direct DMA (hipHostRegister) and undo it. */
 int pnetgpu_host_register(void* p, uint64_t bytes);
 int pnetgpu_host_unregister(void* p);
-/* Block for the oldest submitted batch: 0 (fills *out) or PNETGPU_EEMPTY. */
+/* Block for the oldest submitted batch: 0 (fills *out) or PNETGPU_EEMPTY.
+ * Releases the batch the previous wait returned. */
 int pnetgpu_ring_wait(pnetgpu_ring* ring, pnetgpu_ring_batch* out);
+/* Release the batch the last wait returned now (its views become invalid), so
+ * its slot can take frames before the next wait: a consumer that is done with a
+ * batch releases it and keeps filling while the other slots are in flight. No-op
+ * when nothing is held. */
+int pnetgpu_ring_release(pnetgpu_ring* ring);
 
 /* Classic pcap reader (the pcap.rs:92 from_file receiver): LINKTYPE_ETHERNET,
  * microsecond or nanosecond magic, either byte order. next() returns the

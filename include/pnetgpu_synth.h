@@ -24,6 +24,7 @@ extern "C" {
 #define PNETGPU_SYNTH_TCP1500     2  /* config 3: 1500-B Eth/IPv4/TCP                        */
 #define PNETGPU_SYNTH_IMIX        3  /* config 4: 64/576/1500 B at 7:4:1, UDP/TCP/ICMP echo  */
 #define PNETGPU_SYNTH_UDP6_JUMBO  4  /* config 5: 9000-B Eth/IPv6/UDP                         */
+#define PNETGPU_SYNTH_UDP1500     5  /* north_star's 1500-B Eth/IPv4/UDP (1458 data bytes)    */
 
 /* expect[] slots written by pnetgpu_synth_fill */
 #define PNETGPU_SYNTH_EXP_IP_BAD  0

@@ -17,17 +17,15 @@
 #include "pnetgpu_ring.h"
 #include "rx_internal.h"
 
-// run-claim counter slots per context: one per stream (launches on one stream
-// run in order, so they reuse its slot; slot s's count is stamped by epoch)
-constexpr uint32_t kSchedSlots = 64;
-constexpr uint32_t kMaxCtrs = 128;                                   // counters per slot
+// run-claim counter blocks per context: each launch that claims runs takes a
+// block no other unfinished launch holds (abi.cpp plan_sched); its last wave
+// leaves the counters zero and marks the block free in pinned host memory
+constexpr uint32_t kSchedBlocks = 64;
+constexpr uint32_t kMaxCtrs = 128;                                   // counters per block
 constexpr size_t kCtrStride = 256 / sizeof(unsigned long long);      // 256 B apart
-constexpr size_t kSchedStride = kMaxCtrs * kCtrStride;
-// the slots, then one 256-B line holding the conflict count
-constexpr size_t kSchedBytes = (kSchedSlots * kSchedStride + kCtrStride) * sizeof(unsigned long long);
-// epochs of a slot must grow; the slot is re-zeroed in stream order before its
-// count would wrap
-constexpr uint32_t kEpochWrap = 0xFFFFFF00u;
+// a block: kMaxCtrs counters, then the groups-done line
+constexpr size_t kSchedStride = (kMaxCtrs + 1) * kCtrStride;
+constexpr size_t kSchedBytes = kSchedBlocks * kSchedStride * sizeof(unsigned long long);
 
 struct pnetgpu_ctx {
     int device;
@@ -36,12 +34,18 @@ struct pnetgpu_ctx {
     int per_cu[8][2] = {};
     // of each slice kernel: [strided, run, group] x pseudo {0, 4, 16} x extra
     int slice_per_cu[3][8][2] = {};
-    // run-claim counters of the launches (RunSched): kSchedSlots slots of
-    // kMaxCtrs counters, 256 B apart, owned by the stream in slot_stream
+    // run-claim counter blocks (RunSched): kSchedBlocks blocks of kSchedStride
+    // u64. Block b is free when done_host[b] (pinned, written by the last wave
+    // of the launch that held it) equals seq[b], the sequence number the host
+    // gave that launch.
     unsigned long long* d_sched = nullptr;
-    void* slot_stream[kSchedSlots] = {};
-    uint32_t slot_epoch[kSchedSlots] = {};
-    uint32_t nslots = 0;
+    uint32_t* done_host = nullptr;
+    uint32_t seq[kSchedBlocks] = {};
+    uint32_t next_seq = 0;
+    uint32_t next_block = 0;
+    uint64_t claimed_launches = 0;     // launches that took a block
+    uint64_t static_fallbacks = 0;     // launches that would have claimed, ran static: every block busy
+    uint64_t captured_static = 0;      // launches captured into a graph: static schedule
     // PNETGPU_TUNE_* (-1: default), from the environment at creation only
     int64_t tune[PNETGPU_NTUNE];
 };
@@ -89,34 +93,57 @@ constexpr int kRunFrames = 64;      // frames per wave-run
 // waves of a SIMD, the slower XCDs: tools/wave_times.py) do not set the
 // kernel's end. Launches of fewer than 8 units per wave stay static (1500-B
 // frames at 4 runs per wave: claims measured even to +1 %).
-// The counters are the stream's own slot: launches on one stream are ordered,
-// so the next one may stamp the slot (atomicMax of its epoch) only after the
-// previous one has finished with it; a stream beyond the 64 slots runs static.
-int plan_sched(pnetgpu_ctx* ctx, uint64_t nunits, uint64_t nwaves, void* stream, pnetgpu::RunSched* s) {
+// The counters are a block of the context's pool held by this launch alone,
+// whatever its stream: a block is handed out only after the launch that held
+// it last has finished (its last wave wrote the block's sequence number to
+// pinned host memory, RunQueue::finish), so launches on any streams, reused
+// stream handles and concurrent streams never share counters. With every block
+// held by unfinished launches, or while the stream is being captured into a
+// graph (a replayed launch would reuse the captured block and sequence number
+// while an earlier replay may still hold it), the launch runs the static
+// schedule: the same results without claims. *blk receives the block taken
+// (-1: none) and *prev its previous sequence number, for sched_undo.
+int plan_sched(pnetgpu_ctx* ctx, uint64_t nunits, uint64_t nwaves, void* stream, pnetgpu::RunSched* s, int* blk,
+               uint32_t* prev) {
     *s = pnetgpu::RunSched{};
+    *blk = -1;
     s->nstatic = nunits;
     const int64_t tp = tuning(ctx, PNETGPU_TUNE_STATIC_PCT);
     const int64_t static_pct = tp >= 0 ? tp : PNET_STATIC_PCT;
     if (static_pct >= 100 || nwaves == 0 || nunits < 8 * nwaves) return PNETGPU_OK;
-    uint32_t slot = 0;
-    while (slot < ctx->nslots && ctx->slot_stream[slot] != stream) ++slot;
-    if (slot == ctx->nslots) {
-        if (ctx->nslots == kSchedSlots) return PNETGPU_OK;   // no slot left for this stream: static
-        ctx->slot_stream[ctx->nslots] = stream;
-        ctx->slot_epoch[ctx->nslots++] = (uint32_t)std::max<int64_t>(0, tuning(ctx, PNETGPU_TUNE_SCHED_EPOCH));
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(static_cast<hipStream_t>(stream), &cs) != hipSuccess) {
+        (void)hipGetLastError();
+        cs = hipStreamCaptureStatusActive;       // unknown: the safe choice
     }
-    unsigned long long* ctr = ctx->d_sched + (size_t)slot * kSchedStride;
-    uint32_t e = ++ctx->slot_epoch[slot];
-    if (e >= kEpochWrap) {   // re-zero the slot behind the stream's earlier launches
-        const hipError_t he = hipMemsetAsync(ctr, 0, kSchedStride * sizeof(unsigned long long),
-                                             static_cast<hipStream_t>(stream));
-        if (he != hipSuccess) return pnetgpu::hip_fail(he);
-        ctx->slot_epoch[slot] = e = 1;
+    if (cs != hipStreamCaptureStatusNone) {
+        ++ctx->captured_static;
+        return PNETGPU_OK;
     }
+    uint32_t b = kSchedBlocks;
+    for (uint32_t i = 0; i < kSchedBlocks; ++i) {
+        const uint32_t c = (ctx->next_block + i) % kSchedBlocks;
+        if (__atomic_load_n(&ctx->done_host[c], __ATOMIC_ACQUIRE) == ctx->seq[c]) {
+            b = c;
+            break;
+        }
+    }
+    if (b == kSchedBlocks) {
+        ++ctx->static_fallbacks;
+        return PNETGPU_OK;
+    }
+    ctx->next_block = (b + 1) % kSchedBlocks;
+    *blk = (int)b;
+    *prev = ctx->seq[b];
+    if (++ctx->next_seq == ctx->seq[b]) ++ctx->next_seq;   // never the value the block's word already holds
+    ctx->seq[b] = ctx->next_seq;
+    ++ctx->claimed_launches;
+    unsigned long long* ctr = ctx->d_sched + (size_t)b * kSchedStride;
     s->nstatic = (nunits * (uint64_t)static_pct / 100) / nwaves * nwaves;
-    s->epoch = e;
     s->ctr = ctr;
-    s->conflicts = ctx->d_sched + (size_t)kSchedSlots * kSchedStride;
+    s->groups_done = ctr + (size_t)kMaxCtrs * kCtrStride;
+    s->done_host = ctx->done_host + b;
+    s->seq = ctx->seq[b];
     const int64_t tn = tuning(ctx, PNETGPU_TUNE_CLAIM_COUNTERS);
     const uint64_t nctr = tn > 0 ? (uint64_t)tn : PNET_CLAIM_COUNTERS;
     // every counter needs home waves: wave ids [0, 32 nctr) cover them all
@@ -124,6 +151,13 @@ int plan_sched(pnetgpu_ctx* ctx, uint64_t nunits, uint64_t nwaves, void* stream,
     s->nctr = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>({nctr, kMaxCtrs, homes}));
     s->ctr_stride = (uint32_t)kCtrStride;
     return PNETGPU_OK;
+}
+
+// A launch that took a block failed to start: the block is free again.
+void sched_undo(pnetgpu_ctx* ctx, int blk, uint32_t prev) {
+    if (blk < 0) return;
+    ctx->seq[blk] = prev;
+    --ctx->claimed_launches;
 }
 
 // PNETGPU_<NAME> of each tuning key, read once when a context is created
@@ -144,7 +178,7 @@ bool tuning_valid(int key, int64_t v) {
     case PNETGPU_TUNE_SLICE_KERNEL: return v == 1 || v == 2;
     case PNETGPU_TUNE_SLICE_DENSE_SPAN: return v >= 0 && v <= 65536;
     case PNETGPU_TUNE_DEBUG: return v == 0 || v == 1;
-    case PNETGPU_TUNE_SCHED_EPOCH: return v >= 0 && v <= (int64_t)UINT32_MAX;
+    case PNETGPU_TUNE_SCHED_EPOCH: return v >= 0 && v <= (int64_t)UINT32_MAX;   // retired: accepted, ignored
     default: return false;
     }
 }
@@ -225,10 +259,13 @@ int pnetgpu_ctx_create(int device, pnetgpu_ctx** out) {
     c->device = device;
     c->cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
     tuning_from_env(c);
-    if (hipMalloc((void**)&c->d_sched, kSchedBytes) != hipSuccess) {
-        delete c;
+    if (hipMalloc((void**)&c->d_sched, kSchedBytes) != hipSuccess ||
+        hipHostMalloc((void**)&c->done_host, kSchedBlocks * sizeof(uint32_t),
+                      hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
+        pnetgpu_ctx_destroy(c);
         return PNETGPU_ENOMEM;
     }
+    for (uint32_t i = 0; i < kSchedBlocks; ++i) c->done_host[i] = 0;   // == seq[i]: every block free
     if (hipMemset(c->d_sched, 0, kSchedBytes) != hipSuccess) {
         pnetgpu_ctx_destroy(c);
         return PNETGPU_EHIP;
@@ -240,9 +277,6 @@ int pnetgpu_ctx_create(int device, pnetgpu_ctx** out) {
 int pnetgpu_ctx_set_tuning(pnetgpu_ctx* ctx, int key, int64_t value) {
     if (!ctx || key < 0 || key >= PNETGPU_NTUNE || !tuning_valid(key, value)) return PNETGPU_EINVAL;
     ctx->tune[key] = value;
-    if (key == PNETGPU_TUNE_SCHED_EPOCH && value > 0)   // only ever upward: a stamped slot keeps growing
-        for (uint32_t i = 0; i < ctx->nslots; ++i)
-            ctx->slot_epoch[i] = std::max(ctx->slot_epoch[i], (uint32_t)value);
     return PNETGPU_OK;
 }
 
@@ -255,22 +289,28 @@ int pnetgpu_ctx_get_tuning(const pnetgpu_ctx* ctx, int key, int64_t* value) {
 int pnetgpu_ctx_sched_conflicts(pnetgpu_ctx* ctx, uint64_t* count) {
     pnetgpu::set_last_hip_error(0);
     if (!ctx || !count) return PNETGPU_EINVAL;
-    if (const int rc = set_device(ctx)) return rc;
-    if (const hipError_t e = hipDeviceSynchronize(); e != hipSuccess) return pnetgpu::hip_fail(e);
-    unsigned long long v = 0;
-    const hipError_t e = hipMemcpy(&v, ctx->d_sched + (size_t)kSchedSlots * kSchedStride, sizeof(v),
-                                   hipMemcpyDeviceToHost);
-    if (e != hipSuccess) return pnetgpu::hip_fail(e);
-    *count = v;
+    *count = 0;   // launches never share counters (plan_sched): nothing to report
+    return PNETGPU_OK;
+}
+
+int pnetgpu_ctx_sched_stats(const pnetgpu_ctx* ctx, uint64_t stats[PNETGPU_NSCHED_STATS]) {
+    if (!ctx || !stats) return PNETGPU_EINVAL;
+    stats[PNETGPU_SCHED_CLAIMED] = ctx->claimed_launches;
+    stats[PNETGPU_SCHED_STATIC_BUSY] = ctx->static_fallbacks;
+    stats[PNETGPU_SCHED_STATIC_CAPTURED] = ctx->captured_static;
+    uint64_t busy = 0;
+    for (uint32_t i = 0; i < kSchedBlocks; ++i)
+        busy += __atomic_load_n(&ctx->done_host[i], __ATOMIC_ACQUIRE) != ctx->seq[i];
+    stats[PNETGPU_SCHED_BLOCKS_HELD] = busy;
+    stats[PNETGPU_SCHED_BLOCKS] = kSchedBlocks;
     return PNETGPU_OK;
 }
 
 void pnetgpu_ctx_destroy(pnetgpu_ctx* ctx) {
     if (!ctx) return;
-    if (ctx->d_sched) {
-        (void)hipSetDevice(ctx->device);
-        (void)hipFree(ctx->d_sched);
-    }
+    (void)hipSetDevice(ctx->device);
+    if (ctx->d_sched) (void)hipFree(ctx->d_sched);
+    if (ctx->done_host) (void)hipHostFree(ctx->done_host);
     delete ctx;
 }
 
@@ -346,8 +386,11 @@ static int rx_common(pnetgpu_ctx* ctx, const pnetgpu_batch* b, const pnetgpu_rx_
     const uint64_t want = (a.nruns + wpb - 1) / wpb;
     const uint64_t cap = (uint64_t)ctx->cus * (uint64_t)per_cu;
     const int blocks = (int)std::max<uint64_t>(1, std::min(want, cap));
-    if (const int rc = plan_sched(ctx, a.nruns, (uint64_t)blocks * wpb, stream, &a.sched)) return rc;
+    int blk;
+    uint32_t prev;
+    if (const int rc = plan_sched(ctx, a.nruns, (uint64_t)blocks * wpb, stream, &a.sched, &blk, &prev)) return rc;
     if (const int e = pnetgpu::launch_rx(a, kind, blocks, tx, static_cast<hipStream_t>(stream))) {
+        sched_undo(ctx, blk, prev);
         pnetgpu::set_last_hip_error(e);
         if (debug)
             std::fprintf(stderr, "[pnetgpu] rx launch failed: %s (%d)\n", hipGetErrorString((hipError_t)e), e);
@@ -424,8 +467,13 @@ static int slices_common(pnetgpu_ctx* ctx, const uint8_t* data, uint64_t data_by
     const uint64_t per_block = run ? kBlock : kBlock / 16;
     const int blocks = slice_grid(ctx, run ? 1 : 2, pseudo, extra_offsets != nullptr, (n + per_block - 1) / per_block);
     // scheduled units: slice_run_kernel's runs of 64 slices, slice_kernel's 4
-    if ((rc = plan_sched(ctx, run ? (n + 63) / 64 : (n + 3) / 4, (uint64_t)blocks * 4, stream, &a.sched))) return rc;
+    int blk;
+    uint32_t prev;
+    if ((rc = plan_sched(ctx, run ? (n + 63) / 64 : (n + 3) / 4, (uint64_t)blocks * 4, stream, &a.sched, &blk,
+                         &prev)))
+        return rc;
     if (const int e = pnetgpu::launch_slices(a, pseudo, run, blocks, static_cast<hipStream_t>(stream))) {
+        sched_undo(ctx, blk, prev);
         pnetgpu::set_last_hip_error(e);
         return PNETGPU_EHIP;
     }
@@ -466,11 +514,17 @@ int pnetgpu_checksum_slices_strided(pnetgpu_ctx* ctx, const uint8_t* data, uint6
     // computes it), slice_run_kernel's runs, slice_kernel's 4 slices
     const uint64_t slices_per_unit =
         small ? 64u * (stride ? std::max(1u, std::min(16u, 4096u / (64u * stride))) : 16u) : run ? 64u : 4u;
-    if ((rc = plan_sched(ctx, (n + slices_per_unit - 1) / slices_per_unit, (uint64_t)blocks * 4, stream, &a.sched)))
+    int blk;
+    uint32_t prev;
+    if ((rc = plan_sched(ctx, (n + slices_per_unit - 1) / slices_per_unit, (uint64_t)blocks * 4, stream, &a.sched,
+                         &blk, &prev)))
         return rc;
     const int e = small ? pnetgpu::launch_slices_strided_small(a, blocks, static_cast<hipStream_t>(stream))
                         : pnetgpu::launch_slices(a, 0, run, blocks, static_cast<hipStream_t>(stream));
-    if (e) return pnetgpu::hip_fail((hipError_t)e);
+    if (e) {
+        sched_undo(ctx, blk, prev);
+        return pnetgpu::hip_fail((hipError_t)e);
+    }
     return PNETGPU_OK;
 }
 
@@ -493,8 +547,15 @@ int pnetgpu_checksum_slices_compact(pnetgpu_ctx* ctx, const uint8_t* data, uint6
     const bool run = slice_run_choice(ctx, data_bytes, n);
     const uint64_t per_block = run ? kBlock : kBlock / 16;
     const int blocks = slice_grid(ctx, run ? 1 : 2, 0, false, (n + per_block - 1) / per_block);
-    if ((rc = plan_sched(ctx, run ? (n + 63) / 64 : (n + 3) / 4, (uint64_t)blocks * 4, stream, &a.sched))) return rc;
-    if (const int e = pnetgpu::launch_slices(a, 0, run, blocks, static_cast<hipStream_t>(stream))) return pnetgpu::hip_fail((hipError_t)e);
+    int blk;
+    uint32_t prev;
+    if ((rc = plan_sched(ctx, run ? (n + 63) / 64 : (n + 3) / 4, (uint64_t)blocks * 4, stream, &a.sched, &blk,
+                         &prev)))
+        return rc;
+    if (const int e = pnetgpu::launch_slices(a, 0, run, blocks, static_cast<hipStream_t>(stream))) {
+        sched_undo(ctx, blk, prev);
+        return pnetgpu::hip_fail((hipError_t)e);
+    }
     return PNETGPU_OK;
 }
 

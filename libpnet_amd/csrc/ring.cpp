@@ -18,7 +18,10 @@
 
 namespace {
 
-constexpr int kSlots = 3;          // filling, in flight, held by the application
+// slots per ring: one filling, one held by the application, the rest in flight
+// (each on its own stream, so H2D of batch k+1 overlaps the kernel and D2H of k)
+constexpr int kDefaultSlots = PNETGPU_RING_DEFAULT_SLOTS;
+constexpr int kMaxSlots = PNETGPU_RING_MAX_SLOTS;
 constexpr int kNumCols = 38;       // the 16 record columns, then the 22 header-field columns (ABI v3)
 constexpr uint64_t kDefaultCols = 0xFFFFull;
 // element bytes of each pnetgpu_rx_columns column, in struct order (counters skipped)
@@ -81,7 +84,8 @@ struct pnetgpu_ring {
     uint32_t cap_frames = 0;
     uint32_t flags = 0;
     uint64_t col_mask = kDefaultCols;           // columns computed and copied back (bit k: struct order)
-    Slot slots[kSlots];
+    Slot slots[kMaxSlots];
+    int nslots = kDefaultSlots;
     int filling = -1;
     int held = -1;
     std::deque<int> inflight;
@@ -139,7 +143,7 @@ static bool alloc_rec(Slot& s, size_t bytes) {
 }
 
 static int take_free_slot(pnetgpu_ring* r) {
-    for (int i = 0; i < kSlots; ++i) {
+    for (int i = 0; i < r->nslots; ++i) {
         if (r->slots[i].state == kFree) {
             r->slots[i].state = kFilling;
             r->slots[i].n = 0;
@@ -153,10 +157,11 @@ static int take_free_slot(pnetgpu_ring* r) {
 
 extern "C" {
 
-int pnetgpu_ring_create(pnetgpu_ctx* ctx, uint64_t batch_bytes, uint32_t batch_frames, uint32_t flags,
-                        pnetgpu_ring** out) {
+int pnetgpu_ring_create_ex(pnetgpu_ctx* ctx, uint64_t batch_bytes, uint32_t batch_frames, uint32_t flags,
+                           uint32_t nslots, pnetgpu_ring** out) {
     pnetgpu::set_last_hip_error(0);
     if (!ctx || !out || batch_bytes == 0 || batch_frames == 0) return PNETGPU_EINVAL;
+    if (nslots < PNETGPU_RING_MIN_SLOTS || nslots > (uint32_t)kMaxSlots) return PNETGPU_EINVAL;
     if (flags & ~(PNETGPU_RX_VLAN | PNETGPU_RX_IPV6_EXT | PNETGPU_RX_L3)) return PNETGPU_EINVAL;
     *out = nullptr;
     auto* r = new (std::nothrow) pnetgpu_ring;
@@ -166,12 +171,13 @@ int pnetgpu_ring_create(pnetgpu_ctx* ctx, uint64_t batch_bytes, uint32_t batch_f
     r->cap_bytes = batch_bytes;
     r->cap_frames = batch_frames;
     r->flags = flags;
+    r->nslots = (int)nslots;
     if (hipSetDevice(r->device) != hipSuccess) {
         delete r;
         return pnetgpu::hip_fail(hipGetLastError());
     }
     bool ok = true;
-    for (int i = 0; i < kSlots && ok; ++i) {
+    for (int i = 0; i < r->nslots && ok; ++i) {
         Slot& s = r->slots[i];
         const size_t fb = batch_bytes + 32;    // granule tail
         ok = hipHostMalloc((void**)&s.h_frames, fb, hipHostMallocDefault) == hipSuccess &&
@@ -196,6 +202,13 @@ int pnetgpu_ring_create(pnetgpu_ctx* ctx, uint64_t batch_bytes, uint32_t batch_f
     *out = r;
     return PNETGPU_OK;
 }
+
+int pnetgpu_ring_create(pnetgpu_ctx* ctx, uint64_t batch_bytes, uint32_t batch_frames, uint32_t flags,
+                        pnetgpu_ring** out) {
+    return pnetgpu_ring_create_ex(ctx, batch_bytes, batch_frames, flags, kDefaultSlots, out);
+}
+
+uint32_t pnetgpu_ring_slots(const pnetgpu_ring* r) { return r ? (uint32_t)r->nslots : 0u; }
 
 void pnetgpu_ring_destroy(pnetgpu_ring* r) {
     if (!r) return;
@@ -427,14 +440,24 @@ int pnetgpu_ring_submit_region(pnetgpu_ring* r, const uint8_t* base, const uint6
     *taken = k;
     return ship_slot(r, s, base + o0, id);
 }
-int pnetgpu_ring_wait(pnetgpu_ring* r, pnetgpu_ring_batch* out) {
-    pnetgpu::set_last_hip_error(0);
-    if (!r || !out) return PNETGPU_EINVAL;
-    if (r->held >= 0) {                          // the previous batch is released now
+static void release_held(pnetgpu_ring* r) {
+    if (r->held >= 0) {
         r->slots[r->held].state = kFree;
         r->held = -1;
         if (r->filling < 0) r->filling = take_free_slot(r);
     }
+}
+
+int pnetgpu_ring_release(pnetgpu_ring* r) {
+    if (!r) return PNETGPU_EINVAL;
+    release_held(r);
+    return PNETGPU_OK;
+}
+
+int pnetgpu_ring_wait(pnetgpu_ring* r, pnetgpu_ring_batch* out) {
+    pnetgpu::set_last_hip_error(0);
+    if (!r || !out) return PNETGPU_EINVAL;
+    release_held(r);                             // the previous batch is released now
     if (r->inflight.empty()) return PNETGPU_EEMPTY;
     const int i = r->inflight.front();
     r->inflight.pop_front();
@@ -459,13 +482,15 @@ int pnetgpu_ring_set_columns(pnetgpu_ring* r, uint64_t column_mask) {
     if (!r || (column_mask >> kNumCols)) return PNETGPU_EINVAL;
     const size_t need = rec_capacity(r->cap_frames, column_mask);
     bool grow = false;
-    for (const Slot& s : r->slots) grow = grow || s.rec_cap < need;
+    Slot* const s0 = r->slots;
+    Slot* const s1 = r->slots + r->nslots;
+    for (const Slot* s = s0; s != s1; ++s) grow = grow || s->rec_cap < need;
     if (grow) {   // record blocks are resized only while no batch uses them
-        for (const Slot& s : r->slots)
-            if (s.state == kInFlight || s.state == kHeld) return PNETGPU_EBUSY;
+        for (const Slot* s = s0; s != s1; ++s)
+            if (s->state == kInFlight || s->state == kHeld) return PNETGPU_EBUSY;
         if (hipSetDevice(r->device) != hipSuccess) return pnetgpu::hip_fail(hipGetLastError());
-        for (Slot& s : r->slots)
-            if (s.rec_cap < need && !alloc_rec(s, need)) return PNETGPU_ENOMEM;
+        for (Slot* s = s0; s != s1; ++s)
+            if (s->rec_cap < need && !alloc_rec(*s, need)) return PNETGPU_ENOMEM;
     }
     r->col_mask = column_mask;
     return PNETGPU_OK;

@@ -124,41 +124,39 @@ __device__ __forceinline__ void rotate_prio(uint32_t step) {
 // one claim kept in flight ahead of its use so the atomic's round trip
 // overlaps a whole run: claim() issues the atomic, and its value is read
 // (and waited for) only at the next take(). take() returns the next run;
-// >= nruns ends the loop.
+// >= nruns ends the loop, and then the wave reports its finish (finish()):
+// the counters are left zero for the block's next launch.
 struct RunQueue {
     uint64_t next_static, stride, nstatic, nruns, lo, hi;
     unsigned long long* ctr;
-    unsigned long long* conflicts;
     uint64_t pend;          // claimed ahead (dynamic phase), nruns when none is pending
-    uint32_t epoch;
-    uint32_t kraw, kepoch;  // lane 0: the in-flight claim's count and epoch
-    bool stamped, inflight;
+    uint32_t kraw;          // lane 0: the in-flight claim's count
+    uint32_t gwaves;        // waves whose home is this wave's counter
+    bool inflight, finished;
+    unsigned long long* groups_done;
+    uint32_t* done_host;
+    uint32_t seq, nctr;
 
     __device__ RunQueue(const RunSched& s, uint64_t n_units, uint64_t wave_id, uint64_t wave_stride)
         : next_static(wave_id), stride(wave_stride), nstatic(s.ctr ? s.nstatic : n_units), nruns(n_units), lo(0),
-          hi(0), ctr(s.ctr), conflicts(s.conflicts), pend(n_units), epoch(s.epoch), kraw(0), kepoch(0),
-          stamped(false), inflight(false) {
+          hi(0), ctr(s.ctr), pend(n_units), kraw(0), gwaves(0), inflight(false), finished(false),
+          groups_done(s.groups_done), done_host(s.done_host), seq(s.seq), nctr(s.nctr) {
         if (ctr) {
             const uint64_t h = (wave_id >> 5) % s.nctr, d = nruns - nstatic;
             lo = nstatic + d * h / s.nctr;
             hi = nstatic + d * (h + 1) / s.nctr;
             ctr += h * s.ctr_stride;
+            // the group's size: 32-wave chunks c < ceil(W / 32) with c % nctr == h,
+            // the last chunk holding W % 32 waves when W is not a multiple of 32
+            const uint64_t nch = (wave_stride + 31) / 32, full = wave_stride / 32, rem = wave_stride % 32;
+            uint64_t g = h < nch ? ((nch - 1 - h) / s.nctr + 1) * 32 : 0;
+            if (rem && full % s.nctr == h) g -= 32 - rem;
+            gwaves = (uint32_t)g;
             if (next_static >= nstatic) claim();   // no static share: the first claim now
         }
     }
     __device__ void claim() {
-        if (__lane_id() == 0) {
-            if (!stamped) {
-                // the slot may hold an earlier launch's count: lift it to this
-                // epoch with a zero count (a no-op once any wave has done so)
-                (void)atomicMax(ctr, (unsigned long long)epoch << 32);
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            }
-            const unsigned long long old = atomicAdd(ctr, 1ull);
-            kraw = (uint32_t)old;
-            kepoch = (uint32_t)(old >> 32);
-        }
-        stamped = true;
+        if (__lane_id() == 0) kraw = (uint32_t)atomicAdd(ctr, 1ull);
         inflight = true;
 #ifdef PNET_CLAIM_EAGER   // A/B: the round-3 claim, waited for where it is made
         resolve();
@@ -168,11 +166,27 @@ struct RunQueue {
     __device__ void resolve() {
         if (!inflight) return;
         inflight = false;
-        // another launch stamped this stream's slot while this one runs:
-        // claims may be shared, so the host hears of it (never silent)
-        if (__lane_id() == 0 && kepoch != epoch && conflicts) atomicAdd(conflicts, 1ull);
         const uint64_t r = lo + (uint64_t)__builtin_amdgcn_readfirstlane(kraw);
         pend = r < hi ? r : nruns;
+    }
+    // The wave is done with the counters (no claim in flight: its last one came
+    // back past its counter's slice). The group's last wave zeroes the counter;
+    // the last group's zeroes groups_done and, after a system-scope fence, hands
+    // the block back to the host.
+    __device__ void finish() {
+        if (!ctr || finished) return;
+        finished = true;
+        if (__lane_id() == 0) {
+            const unsigned long long old = atomicAdd(ctr, 1ull << 32);
+            if ((uint32_t)(old >> 32) + 1 == gwaves) {
+                (void)atomicExch(ctr, 0ull);
+                if (atomicAdd(groups_done, 1ull) + 1 == nctr) {
+                    (void)atomicExch(groups_done, 0ull);
+                    __threadfence_system();
+                    __hip_atomic_store(done_host, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+                }
+            }
+        }
     }
     __device__ uint64_t take() {
         if (next_static < nstatic) {
@@ -184,6 +198,7 @@ struct RunQueue {
         resolve();
         const uint64_t r = pend;
         if (r < nruns) claim();
+        else finish();
         return r;
     }
 };

@@ -10,17 +10,20 @@ namespace pnetgpu {
 // Run scheduling of a persistent-grid launch (RunQueue in rx_common.h): units
 // (runs, or slice blocks) [0, nstatic) go to the waves in grid-stride order
 // (nstatic is a multiple of the wave count); units [nstatic, n) are claimed one
-// at a time from nctr counters, ctr_stride u64 apart from ctr (high 32 bits of
-// a counter: the launch epoch, stamped by atomicMax; low 32 bits: claims), so
-// waves whose share ran slow do not set the kernel's end. ctr == nullptr: all
-// units static. The counters belong to the launch's stream (abi.cpp
-// plan_sched): a claim that returns another epoch means a concurrent launch
-// took the slot, and is counted at `conflicts`.
+// at a time from nctr counters, ctr_stride u64 apart from ctr, so waves whose
+// share ran slow do not set the kernel's end. ctr == nullptr: all units static.
+// The counters are one block of the context's pool (abi.cpp plan_sched), owned
+// by this launch alone: zero when it starts (low 32 bits of a counter: claims;
+// high 32 bits: the waves of its group that have finished). The last wave of
+// each group zeroes its counter, the last group zeroes groups_done and writes
+// `seq` to the pinned host word done_host, which frees the block for another
+// launch (the host reuses a block only once its word shows the seq it issued).
 struct RunSched {
     unsigned long long* ctr;
-    unsigned long long* conflicts;
+    unsigned long long* groups_done;
+    uint32_t* done_host;
     uint64_t nstatic;
-    uint32_t epoch;
+    uint32_t seq;
     uint32_t nctr;
     uint32_t ctr_stride;
 };

@@ -169,6 +169,16 @@ Built build(int workload, uint64_t seed, uint64_t i, uint32_t corrupt_ppm, uint8
             l4off = 34; l4hdr = 20; l4end = len;
             break;
         }
+        case PNETGPU_SYNTH_UDP1500: {
+            // rs_sender.rs:54-72's frame at full MTU: Eth 14 | IPv4 20 (total_length
+            // 1486) | UDP 8 (length 1466) | 1458 random data bytes, no padding
+            eth_header(f, r, 0x0800, false);
+            ipv4_header(f + 14, r, 17, (uint16_t)(len - 14), false);
+            const uint32_t n = len - 34;
+            udp_seg(f + 34, n, n - 8, r, pseudo_v4(f + 14, 17, n), false);
+            l4off = 34; l4hdr = 8; l4end = len;
+            break;
+        }
         case PNETGPU_SYNTH_IMIX: {
             eth_header(f, r, 0x0800, false);
             const uint32_t k = (uint32_t)(r.next() % 3);
@@ -217,7 +227,8 @@ bool layout(int workload, uint64_t first, uint64_t n, uint64_t seed, uint64_t* t
     switch (workload) {
         case PNETGPU_SYNTH_RS_SENDER:
         case PNETGPU_SYNTH_UDP64: *stride = 64; break;
-        case PNETGPU_SYNTH_TCP1500: *stride = 1500; break;
+        case PNETGPU_SYNTH_TCP1500:
+        case PNETGPU_SYNTH_UDP1500: *stride = 1500; break;
         case PNETGPU_SYNTH_UDP6_JUMBO: *stride = 9000; break;
         case PNETGPU_SYNTH_IMIX: *stride = 0; break;
         default: return false;

@@ -134,11 +134,19 @@ class Context:
                 self.set_tuning(k, v)
 
     def sched_conflicts(self):
-        """Claims that found this context's stream slot taken by a concurrent
-        launch (pnetgpu_ctx_sched_conflicts; synchronises the device)."""
+        """pnetgpu_ctx_sched_conflicts: always 0 (launches never share claim counters)."""
         v = ctypes.c_uint64()
         check(lib.pnetgpu_ctx_sched_conflicts(self.handle, ctypes.byref(v)), "pnetgpu_ctx_sched_conflicts")
         return v.value
+
+    def sched_stats(self):
+        """pnetgpu_ctx_sched_stats: {"claimed", "static_busy", "static_captured",
+        "blocks_held", "blocks"} — launches that took a counter block, ran static
+        because every block was held, or were captured into a graph; blocks
+        held now and the pool size."""
+        v = (ctypes.c_uint64 * DEFS["PNETGPU_NSCHED_STATS"])()
+        check(lib.pnetgpu_ctx_sched_stats(self.handle, v), "pnetgpu_ctx_sched_stats")
+        return dict(zip(("claimed", "static_busy", "static_captured", "blocks_held", "blocks"), (int(x) for x in v)))
 
     def close(self):
         if getattr(self, "handle", None):
@@ -386,10 +394,14 @@ def checksum_slices_compact(data, desc, stream=None):
     _check_u8_cuda(data, "data")
     if not isinstance(desc, torch.Tensor) or desc.dtype not in _I64:
         raise TypeError("desc must be an int64 / uint64 tensor of packed pnetgpu_slice_desc records")
-    if not desc.is_cuda or desc.device != data.device or not desc.is_contiguous():
-        desc = desc.to(data.device).contiguous()
-    n = desc.numel()
-    out = torch.empty(n, dtype=torch.int16, device=data.device)
+    copied = not desc.is_cuda or desc.device != data.device or not desc.is_contiguous()
+    with torch.cuda.stream(stream) if stream is not None else _nullcontext():
+        # the copy (and the output) on the launch's stream: ordered before the
+        # kernel, and the allocator's stream for the temporary is the one that reads it
+        if copied:
+            desc = desc.to(data.device).contiguous()
+        n = desc.numel()
+        out = torch.empty(n, dtype=torch.int16, device=data.device)
     ctx = context(data.device.index)
     check(lib.pnetgpu_checksum_slices_compact(ctx.handle, _ptr(data), data.numel(), n, _ptr(desc), _ptr(out),
                                               _stream_handle(stream, data.device)), "pnetgpu_checksum_slices_compact")

@@ -25,6 +25,12 @@ def _setup():
     vp, u64, u32, i32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int
     lib.pnetgpu_ring_create.restype = i32
     lib.pnetgpu_ring_create.argtypes = [vp, u64, u32, u32, ctypes.POINTER(vp)]
+    lib.pnetgpu_ring_create_ex.restype = i32
+    lib.pnetgpu_ring_create_ex.argtypes = [vp, u64, u32, u32, u32, ctypes.POINTER(vp)]
+    lib.pnetgpu_ring_slots.restype = u32
+    lib.pnetgpu_ring_slots.argtypes = [vp]
+    lib.pnetgpu_ring_release.restype = i32
+    lib.pnetgpu_ring_release.argtypes = [vp]
     lib.pnetgpu_ring_destroy.restype = None
     lib.pnetgpu_ring_destroy.argtypes = [vp]
     lib.pnetgpu_ring_push.restype = i32
@@ -60,7 +66,9 @@ _setup()
 
 class Batch:
     """A finished ring batch. With copy=False the arrays are views of the ring's
-    pinned memory, valid until the ring's next wait (the C-ABI contract)."""
+    pinned memory, valid until the ring's next wait or release (the C-ABI
+    contract): the generators below release a batch when they resume after
+    yielding it, so views must not outlive the consumer's loop iteration."""
 
     def __init__(self, rb, copy=True):
         n = int(rb.n_frames)
@@ -87,16 +95,21 @@ class Batch:
 
 
 class Ring:
-    """Pinned host batches -> asynchronous GPU verification (three rotating slots)."""
+    """Pinned host batches -> asynchronous GPU verification (rotating slots: one
+    filling, one held by the consumer, the rest in flight)."""
 
-    def __init__(self, batch_bytes=64 << 20, batch_frames=1 << 18, device=0, copy=True, flags=0, columns=None):
-        """columns: names of the record columns to compute and copy back (default all)."""
+    def __init__(self, batch_bytes=64 << 20, batch_frames=1 << 18, device=0, copy=True, flags=0, columns=None,
+                 slots=None):
+        """columns: names of the record columns to compute and copy back (default all);
+        slots: slot count (default PNETGPU_RING_DEFAULT_SLOTS)."""
         self.ctx = context(device)
         self.copy = copy
         h = ctypes.c_void_p()
-        check(lib.pnetgpu_ring_create(self.ctx.handle, batch_bytes, batch_frames, flags, ctypes.byref(h)),
-              "pnetgpu_ring_create")
+        slots = DEFS["PNETGPU_RING_DEFAULT_SLOTS"] if slots is None else slots
+        check(lib.pnetgpu_ring_create_ex(self.ctx.handle, batch_bytes, batch_frames, flags, slots, ctypes.byref(h)),
+              "pnetgpu_ring_create_ex")
         self.h = h
+        self.slots = int(lib.pnetgpu_ring_slots(h))
         self.pending = 0
         if columns is not None:
             mask = 0
@@ -124,6 +137,15 @@ class Ring:
         self.pending -= 1
         return Batch(rb, self.copy)
 
+    def release(self):
+        """Release the batch the last wait returned (pnetgpu_ring_release)."""
+        check(lib.pnetgpu_ring_release(self.h), "pnetgpu_ring_release")
+
+    def wait(self):
+        """The oldest submitted batch (blocking), or None when nothing is in flight.
+        It stays held (copy=False views valid) until the next wait or release."""
+        return self._wait()
+
     def submit(self):
         bid = ctypes.c_uint64()
         check(lib.pnetgpu_ring_submit(self.h, ctypes.byref(bid)), "pnetgpu_ring_submit")
@@ -144,6 +166,7 @@ class Ring:
                 b = self._wait()
                 if b is not None:
                     yield b
+                    self.release()             # the consumer is done with it: refill its slot now
                 continue
             check(rc, "pnetgpu_ring_push")
 
@@ -170,6 +193,7 @@ class Ring:
                 b = self._wait()
                 if b is not None:
                     yield b
+                    self.release()             # the consumer is done with it: refill its slot now
                 continue
             check(rc, "pnetgpu_ring_push_many")
 
@@ -196,6 +220,7 @@ class Ring:
                 b = self._wait()
                 if b is not None:
                     yield b
+                    self.release()             # the consumer is done with it: refill its slot now
                 continue
             if rc == EFULL:                      # frames pushed earlier are still filling: ship them
                 before = self.pending
@@ -213,6 +238,7 @@ class Ring:
             if b is None:
                 return
             yield b
+            self.release()
 
 
 class HostRegistration:

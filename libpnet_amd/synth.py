@@ -10,6 +10,7 @@ WORKLOADS = {
     "rs_sender": DEFS["PNETGPU_SYNTH_RS_SENDER"],
     "udp64": DEFS["PNETGPU_SYNTH_UDP64"],
     "tcp1500": DEFS["PNETGPU_SYNTH_TCP1500"],
+    "udp1500": DEFS["PNETGPU_SYNTH_UDP1500"],
     "imix": DEFS["PNETGPU_SYNTH_IMIX"],
     "udp6_jumbo": DEFS["PNETGPU_SYNTH_UDP6_JUMBO"],
 }

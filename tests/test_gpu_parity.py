@@ -325,7 +325,7 @@ def test_stride_mode_random_frames_every_kernel(stride, flen, tune):
 
 # ---- BASELINE workloads at full per-GPU size -------------------------------
 
-FULL = {"udp64": 1 << 24, "tcp1500": 1 << 20, "imix": 1 << 22, "udp6_jumbo": 1 << 17}
+FULL = {"udp64": 1 << 24, "tcp1500": 1 << 20, "udp1500": 1 << 20, "imix": 1 << 22, "udp6_jumbo": 1 << 17}
 
 
 @pytest.mark.parametrize("name", list(FULL))

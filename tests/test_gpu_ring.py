@@ -1,10 +1,12 @@
 """GPU end-to-end of the batch producer: frames pushed one by one (or from a pcap
 replay) through the pinned ring come back with records identical to the oracle's."""
+import ctypes
+
 import numpy as np
 import pytest
 
 import libpnet_amd as lp
-from libpnet_amd._lib import PnetGpuError
+from libpnet_amd._lib import PnetGpuError, check, lib
 from oracle import coracle
 from tests import framegen
 from tests.pcaputil import write_pcap
@@ -134,3 +136,66 @@ def test_ring_column_subset():
     out = list(ring.feed_region(w.buf, offs, lens)) + list(ring.drain())
     assert all(set(b.records) == set(lp.IPV4_COLUMNS) for b in out)
     check_batches(out, frames)
+
+
+def _oracle_check(b, ident):
+    rec = coracle.rx_batch(np.asarray(b.frames), b.n, offsets=b.offsets, lengths=b.lengths)
+    assert b.records, ident
+    for c, v in b.records.items():
+        assert np.array_equal(v, rec[c]), (ident, c)
+
+
+@pytest.mark.parametrize("slots", [4, 6])
+def test_ring_holds_a_batch_while_others_complete(slots):
+    """With the consumer holding one batch (copy=False views of pinned memory),
+    the other slots keep shipping: `slots - 2` more batches are submitted and
+    finish on the GPU while it is held, the held batch's frames and records are
+    untouched by them, and every batch equals the oracle."""
+    import torch
+    w = lp.synth.make("imix", 40000, seed=21, corrupt_ppm=20000)
+    ring = lp.Ring(batch_bytes=2 << 20, batch_frames=4000, copy=False, slots=slots)
+    assert ring.slots == slots
+    per = 3000
+    ranges = [(k * per, (k + 1) * per) for k in range(slots)]
+    offs, lens = w.offsets, w.lengths
+
+    def push(lo, hi):
+        pushed = ctypes.c_uint64()
+        check(lib.pnetgpu_ring_push_many(ring.h, ctypes.c_void_p(w.buf.ctypes.data),
+                                       ctypes.c_void_p(offs[lo:].ctypes.data),
+                                       ctypes.c_void_p(lens[lo:].ctypes.data), hi - lo,
+                                       ctypes.byref(pushed)), "push_many")
+        assert pushed.value == hi - lo
+        ring.submit()
+
+    push(*ranges[0])
+    held = ring.wait()                      # batch 0 held from here on
+    assert held.id == 0 and held.n == per
+    snap = {c: v.copy() for c, v in held.records.items()}
+    frames0 = np.asarray(held.frames).copy()
+    for lo, hi in ranges[1:slots - 1]:      # every other slot but the filling one: in flight
+        push(lo, hi)
+    torch.cuda.synchronize()
+    # the slots are all taken: one held, slots - 2 in flight, one filling
+    for c, v in held.records.items():
+        assert np.array_equal(v, snap[c]), c
+    assert np.array_equal(np.asarray(held.frames), frames0)
+    _oracle_check(held, 0)
+    got = []
+    while True:
+        b = ring.wait()                     # releases the previous batch
+        if b is None:
+            break
+        _oracle_check(b, b.id)
+        got.append((b.id, b.n))
+    assert got == [(k, per) for k in range(1, slots - 1)]
+    ring.close()
+
+
+def test_ring_slot_count_bounds():
+    for bad in (0, 1, lp.DEFS["PNETGPU_RING_MAX_SLOTS"] + 1):
+        with pytest.raises(PnetGpuError):
+            lp.Ring(batch_bytes=1 << 16, batch_frames=64, slots=bad)
+    r = lp.Ring(batch_bytes=1 << 16, batch_frames=64)
+    assert r.slots == lp.DEFS["PNETGPU_RING_DEFAULT_SLOTS"] >= 4
+    r.close()

@@ -1,13 +1,19 @@
 """GPU: the receive kernels' run scheduling (RxArgs::sched).
 
 A launch hands each persistent wave a static grid-stride share of the batch's
-runs and lets the waves claim the rest from per-launch counters. These tests
-check that every run is processed exactly once whatever the static share and
-the counter count, across ragged batch ends, every kernel kind that claims
-(small, MTU, mixed), counter-slot reuse over many launches (epochs), the
-epoch wrap, and launches of one context interleaved on three streams. Results are compared with
-the oracle (bit-exact) and the per-launch counters with the oracle's counts.
+runs and lets the waves claim the rest from counters: one block of the
+context's pool, held by that launch alone and handed back zeroed by its last
+wave. These tests check that every run is processed exactly once whatever the
+static share and the counter count, across ragged batch ends, every kernel kind
+that claims (small, MTU, mixed), block reuse over many launches, launches of
+one context interleaved on several streams, a destroyed stream handle reused
+with work in flight, more launches in flight than the pool has blocks (static
+fallback), and launches captured into a HIP graph and replayed. Results are
+compared with the oracle (bit-exact) and the per-launch counters with the
+oracle's counts; after every test all blocks are back in the pool.
 """
+import ctypes
+
 import numpy as np
 import pytest
 import torch
@@ -45,6 +51,22 @@ class _Dev:
         return lp.rx_process(self.d, offsets=self.offs, lengths=self.lens, columns=cols, stream=stream)
 
 
+def _stats():
+    return lp.engine.context(0).sched_stats()
+
+
+def _delta(a, b):
+    return {k: b[k] - a[k] for k in ("claimed", "static_busy", "static_captured")}
+
+
+def _hip():
+    # the HIP runtime already in the process (PyTorch's, which libpnetgpu.so binds to)
+    hip = ctypes.CDLL("libamdhip64.so.7")
+    hip.hipStreamCreate.argtypes = [ctypes.POINTER(ctypes.c_void_p)]
+    hip.hipStreamDestroy.argtypes = [ctypes.c_void_p]
+    return hip
+
+
 def _oracle(w, n):
     if w.stride:
         rec = coracle.rx_batch(w.buf, n, stride=w.stride, frame_len=w.frame_len, nthreads=NTHREADS)
@@ -70,9 +92,10 @@ def test_every_run_once_any_static_share(name, tune):
         assert res.counter_dict() == want, (pct, nctr)
 
 
-def test_counter_slot_reused_across_many_launches(tune):
-    """Many launches on one stream: each stamps the stream's counter slot with
-    the next epoch and must start from zero claims."""
+def test_counter_blocks_reused_across_many_launches(tune):
+    """150 launches on one stream with no host synchronization: each takes a
+    free block of the pool (or runs static once all 64 are held), must start
+    from zero claims, and hands its block back at the end."""
     n = SIZES["udp64"]
     w = lp.synth.make("udp64", n, seed=12, corrupt_ppm=10000)
     rec, lens = _oracle(w, n)
@@ -80,36 +103,113 @@ def test_counter_slot_reused_across_many_launches(tune):
     dv = _Dev(w)
     tune("static_pct", 90)
     tune("claim_counters", 16)
+    s0 = _stats()
     results = [dv.run(n) for _ in range(150)]
     torch.cuda.synchronize()
+    d = _delta(s0, _stats())
+    assert d["claimed"] + d["static_busy"] == 150 and d["claimed"] >= 64, d
     for i in (0, 63, 64, 65, 127, 128, 149):
         compare(results[i], rec)
     for r in results:
         assert r.counter_dict() == want
     assert lp.engine.context(0).sched_conflicts() == 0
+    assert _stats()["blocks_held"] == 0
 
 
-def test_epoch_wrap_rezeroes_the_slot_in_stream_order(tune):
-    """A stream slot whose launch epoch reaches the wrap threshold is re-zeroed
-    with an async memset on the launch's own stream (no device-wide sync):
-    launches across the wrap, with no host synchronization between them,
-    every one bit-exact, and no claim ever sees a foreign epoch."""
+def test_more_launches_in_flight_than_blocks(tune):
+    """Four streams held behind a spin kernel: the first 64 launches take the
+    pool's 64 blocks, the other 36 find every block held and run the static
+    schedule. Every record equals the oracle's, and once the launches are done
+    every block is back."""
+    n = 8 * 1024 * 64                         # 8 runs x 256 CUs x 4 waves x 64 frames
+    w = lp.synth.make("udp64", n, seed=17, corrupt_ppm=10000)
+    rec, lens = _oracle(w, n)
+    want = oracle_counters(rec, lens)
+    dv = _Dev(w)
+    tune("blocks_per_cu", 1)
+    tune("static_pct", 25)
+    streams = [torch.cuda.Stream() for _ in range(4)]
+    gate_s, gate = torch.cuda.Stream(), torch.cuda.Event()
+    with torch.cuda.stream(gate_s):
+        torch.cuda._sleep(int(3e8))           # holds the launches until all 100 are enqueued
+    gate.record(gate_s)
+    for s in streams:
+        s.wait_event(gate)
+    s0 = _stats()
+    assert s0["blocks_held"] == 0 and s0["blocks"] == 64
+    results = [dv.run(n, stream=streams[i % 4], cols=("status", "l4_csum")) for i in range(100)]
+    d = _delta(s0, _stats())
+    torch.cuda.synchronize()
+    assert d == {"claimed": 64, "static_busy": 36, "static_captured": 0}, d
+    compare(results[0], rec)
+    for i, r in enumerate(results):
+        for c, col in r.columns.items():
+            assert torch.equal(col, results[0].columns[c]), (i, c)
+        assert r.counter_dict() == want, i
+    assert _stats()["blocks_held"] == 0
+
+
+def test_destroyed_stream_handle_reused_with_work_in_flight(tune):
+    """Launches on a raw HIP stream, which is destroyed with them in flight;
+    a new stream (often at the same handle) takes more launches at once. No
+    launch shares counters with another, so every record is exact and rc 0
+    means right."""
     n = SIZES["udp64"]
-    w = lp.synth.make("udp64", n, seed=14, corrupt_ppm=10000)
+    w = lp.synth.make("udp64", n, seed=18, corrupt_ppm=10000)
     rec, lens = _oracle(w, n)
     want = oracle_counters(rec, lens)
     dv = _Dev(w)
     tune("static_pct", 50)
-    s = torch.cuda.Stream()
-    dv.run(n, stream=s)                       # the stream owns a slot from here on
-    tune("sched_epoch", 0xFFFFFF00 - 4)       # its next epochs: ...FC, FD, FE, FF, then wrap to 1
-    results = [dv.run(n, stream=s) for _ in range(10)]
+    hip = _hip()
+    h1, h2 = ctypes.c_void_p(), ctypes.c_void_p()
+    assert hip.hipStreamCreate(ctypes.byref(h1)) == 0
+    s1 = torch.cuda.ExternalStream(h1.value)
+    s0 = _stats()
+    first = [dv.run(n, stream=s1) for _ in range(6)]
+    assert hip.hipStreamDestroy(h1) == 0
+    assert hip.hipStreamCreate(ctypes.byref(h2)) == 0
+    s2 = torch.cuda.ExternalStream(h2.value)
+    second = [dv.run(n, stream=s2) for _ in range(6)]
     torch.cuda.synchronize()
-    for r in results:
+    assert hip.hipStreamDestroy(h2) == 0
+    assert _delta(s0, _stats())["claimed"] == 12
+    for r in (first[0], first[-1], second[0], second[-1]):
+        compare(r, rec)
+    for r in first + second:
         assert r.counter_dict() == want
-    compare(results[4], rec)
-    compare(results[-1], rec)
-    assert lp.engine.context(0).sched_conflicts() == 0
+    assert _stats()["blocks_held"] == 0
+
+
+def test_graph_capture_replays(tune):
+    """A launch captured into a HIP graph runs the static schedule (a replay
+    cannot take a fresh block): replayed three times, each replay's records and
+    counters equal the oracle's; the uncaptured launch beside it claims."""
+    n = SIZES["imix"]
+    w = lp.synth.make("imix", n, seed=19, corrupt_ppm=10000)
+    rec, lens = _oracle(w, n)
+    want = oracle_counters(rec, lens)
+    dv = _Dev(w)
+    tune("static_pct", 50)
+    res = lp.RxResult(n, "cuda:0", lp.IPV4_COLUMNS, counters=True)
+    lp.rx_process(dv.d, offsets=dv.offs, lengths=dv.lens, out=res)   # first use outside the capture
+    torch.cuda.synchronize()
+    s0 = _stats()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        res.counters.zero_()
+        lp.rx_process(dv.d, offsets=dv.offs, lengths=dv.lens, out=res)
+    assert _delta(s0, _stats())["static_captured"] == 1
+    for rep in range(3):
+        res.block.fill_(0x5A)
+        g.replay()
+        torch.cuda.synchronize()
+        compare(res, rec)
+        assert res.counter_dict() == want, rep
+    other = dv.run(n)
+    torch.cuda.synchronize()
+    compare(other, rec)
+    assert _delta(s0, _stats())["claimed"] == 1
+    assert _stats()["blocks_held"] == 0
 
 
 def test_three_streams_no_host_sync(tune):
@@ -136,6 +236,7 @@ def test_three_streams_no_host_sync(tune):
             assert torch.equal(col, results[0].columns[c]), (i, c)
         assert r.counter_dict() == want, i
     assert lp.engine.context(0).sched_conflicts() == 0
+    assert _stats()["blocks_held"] == 0
 
 
 @pytest.mark.parametrize("pct,nctr", [(0, 64), (50, 7), (92, 1)])
@@ -185,13 +286,14 @@ def test_slice_kernels_claim_path(pct, nctr, tune):
     so = 3 + 20 * np.arange(ns, dtype=np.uint64)
     swant = coracle.checksum_slices(sbuf, so, np.full(ns, 20, np.uint32), np.full(ns, 5, np.uint32))
     assert np.array_equal(got, swant)
+    torch.cuda.synchronize()
+    assert _stats()["blocks_held"] == 0
 
 
-def test_more_streams_than_slots(tune):
-    """A context gives its first 64 distinct streams a counter slot each; a
-    launch on any further stream runs the static schedule. 70 streams, two
-    launches each with no host synchronization: every record equal to the
-    oracle-checked one and no claim ever saw a foreign epoch."""
+def test_many_streams(tune):
+    """70 streams (PyTorch's pool: distinct handles or not), two launches each
+    with no host synchronization: every record equal to the oracle-checked
+    one, whichever blocks the launches took."""
     n = 8 * 1024 * 64
     w = lp.synth.make("udp64", n, seed=16, corrupt_ppm=10000)
     rec, lens = _oracle(w, n)
@@ -208,3 +310,4 @@ def test_more_streams_than_slots(tune):
             assert torch.equal(col, results[0].columns[c]), (i, c)
         assert r.counter_dict() == want, i
     assert lp.engine.context(0).sched_conflicts() == 0
+    assert _stats()["blocks_held"] == 0

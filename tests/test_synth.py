@@ -19,7 +19,7 @@ def run_oracle(w, nthreads=4):
     return coracle.rx_batch(w.buf, w.n, offsets=w.offsets, lengths=w.lengths, nthreads=nthreads)
 
 
-@pytest.mark.parametrize("name,n", [("rs_sender", 64), ("udp64", 50000), ("tcp1500", 3000), ("imix", 20000),
+@pytest.mark.parametrize("name,n", [("rs_sender", 64), ("udp64", 50000), ("tcp1500", 3000), ("udp1500", 3000), ("imix", 20000),
                                     ("udp6_jumbo", 300)])
 def test_workload_verifies_and_counts(name, n):
     w = lp.synth.make(name, n, seed=5, corrupt_ppm=10000)
@@ -43,7 +43,7 @@ def test_deterministic_across_threads():
     assert (a.buf == b.buf).all() and (a.offsets == b.offsets).all()
 
 
-@pytest.mark.parametrize("name", ["udp64", "imix", "tcp1500"])
+@pytest.mark.parametrize("name", ["udp64", "imix", "tcp1500", "udp1500"])
 def test_range_is_a_slice_of_the_whole_batch(name):
     """pnetgpu_synth_fill_range: frames [first, first + n) equal those frames of the
     whole batch byte for byte (a rank's shard of the bench's global batch), and
