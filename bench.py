@@ -275,10 +275,35 @@ def config0_block(steps, warmup, device):
     out["gpu_tx_fill_kernel_ms"] = round(ms_tx, 4)
     out["gpu_rx_verify_mframes_s"] = round(n / (ms_rx * 1e-3) / 1e6, 1)
     out["gpu_rx_verify_kernel_ms"] = round(ms_rx, 4)
+    out["loopback_netns"] = loopback_leg()
     out["note"] = ("CPU: oracle/pnet_oracle.c (rs_sender_build = rs_sender.rs:25-72 per frame; receive = the "
                    "packetdump.rs chain per frame, dummy-ring hand-over); GPU: kernel time over 2^20 resident "
-                   "frames (a 64-MiB batch, L2/MALL-resident: not an HBM figure); loopback send/recv not run "
-                   "(no CAP_NET_RAW)")
+                   "frames (a 64-MiB batch, L2/MALL-resident: not an HBM figure); loopback_netns: the live "
+                   "AF_PACKET send/receive over lo in a private user+network namespace (tests/netns_loopback.py: "
+                   "rs_sender's frame + 20000 synthetic 64-B frames sent, received in the TPACKET_V3 ring, "
+                   "verified on the GPU zero-copy from the ring against the oracle; a parity leg, the Python "
+                   "send loop's rate is not a benchmark)")
+    return out
+
+
+def loopback_leg(frames=20000):
+    """configs[0]'s loopback send/receive (rs_sender.rs:103-105, rs_receiver.rs:39-55)
+    in a fresh process under `unshare --user --net --map-root-user` (CAP_NET_RAW
+    over its own lo; the process starts before it touches the GPU)."""
+    import shutil
+    if shutil.which("unshare") is None:
+        return {"skipped": "unshare(1) not installed"}
+    cmd = ["unshare", "--user", "--net", "--map-root-user", sys.executable, "-u",
+           os.path.join("tests", "netns_loopback.py"), "--frames", str(frames), "--gpu"]
+    try:
+        r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=240)
+    except Exception as e:   # never fails the bench line
+        return {"skipped": f"{type(e).__name__}: {e}"}
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    if not lines:
+        return {"skipped": f"rc {r.returncode}: {r.stderr.strip()[-300:]}"}
+    out = json.loads(lines[-1])
+    out["rc"] = r.returncode
     return out
 
 
@@ -365,7 +390,7 @@ def e2e_ring_rate(sh, seconds=3.0, columns=None, slots=None):
     return {"mpkts_s": round(frames / el / 1e6, 1), "gb_s": round(nbytes / el / 1e9, 2),
             **_ring_link(frames, nbytes, el, rb, nb),
             "note": "host frames pushed into the pinned ring with pnetgpu_ring_push_many (descriptors and "
-                    "source-adjacent frame copies split over up to 8 host threads), async H2D -> rx kernel -> D2H of "
+                    "source-adjacent frame copies split over up to 16 host threads), async H2D -> rx kernel -> D2H of "
                     f"the record columns ({rb} B/frame: {', '.join(columns)}), {nslots} rotating slots of 1 Mi frames",
             "slots": nslots}
 
@@ -430,6 +455,24 @@ def time_launches(fn, steps, warmup, stream):
     return a.elapsed_time(b) / steps
 
 
+def tx_sector_writes(sh):
+    """Bytes the HBM must write per launch to patch the two checksum fields in
+    place: every 32-B sector that holds a byte of either field (the IPv4 header
+    checksum at frame offset 24, the L4 checksum at 34 + 6 / 16 / 2 for UDP /
+    TCP / ICMP), counted per frame from the frame offsets; the status column
+    adds 2 B per frame. For 64-B frames the two fields sit in the frame's two
+    sectors, so the floor is the whole frame (rs_sender.rs:38-39,70-71 patch
+    both)."""
+    w = sh.w
+    offs = np.arange(sh.n, dtype=np.int64) * w.stride
+    proto = sh.w.buf[offs[:1] + 23][0] if sh.n else 17
+    l4 = 34 + {17: 6, 6: 16, 1: 2}.get(int(proto), 6)
+    sec = np.stack([(offs + p) // 32 for p in (24, 25, l4, l4 + 1)], axis=1)
+    sec.sort(axis=1)
+    distinct = 1 + (np.diff(sec, axis=1) != 0).sum(axis=1)
+    return int(distinct.sum()) * 32 + 2 * sh.n
+
+
 def tx_fill_rate(sh, steps, warmup, device):
     """Sender side (configs[0] builds and checksums frames
     the way benches/rs_sender.rs:38-39,70-71 does): pnetgpu_tx_fill_checksums over
@@ -463,6 +506,12 @@ def tx_fill_rate(sh, steps, warmup, device):
     # what the writes cost in HBM: PMC WRITE_SIZE per frame against the 4 B of
     # checksum fields that change (profiles/pmc_tx_<workload>.json; the sector
     # floor of two fields in two 32-B sectors is 64 B: profiles/r04/tx_writes/)
+    # the same kernel time against the sector floor: frames read once plus
+    # every 32-B sector holding a checksum byte written (what a patch in place
+    # must write; `frac` counts only the 4 changed bytes per frame)
+    floor = sh.frame_bytes + tx_sector_writes(sh)
+    out["sector_floor_bytes_per_launch"] = floor
+    out["frac_sector_floor"] = round(floor / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
     wb = load_traffic(f"tx_{sh.name}", "write_bytes_per_launch")
     if wb:
         out["pmc_write_bytes_per_frame"] = round(wb / sh.n, 1)
@@ -872,8 +921,10 @@ def main():
             line["e2e_pcie_verify"] = e2e_rate(sh, device, columns=VERIFY_COLUMNS)
             # the 1500-B batches over the same pipeline (the link's large-frame rate)
             for name in ("udp1500", "tcp1500"):
-                if name in results and results[name]["sh"].w.buf is not None:
+                if name != primary and name in results and results[name]["sh"].w.buf is not None:
                     line["workloads"][name]["e2e_pcie"] = e2e_rate(results[name]["sh"], device)
+                    if name == "udp1500":
+                        line["workloads"][name]["e2e_zero_copy"] = e2e_zero_copy_rate(results[name]["sh"])
         print(json.dumps(line), flush=True)
     if dist_on:
         torch.distributed.barrier()

@@ -69,9 +69,10 @@ void pnetgpu_ring_destroy(pnetgpu_ring* ring);
 int pnetgpu_ring_push(pnetgpu_ring* ring, const uint8_t* frame, uint32_t len);
 /* Copy n frames (frame i = buf[offsets[i], +lengths[i]) on the host) until the
  * batch is full; *pushed = how many were taken (may be < n: then submit).
- * Frames adjacent in buf are copied by one memcpy, and pushes of >= 8 MiB are
- * split over up to 8 host threads; the batch holds the same frames in the same
- * order as n single pushes would. */
+ * Frames adjacent in buf are copied by one memcpy, and pushes of >= 2^16 frames
+ * are split over up to 16 host threads (descriptors, the cut where the batch
+ * fills and the copies); the batch holds the same frames in the same order as
+ * n single pushes would. */
 int pnetgpu_ring_push_many(pnetgpu_ring* ring, const uint8_t* buf, const uint64_t* offsets,
                            const uint32_t* lengths, uint64_t n, uint64_t* pushed);
 /* Ship the filling batch (no-op returning 0 with *id = UINT64_MAX if empty). */

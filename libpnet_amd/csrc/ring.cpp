@@ -277,18 +277,20 @@ int pnetgpu_ring_push_many(pnetgpu_ring* r, const uint8_t* buf, const uint64_t* 
     // Large pushes are split over host threads, descriptors included: one
     // thread's memcpy into pinned memory tops out far below the PCIe link the
     // batch is headed for, and a serial descriptor pass capped 64-B frames at
-    // ~330 Mframes/s end to end. Pass 1 sums each chunk's lengths; when the whole
-    // push fits (every push but the one that fills a slot by bytes), pass 2
-    // fills each chunk at its prefix offset.
+    // ~330 Mframes/s end to end. Pass 1 sums each chunk's lengths; the last
+    // thread to finish finds the cut (all m frames, or the first chunk whose
+    // frames overflow the slot, scanned to the exact frame: the same cut as
+    // single pushes), and pass 2 fills every chunk's frames below the cut at
+    // its prefix offset.
     uint64_t k = 0, bytes = 0;
     unsigned nt = 1;
-    if (m >= (1u << 16)) nt = std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
+    if (m >= (1u << 16)) nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
     bool done = false;
     if (nt > 1) {
         std::vector<uint64_t> csum(nt, 0);
         std::vector<uint32_t> cmax(nt, 0);
         std::atomic<unsigned> arrived{0};
-        std::atomic<bool> fits{false};
+        uint64_t kcut = 0, bcut = 0;       // written by the decider before the release below
         std::atomic<int> start{0};   // 0: wait, 1: go, 2: abandoned (a thread could not be created)
         auto work = [&](unsigned t) {
             while (start.load(std::memory_order_acquire) == 0) std::this_thread::yield();
@@ -298,16 +300,23 @@ int pnetgpu_ring_push_many(pnetgpu_ring* r, const uint8_t* buf, const uint64_t* 
             for (uint64_t i = lo; i < hi; ++i) sum += lengths[i];
             csum[t] = sum;
             if (arrived.fetch_add(1) + 1 == nt) {   // the last to arrive decides
-                uint64_t tot = 0;
-                for (unsigned c = 0; c < nt; ++c) tot += csum[c];
-                fits.store(tot <= room_b, std::memory_order_release);
-                arrived.fetch_add(1);                  // == nt + 1: released
+                uint64_t cum = 0;
+                unsigned c = 0;
+                while (c < nt && cum + csum[c] <= room_b) cum += csum[c++];
+                uint64_t kk = m;
+                if (c < nt) {                       // chunk c overflows: its exact cut
+                    kk = m * c / nt;
+                    while (lengths[kk] <= room_b - cum) cum += lengths[kk++];
+                }
+                kcut = kk;
+                bcut = cum;
+                arrived.fetch_add(1, std::memory_order_release);   // == nt + 1: released
             }
             while (arrived.load(std::memory_order_acquire) <= nt) std::this_thread::yield();
-            if (!fits.load(std::memory_order_acquire)) return;
+            if (lo >= kcut) return;
             uint64_t at = s.bytes;
             for (unsigned c = 0; c < t; ++c) at += csum[c];
-            cmax[t] = fill_range(lo, hi, at);
+            cmax[t] = fill_range(lo, std::min(hi, kcut), at);
         };
         // no exception may cross the C-ABI: a thread that cannot be created
         // (process/thread limits) releases the ones already started, which
@@ -323,12 +332,11 @@ int pnetgpu_ring_push_many(pnetgpu_ring* r, const uint8_t* buf, const uint64_t* 
         start.store(started ? 1 : 2, std::memory_order_release);
         if (started) work(0);
         for (auto& t : th) t.join();
-        if (started && fits.load()) {
-            k = m;
-            for (unsigned c = 0; c < nt; ++c) {
-                bytes += csum[c];
-                s.max_len = std::max(s.max_len, cmax[c]);
-            }
+        if (started) {
+            if (kcut == 0) return PNETGPU_EFULL;
+            k = kcut;
+            bytes = bcut;
+            for (unsigned c = 0; c < nt; ++c) s.max_len = std::max(s.max_len, cmax[c]);
             done = true;
         }
     }
