@@ -292,10 +292,16 @@ int pnetgpu_ring_push_many(pnetgpu_ring* r, const uint8_t* buf, const uint64_t* 
         std::atomic<unsigned> arrived{0};
         uint64_t kcut = 0, bcut = 0;       // written by the decider before the release below
         std::atomic<int> start{0};   // 0: wait, 1: go, 2: abandoned (a thread could not be created)
+        // barrier 1 (the cut) and, when the push overflows the slot, barrier 2
+        // (the frames below the cut re-split evenly: otherwise one chunk would
+        // hold all of them — 1500-B frames fill a 64-MiB slot within the first
+        // of 16 chunks of a 2^20-frame push)
+        std::atomic<unsigned> arrived2{0};
+        bool rechunk = false;
         auto work = [&](unsigned t) {
             while (start.load(std::memory_order_acquire) == 0) std::this_thread::yield();
             if (start.load(std::memory_order_acquire) == 2) return;
-            const uint64_t lo = m * t / nt, hi = m * (t + 1) / nt;
+            uint64_t lo = m * t / nt, hi = m * (t + 1) / nt;
             uint64_t sum = 0;
             for (uint64_t i = lo; i < hi; ++i) sum += lengths[i];
             csum[t] = sum;
@@ -310,9 +316,19 @@ int pnetgpu_ring_push_many(pnetgpu_ring* r, const uint8_t* buf, const uint64_t* 
                 }
                 kcut = kk;
                 bcut = cum;
+                rechunk = kk < m && kk >= (uint64_t)nt * 64;
                 arrived.fetch_add(1, std::memory_order_release);   // == nt + 1: released
             }
             while (arrived.load(std::memory_order_acquire) <= nt) std::this_thread::yield();
+            if (rechunk) {                          // [0, kcut) in nt even chunks, their sums again
+                lo = kcut * t / nt;
+                hi = kcut * (t + 1) / nt;
+                sum = 0;
+                for (uint64_t i = lo; i < hi; ++i) sum += lengths[i];
+                csum[t] = sum;
+                arrived2.fetch_add(1, std::memory_order_acq_rel);
+                while (arrived2.load(std::memory_order_acquire) < nt) std::this_thread::yield();
+            }
             if (lo >= kcut) return;
             uint64_t at = s.bytes;
             for (unsigned c = 0; c < t; ++c) at += csum[c];

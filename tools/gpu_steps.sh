@@ -44,5 +44,5 @@ for S in "$@"; do
   rc=$?
   echo "step $n $S rc=$rc"
   if [ $rc -ne 0 ]; then tail -30 $L; exit $rc; fi
-  grep -E "passed|failed" $L 2>/dev/null | tail -1
+  grep -E "passed|failed" $L 2>/dev/null | tail -1 || true
 done
