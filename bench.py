@@ -881,9 +881,10 @@ def main():
             line["config0"] = config0_block(args.steps, args.warmup, device)
             line["reference_shapes"] = refshapes_block(args.steps, args.warmup, device)
             line["tx_fill"] = tx_fill_rate(sh, args.steps, args.warmup, device)
-            if "tcp1500" in results:
-                line["workloads"]["tcp1500"]["tx_fill"] = tx_fill_rate(results["tcp1500"]["sh"], args.steps,
-                                                                       args.warmup, device)
+            for name in ("tcp1500", "udp1500"):
+                if name in results and name != primary:
+                    line["workloads"][name]["tx_fill"] = tx_fill_rate(results[name]["sh"], args.steps, args.warmup,
+                                                                      device)
             if "tcp1500" in results:
                 line["workloads"]["tcp1500"]["ipv4_checksum_slices"] = slices_rate(results["tcp1500"]["sh"], args.steps,
                                                                                    args.warmup, device)

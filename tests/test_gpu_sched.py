@@ -43,12 +43,23 @@ class _Dev:
             self.lens = to_dev(w.lengths.astype(np.int32))
         torch.cuda.synchronize()
 
-    def run(self, n, stream=None, cols=lp.IPV4_COLUMNS):
+    def run(self, n, stream=None, cols=lp.IPV4_COLUMNS, out=None):
         w = self.w
         if w.stride:
             return lp.rx_process(self.d, stride=w.stride, frame_len=w.frame_len, n_frames=n, columns=cols,
-                                 stream=stream)
-        return lp.rx_process(self.d, offsets=self.offs, lengths=self.lens, columns=cols, stream=stream)
+                                 stream=stream, out=out)
+        return lp.rx_process(self.d, offsets=self.offs, lengths=self.lens, columns=cols, stream=stream, out=out)
+
+
+def _outs(k, n, cols=lp.IPV4_COLUMNS):
+    """k result blocks with zeroed counters, allocated and zeroed (on the
+    current stream) BEFORE launches on other streams: an RxResult made per
+    launch zeroes its counters on the current stream, which is not ordered
+    with a launch on another stream (with 4 hardware queues a stream's zeroing
+    can even queue behind another stream's held work)."""
+    outs = [lp.RxResult(n, "cuda:0", cols, counters=True) for _ in range(k)]
+    torch.cuda.synchronize()
+    return outs
 
 
 def _stats():
@@ -129,6 +140,7 @@ def test_more_launches_in_flight_than_blocks(tune):
     tune("blocks_per_cu", 1)
     tune("static_pct", 25)
     streams = [torch.cuda.Stream() for _ in range(4)]
+    outs = _outs(100, n, ("status", "l4_csum"))   # before the gate: _outs synchronizes
     gate_s, gate = torch.cuda.Stream(), torch.cuda.Event()
     with torch.cuda.stream(gate_s):
         torch.cuda._sleep(int(3e8))           # holds the launches until all 100 are enqueued
@@ -137,7 +149,7 @@ def test_more_launches_in_flight_than_blocks(tune):
         s.wait_event(gate)
     s0 = _stats()
     assert s0["blocks_held"] == 0 and s0["blocks"] == 64
-    results = [dv.run(n, stream=streams[i % 4], cols=("status", "l4_csum")) for i in range(100)]
+    results = [dv.run(n, stream=streams[i % 4], out=outs[i]) for i in range(100)]
     d = _delta(s0, _stats())
     torch.cuda.synchronize()
     assert d == {"claimed": 64, "static_busy": 36, "static_captured": 0}, d
@@ -164,12 +176,13 @@ def test_destroyed_stream_handle_reused_with_work_in_flight(tune):
     h1, h2 = ctypes.c_void_p(), ctypes.c_void_p()
     assert hip.hipStreamCreate(ctypes.byref(h1)) == 0
     s1 = torch.cuda.ExternalStream(h1.value)
+    outs = _outs(12, n)
     s0 = _stats()
-    first = [dv.run(n, stream=s1) for _ in range(6)]
+    first = [dv.run(n, stream=s1, out=outs[i]) for i in range(6)]
     assert hip.hipStreamDestroy(h1) == 0
     assert hip.hipStreamCreate(ctypes.byref(h2)) == 0
     s2 = torch.cuda.ExternalStream(h2.value)
-    second = [dv.run(n, stream=s2) for _ in range(6)]
+    second = [dv.run(n, stream=s2, out=outs[6 + i]) for i in range(6)]
     torch.cuda.synchronize()
     assert hip.hipStreamDestroy(h2) == 0
     assert _delta(s0, _stats())["claimed"] == 12
@@ -228,7 +241,8 @@ def test_three_streams_no_host_sync(tune):
     tune("static_pct", 25)
     tune("claim_counters", 8)
     streams = [torch.cuda.Stream() for _ in range(3)]
-    results = [dv.run(n, stream=streams[i % 3]) for i in range(150)]
+    outs = _outs(150, n)
+    results = [dv.run(n, stream=streams[i % 3], out=outs[i]) for i in range(150)]
     torch.cuda.synchronize()
     compare(results[0], rec)
     for i, r in enumerate(results):
@@ -302,7 +316,8 @@ def test_many_streams(tune):
     tune("blocks_per_cu", 1)
     tune("static_pct", 25)
     streams = [torch.cuda.Stream() for _ in range(70)]
-    results = [dv.run(n, stream=streams[i % 70], cols=("status", "l4_csum")) for i in range(140)]
+    outs = _outs(140, n, ("status", "l4_csum"))
+    results = [dv.run(n, stream=streams[i % 70], out=outs[i]) for i in range(140)]
     torch.cuda.synchronize()
     compare(results[0], rec)
     for i, r in enumerate(results):

@@ -14,6 +14,7 @@
 #   variant:V:K                tests/test_gpu_parity.py -k K on libpnetgpu_V.so (PNETGPU_LIB)
 #   ab:W:ROUNDS:V+V...         tools/abvar.sh interleaved A/B of library variants
 #   e2e:W:SLOTS                tools/e2e_slots.py (ring slot sweep, e.g. 3,4,6)
+#   py:SCRIPT[:ARGS]           python -u SCRIPT ARGS ('+' for spaces), output in the step log
 set -o pipefail
 TAG=$1; shift
 O=gpurun_out/$TAG
@@ -39,6 +40,7 @@ for S in "$@"; do
                $PYT tests/test_gpu_parity.py -k "$A2" > $L 2>&1 ;;
     ab) timeout -k 10 1200 bash tools/abvar.sh $A1 $A2 ${A3//+/ } > $L 2>&1 ;;
     e2e) timeout -k 10 400 python -u tools/e2e_slots.py --workload $A1 --slots $A2 > $O/e2e_$A1.json 2> $L ;;
+    py) timeout -k 10 600 python -u $A1 ${A2//+/ } > $L 2>&1 ;;
     *) echo "unknown step $S"; exit 2 ;;
   esac
   rc=$?
