@@ -6,8 +6,11 @@ and jumbo (G=64, U=9) — forced with the rx_kind tuning. Interleaved rounds on
 one box, kernel time per launch from one event pair around back-to-back
 launches, records of every shape compared with the mixed shape's.
 
-Batches (~1.5 GiB each): udp1500 frames packed; tcp1500 frames packed; a 1:1
-mix of 64-B and 1500-B frames; 576-B frames (IMIX's middle class); IMIX.
+Batches (~1.2-1.6 GiB each): udp1500 frames packed; tcp1500 frames packed; a
+1:1 mix of 64-B and 1500-B frames; 576-B frames (IMIX's middle class); IMIX;
+cutL: the first L bytes of udp1500 frames packed (L = 768 ... 1280: where the
+shapes cross); jumbo9000: 9000-B IPv6 frames packed; jmix: 64-B and 9000-B
+frames at 7:1.
 
   python tools/desc_shape_probe.py [--rounds 3] [--reps 10]
 """
@@ -59,6 +62,28 @@ def build(name):
             src = w.offsets[idx][:, None] + np.arange(576, dtype=np.uint64)[None, :]
             frames[k:k + idx.size] = w.buf[src.astype(np.int64)]
         return packed(buf, np.full(keep.size, 576, np.uint32))
+    if name.startswith("cut"):                        # the first L bytes of udp1500 frames, packed
+        L = int(name[3:])
+        n = min(1 << 20, (1536 << 20) // L)
+        w = lp.synth.make("udp1500", n, seed=45, corrupt_ppm=10000)
+        buf = np.zeros(n * L + 64, np.uint8)
+        buf[: n * L].reshape(n, L)[:] = w.buf[: n * 1500].reshape(n, 1500)[:, :L]
+        return packed(buf, np.full(n, L, np.uint32))
+    if name == "jumbo9000":
+        n = 1 << 17
+        w = lp.synth.make("udp6_jumbo", n, seed=46, corrupt_ppm=10000)
+        return packed(w.buf, np.full(n, 9000, np.uint32))
+    if name == "jmix":                                # 7:1 64-B and 9000-B frames
+        k = 1 << 16
+        a = lp.synth.make("udp64", 7 * k, seed=47, corrupt_ppm=10000)
+        b = lp.synth.make("udp6_jumbo", k, seed=48, corrupt_ppm=10000)
+        grp = 7 * 64 + 9000
+        buf = np.zeros(k * grp + 64, np.uint8)
+        g = buf[: k * grp].reshape(k, grp)
+        g[:, :448] = a.buf[: 7 * k * 64].reshape(k, 448)
+        g[:, 448:] = b.buf[: k * 9000].reshape(k, 9000)
+        lens = np.tile(np.array([64] * 7 + [9000], np.uint32), k)
+        return packed(buf, lens)
     raise KeyError(name)
 
 
