@@ -135,6 +135,19 @@ extern "C" {
  * pinned ring (pnetgpu_ring.h) uses it whenever a batch qualifies. */
 #define PNETGPU_DESC_COMPACT      0x100u
 
+/* Frame-size hints (descriptor mode; ignored with stride > 0). A descriptor
+ * batch's lengths are device-resident, so the library cannot see its size mix
+ * and runs the mixed shape (built for IMIX-like batches). A caller that knows
+ * its frames (the pinned ring does, from the lengths it pushes) may name the
+ * shape the fixed-stride kinds use: measured on one MI355X box
+ * (profiles/r05/shape/), packed 1500-B frames 0.33 ms mixed -> 0.28 ms MTU,
+ * 9000-B frames 0.205 -> 0.176 ms jumbo, 64-B/9000-B frames at 7:1 0.122 ->
+ * 0.109 ms jumbo — but IMIX 0.34 ms mixed -> 0.58 ms MTU, 1.29 ms jumbo, so
+ * the hint must describe the batch. Records are identical whatever the hint.
+ * pnetgpu_desc_size_hint computes it from host-side lengths. */
+#define PNETGPU_DESC_HINT_LARGE   0x200u  /* (nearly) every frame >= 768 B: the MTU shape       */
+#define PNETGPU_DESC_HINT_JUMBO   0x400u  /* most bytes in frames >= 4 KiB: the jumbo shape      */
+
 /* ---- batch-wide counters (rx columns .counters, uint64 each, accumulated) */
 #define PNETGPU_CTR_FRAMES        0  /* frames with a valid descriptor            */
 #define PNETGPU_CTR_BYTES         1  /* sum of their lengths                      */
@@ -274,6 +287,12 @@ int pnetgpu_ctx_sched_conflicts(pnetgpu_ctx* ctx, uint64_t* count);
 #define PNETGPU_SCHED_BLOCKS           4
 #define PNETGPU_NSCHED_STATS           5
 int pnetgpu_ctx_sched_stats(const pnetgpu_ctx* ctx, uint64_t stats[PNETGPU_NSCHED_STATS]);
+
+/* The PNETGPU_DESC_HINT_* flag for a descriptor batch with these host-side
+ * lengths: JUMBO when frames of >= 4096 B carry >= 80 % of the bytes, LARGE
+ * when >= 15/16 of the frames are >= 768 B, else 0 (the mixed shape). Host
+ * arithmetic over the lengths only (no device work); n = 0 gives 0. */
+uint32_t pnetgpu_desc_size_hint(const uint32_t* lengths, uint64_t n);
 
 /* Receive path: parse + verify every frame of `batch`, write `cols`. */
 int pnetgpu_rx_process(pnetgpu_ctx* ctx, const pnetgpu_batch* batch,

@@ -10,7 +10,7 @@ from . import packet, synth  # noqa: F401  (packet: pnet_packet's function names
 from .ring import HostRegistration, Ring, pcap_frames, pcap_index, pcap_info  # noqa: F401
 from .afpacket import AfPacket, tpacket3_walk  # noqa: F401
 from .views import frame_view  # noqa: F401
-from .engine import (ALL_COLUMNS, COUNTER_NAMES, DESC_COMPACT, FIELD_COLUMNS, IPV4_COLUMNS, RECORD_COLUMNS,  # noqa: F401
+from .engine import (ALL_COLUMNS, COUNTER_NAMES, DESC_COMPACT, DESC_HINT_JUMBO, DESC_HINT_LARGE, desc_size_hint, FIELD_COLUMNS, IPV4_COLUMNS, RECORD_COLUMNS,  # noqa: F401
                      Context, RxResult,
                      checksum_adv_slices, checksum_slices, checksum_slices_compact, checksum_slices_strided, column_bytes, context, ipv4_checksum_slices,
                      ipv6_checksum_slices, last_rx_kernel, rx_process, slice_descriptors, tx_fill_checksums)

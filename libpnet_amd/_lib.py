@@ -105,6 +105,8 @@ def _load():
     L.pnetgpu_ctx_get_tuning.argtypes = [vp, i32, ctypes.POINTER(ctypes.c_int64)]
     L.pnetgpu_ctx_sched_conflicts.restype = i32
     L.pnetgpu_ctx_sched_conflicts.argtypes = [vp, ctypes.POINTER(u64)]
+    L.pnetgpu_desc_size_hint.restype = u32
+    L.pnetgpu_desc_size_hint.argtypes = [vp, u64]
     L.pnetgpu_ctx_sched_stats.restype = i32
     L.pnetgpu_ctx_sched_stats.argtypes = [vp, vp]
     for f in (L.pnetgpu_rx_process, L.pnetgpu_tx_fill_checksums):

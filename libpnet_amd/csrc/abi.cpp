@@ -325,9 +325,10 @@ static int rx_common(pnetgpu_ctx* ctx, const pnetgpu_batch* b, const pnetgpu_rx_
         (cols->dst_ipv6 && (reinterpret_cast<uintptr_t>(cols->dst_ipv6) & 15)))
         return PNETGPU_EINVAL;
     if (b->n_frames > (UINT64_MAX - kRunFrames) / 2) return PNETGPU_EINVAL;
-    if ((b->flags & ~(PNETGPU_RX_VLAN | PNETGPU_RX_IPV6_EXT | PNETGPU_RX_L3 | PNETGPU_DESC_COMPACT)) || b->reserved)
-        return PNETGPU_EINVAL;
-    const uint32_t rxf = b->flags & ~PNETGPU_DESC_COMPACT;   // parse extensions only
+    constexpr uint32_t kRxFlags = PNETGPU_RX_VLAN | PNETGPU_RX_IPV6_EXT | PNETGPU_RX_L3;
+    constexpr uint32_t kHints = PNETGPU_DESC_HINT_LARGE | PNETGPU_DESC_HINT_JUMBO;
+    if ((b->flags & ~(kRxFlags | PNETGPU_DESC_COMPACT | kHints)) || b->reserved) return PNETGPU_EINVAL;
+    const uint32_t rxf = b->flags & kRxFlags;   // parse extensions only
     int rc = set_device(ctx);
     if (rc) return rc;
 
@@ -356,7 +357,11 @@ static int rx_common(pnetgpu_ctx* ctx, const pnetgpu_batch* b, const pnetgpu_rx_
     // shape of the batch's frame sizes: MTU or jumbo for fixed stride, mixed for
     // descriptor batches (their lengths are device-resident).
     int kind = pnetgpu::kKindMixed;
-    if (b->stride) {
+    if (!b->stride) {
+        // the caller's size hint (PNETGPU_DESC_HINT_*): the lengths are device-resident
+        if (b->flags & PNETGPU_DESC_HINT_JUMBO) kind = pnetgpu::kKindJumbo;
+        else if (b->flags & PNETGPU_DESC_HINT_LARGE) kind = pnetgpu::kKindMtu;
+    } else {
         const uint64_t base_sh = (a.delta + b->first_offset) & 15u;
         const uint64_t last_end = a.delta + b->first_offset + (b->n_frames - 1) * (uint64_t)b->stride + b->frame_len;
         const bool fits = b->n_frames <= (UINT64_MAX - a.delta - b->first_offset - b->frame_len) / b->stride &&
@@ -397,6 +402,18 @@ static int rx_common(pnetgpu_ctx* ctx, const pnetgpu_batch* b, const pnetgpu_rx_
         return PNETGPU_EHIP;
     }
     return PNETGPU_OK;
+}
+
+uint32_t pnetgpu_desc_size_hint(const uint32_t* lengths, uint64_t n) {
+    if (!lengths) return 0;
+    uint64_t bytes = 0, jumbo_bytes = 0, large = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        const uint32_t l = lengths[i];
+        bytes += l;
+        if (l >= pnetgpu::kHintJumboMin) jumbo_bytes += l;
+        if (l >= pnetgpu::kHintLargeMin) ++large;
+    }
+    return pnetgpu::desc_size_hint(n, bytes, large, jumbo_bytes);
 }
 
 int pnetgpu_rx_process(pnetgpu_ctx* ctx, const pnetgpu_batch* b, const pnetgpu_rx_columns* cols, void* stream) {

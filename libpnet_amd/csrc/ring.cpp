@@ -39,6 +39,9 @@ struct Slot {
     uint32_t* h_off32 = nullptr;
     uint16_t* h_len16 = nullptr;
     uint32_t max_len = 0;
+    // size statistics of the batch for its PNETGPU_DESC_HINT_* (desc_size_hint)
+    uint64_t n_large = 0, jumbo_bytes = 0;
+    uint64_t frame_bytes = 0;               // sum of the frame lengths (bytes counts gaps in a region)
     uint8_t* d_frames = nullptr;
     uint64_t* d_off = nullptr;
     uint32_t* d_len = nullptr;
@@ -149,6 +152,9 @@ static int take_free_slot(pnetgpu_ring* r) {
             r->slots[i].n = 0;
             r->slots[i].bytes = 0;
             r->slots[i].max_len = 0;
+            r->slots[i].n_large = 0;
+            r->slots[i].jumbo_bytes = 0;
+            r->slots[i].frame_bytes = 0;
             return i;
         }
     }
@@ -231,7 +237,10 @@ int pnetgpu_ring_push(pnetgpu_ring* r, const uint8_t* frame, uint32_t len) {
     s.h_off32[s.n] = (uint32_t)s.bytes;
     s.h_len16[s.n] = (uint16_t)len;
     s.max_len = std::max(s.max_len, len);
+    s.n_large += len >= pnetgpu::kHintLargeMin;
+    s.jumbo_bytes += len >= pnetgpu::kHintJumboMin ? len : 0;
     s.bytes += len;
+    s.frame_bytes += len;
     s.n += 1;
     return PNETGPU_OK;
 }
@@ -251,8 +260,12 @@ int pnetgpu_ring_push_many(pnetgpu_ring* r, const uint8_t* buf, const uint64_t* 
     // frames [lo, hi) with their slot byte offsets starting at `at`: descriptors,
     // then the bytes (runs of frames adjacent in the source go in one memcpy);
     // returns the chunk's largest length
-    auto fill_range = [&](uint64_t lo, uint64_t hi, uint64_t at) {
+    struct Stats {
         uint32_t mx = 0;
+        uint64_t large = 0, jumbo = 0;
+    };
+    auto fill_range = [&](uint64_t lo, uint64_t hi, uint64_t at) {
+        Stats st;
         uint64_t o = at;
         for (uint64_t i = lo; i < hi; ++i) {
             const uint32_t len = lengths[i];
@@ -260,7 +273,9 @@ int pnetgpu_ring_push_many(pnetgpu_ring* r, const uint8_t* buf, const uint64_t* 
             s.h_len[s.n + i] = len;
             s.h_off32[s.n + i] = (uint32_t)o;
             s.h_len16[s.n + i] = (uint16_t)len;
-            mx = std::max(mx, len);
+            st.mx = std::max(st.mx, len);
+            st.large += len >= pnetgpu::kHintLargeMin;
+            st.jumbo += len >= pnetgpu::kHintJumboMin ? len : 0;
             o += len;
         }
         const uint64_t* doff = s.h_off + s.n;
@@ -272,7 +287,7 @@ int pnetgpu_ring_push_many(pnetgpu_ring* r, const uint8_t* buf, const uint64_t* 
             if (run) std::memcpy(dst + doff[i], buf + offsets[i], run);
             i = j;
         }
-        return mx;
+        return st;
     };
     // Large pushes are split over host threads, descriptors included: one
     // thread's memcpy into pinned memory tops out far below the PCIe link the
@@ -288,7 +303,7 @@ int pnetgpu_ring_push_many(pnetgpu_ring* r, const uint8_t* buf, const uint64_t* 
     bool done = false;
     if (nt > 1) {
         std::vector<uint64_t> csum(nt, 0);
-        std::vector<uint32_t> cmax(nt, 0);
+        std::vector<Stats> cst(nt);
         std::atomic<unsigned> arrived{0};
         uint64_t kcut = 0, bcut = 0;       // written by the decider before the release below
         std::atomic<int> start{0};   // 0: wait, 1: go, 2: abandoned (a thread could not be created)
@@ -332,7 +347,7 @@ int pnetgpu_ring_push_many(pnetgpu_ring* r, const uint8_t* buf, const uint64_t* 
             if (lo >= kcut) return;
             uint64_t at = s.bytes;
             for (unsigned c = 0; c < t; ++c) at += csum[c];
-            cmax[t] = fill_range(lo, std::min(hi, kcut), at);
+            cst[t] = fill_range(lo, std::min(hi, kcut), at);
         };
         // no exception may cross the C-ABI: a thread that cannot be created
         // (process/thread limits) releases the ones already started, which
@@ -352,17 +367,25 @@ int pnetgpu_ring_push_many(pnetgpu_ring* r, const uint8_t* buf, const uint64_t* 
             if (kcut == 0) return PNETGPU_EFULL;
             k = kcut;
             bytes = bcut;
-            for (unsigned c = 0; c < nt; ++c) s.max_len = std::max(s.max_len, cmax[c]);
+            for (unsigned c = 0; c < nt; ++c) {
+                s.max_len = std::max(s.max_len, cst[c].mx);
+                s.n_large += cst[c].large;
+                s.jumbo_bytes += cst[c].jumbo;
+            }
             done = true;
         }
     }
     if (!done) {
         while (k < m && lengths[k] <= room_b - bytes) bytes += lengths[k++];
         if (k == 0) return PNETGPU_EFULL;
-        s.max_len = std::max(s.max_len, fill_range(0, k, s.bytes));
+        const Stats st = fill_range(0, k, s.bytes);
+        s.max_len = std::max(s.max_len, st.mx);
+        s.n_large += st.large;
+        s.jumbo_bytes += st.jumbo;
     }
     s.n += k;
     s.bytes += bytes;
+    s.frame_bytes += bytes;
     *pushed = k;
     return PNETGPU_OK;
 }
@@ -395,7 +418,10 @@ static int ship_slot(pnetgpu_ring* r, Slot& s, const uint8_t* src, uint64_t* id)
     b.n_frames = s.n;
     b.offsets = s.d_off;
     b.lengths = s.d_len;
-    b.flags = r->flags | (compact ? PNETGPU_DESC_COMPACT : 0u);
+    // the batch's size mix picks the kernel's tail shape (frames of >= 768 B:
+    // MTU; mostly jumbo bytes: jumbo; else mixed); records are the same
+    b.flags = r->flags | (compact ? PNETGPU_DESC_COMPACT : 0u) |
+              pnetgpu::desc_size_hint(s.n, s.frame_bytes, s.n_large, s.jumbo_bytes);
     pnetgpu_rx_columns c{};
     uint64_t at = 8ull * PNETGPU_NCOUNTERS;          // the counters lead the record block
     for (int k = 0; k < kNumCols; ++k) {
@@ -444,7 +470,8 @@ int pnetgpu_ring_submit_region(pnetgpu_ring* r, const uint8_t* base, const uint6
     if (s.n) return PNETGPU_EFULL;               // pushed frames are waiting: submit them first
     // the longest prefix of frames, ascending and non-overlapping, whose span fits the slot
     const uint64_t o0 = offsets[0];
-    uint64_t k = 0, end = o0;
+    uint64_t k = 0, end = o0, fbytes = 0, large = 0, jumbo = 0;
+    uint32_t mx = 0;
     while (k < n && k < r->cap_frames) {
         if (offsets[k] < end) return PNETGPU_EINVAL;   // frames must ascend without overlap
         const uint64_t fe = offsets[k] + lengths[k];
@@ -453,13 +480,20 @@ int pnetgpu_ring_submit_region(pnetgpu_ring* r, const uint8_t* base, const uint6
         s.h_len[k] = lengths[k];
         s.h_off32[k] = (uint32_t)(offsets[k] - o0);
         s.h_len16[k] = (uint16_t)lengths[k];
-        s.max_len = std::max(s.max_len, lengths[k]);
+        mx = std::max(mx, lengths[k]);
+        fbytes += lengths[k];
+        large += lengths[k] >= pnetgpu::kHintLargeMin;
+        jumbo += lengths[k] >= pnetgpu::kHintJumboMin ? lengths[k] : 0;
         end = fe;
         ++k;
     }
     if (k == 0) return PNETGPU_EFULL;            // the first frame alone exceeds batch_bytes
     s.n = (uint32_t)k;
-    s.bytes = end - o0;
+    s.bytes = end - o0;                          // the span shipped (gaps included)
+    s.frame_bytes = fbytes;
+    s.max_len = mx;
+    s.n_large = large;
+    s.jumbo_bytes = jumbo;
     s.frames_view = base + o0;
     *taken = k;
     return ship_slot(r, s, base + o0, id);

@@ -95,6 +95,18 @@ constexpr int kWaveTimeSlots = 16384;
 // group-rounds issued, slots used and ideal slots (WaveTimer::tail)
 constexpr int kWaveTimeWords = 13;
 
+// PNETGPU_DESC_HINT_* of a descriptor batch from its length statistics (n
+// frames, their bytes, frames >= 768 B, bytes in frames >= 4096 B): the rule of
+// pnetgpu_desc_size_hint, shared with the ring's per-batch counts
+inline uint32_t desc_size_hint(uint64_t n, uint64_t bytes, uint64_t large, uint64_t jumbo_bytes) {
+    if (n == 0) return 0;
+    if (jumbo_bytes && jumbo_bytes * 5 >= bytes * 4) return PNETGPU_DESC_HINT_JUMBO;
+    if (large * 16 >= n * 15) return PNETGPU_DESC_HINT_LARGE;
+    return 0;
+}
+constexpr uint32_t kHintLargeMin = 768;     // bytes: a frame the MTU shape takes well
+constexpr uint32_t kHintJumboMin = 4096;    // bytes: a frame of the jumbo shape
+
 // device index a context is bound to (abi.cpp)
 int ctx_device(const pnetgpu_ctx* ctx);
 

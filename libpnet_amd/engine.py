@@ -73,6 +73,15 @@ IPV4_COLUMNS = ("status", "ip_csum", "l4_csum", "ethertype", "ip_proto", "ttl", 
                 "src_port", "dst_port", "src_ipv4", "dst_ipv4")
 RX_VLAN, RX_IPV6_EXT, RX_L3 = DEFS["PNETGPU_RX_VLAN"], DEFS["PNETGPU_RX_IPV6_EXT"], DEFS["PNETGPU_RX_L3"]
 DESC_COMPACT = DEFS["PNETGPU_DESC_COMPACT"]
+#: frame-size hints of a descriptor batch (the tail shape only; records are identical)
+DESC_HINT_LARGE, DESC_HINT_JUMBO = DEFS["PNETGPU_DESC_HINT_LARGE"], DEFS["PNETGPU_DESC_HINT_JUMBO"]
+
+
+def desc_size_hint(lengths):
+    """pnetgpu_desc_size_hint over host-side frame lengths: DESC_HINT_JUMBO,
+    DESC_HINT_LARGE or 0, to OR into rx_process's flags for a descriptor batch."""
+    a = np.ascontiguousarray(lengths, dtype=np.uint32)
+    return int(lib.pnetgpu_desc_size_hint(ctypes.c_void_p(a.ctypes.data), a.size))
 #: every column: the record columns and the ABI-v3 header-field getters
 ALL_COLUMNS = ALL_COLUMN_NAMES
 #: the record columns of ABI v2 (status, checksums, dispatch fields, addresses, VLAN, L3 offset)
@@ -292,7 +301,9 @@ def rx_process(data, *, n_frames=None, stride=0, frame_len=None, first_offset=0,
     Fixed-stride mode: stride > 0, frame i = data[first_offset + i*stride, +frame_len).
     Descriptor mode:   offsets (int64) / lengths (int32) CUDA tensors, frame i = data[off_i, +len_i);
                        with flags |= DESC_COMPACT, offsets (u32 as int32/uint32) / lengths
-                       (u16 as int16/uint16) — 6 B per frame of descriptors instead of 12.
+                       (u16 as int16/uint16) — 6 B per frame of descriptors instead of 12;
+                       flags |= desc_size_hint(host_lengths) names the kernel's tail
+                       shape for the batch's size mix (MTU / jumbo frames).
     ctx: a Context (default: one shared per device); one host thread per context at a time.
     Returns an RxResult (device columns, accumulated counters)."""
     return _rx_or_tx("pnetgpu_rx_process", data, n_frames, stride, frame_len, first_offset, offsets, lengths,

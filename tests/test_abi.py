@@ -131,3 +131,24 @@ def test_environment_read_only_at_context_creation():
         fn = text.rfind("\nvoid tuning_from_env(", 0, hits[0])
         assert fn >= 0 and text.find("\n}\n", fn) > hits[0]
         assert "tuning_from_env(c);" in text[text.index("int pnetgpu_ctx_create"):]
+
+
+def test_desc_size_hint_rule():
+    """pnetgpu_desc_size_hint: the tail shape a descriptor batch's host-side
+    lengths call for (include/pnetgpu.h) — host arithmetic only."""
+    import numpy as np
+    import libpnet_amd as lp
+    L, J = lp.DESC_HINT_LARGE, lp.DESC_HINT_JUMBO
+    assert lp.desc_size_hint(np.zeros(0, np.uint32)) == 0
+    assert lp.desc_size_hint(np.full(1000, 1500)) == L                      # MTU traffic
+    assert lp.desc_size_hint(np.full(1000, 768)) == L
+    assert lp.desc_size_hint(np.full(1000, 767)) == 0
+    assert lp.desc_size_hint(np.full(1000, 9000)) == J                      # jumbo traffic
+    assert lp.desc_size_hint(np.tile([64] * 7 + [9000], 100)) == J          # 95 % of the bytes jumbo
+    imix = lp.synth.lengths("imix", 100000, seed=1)
+    assert lp.desc_size_hint(imix) == 0                                     # IMIX: the mixed shape
+    assert lp.desc_size_hint(np.array([64] * 1 + [1500] * 15)) == L         # 15/16 large
+    assert lp.desc_size_hint(np.array([64] * 2 + [1500] * 15)) == 0
+    mixed_jumbo = np.array([1500] * 10 + [9000])                            # 9000 of 24000 B: not jumbo
+    assert lp.desc_size_hint(mixed_jumbo) == L
+    assert _lib.lib.pnetgpu_desc_size_hint(None, 5) == 0

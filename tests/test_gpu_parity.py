@@ -1018,3 +1018,66 @@ def test_slice_argument_validation():
         args = {"stride": 20, "slice_len": 20, "skipword": 5, **kw}
         with pytest.raises(ValueError):
             lp.checksum_slices_strided(d, 10, args["stride"], args["slice_len"], args["skipword"])
+
+
+# ---- descriptor batches with a frame-size hint (PNETGPU_DESC_HINT_*) --------
+
+_HINT_KERNEL = {0: "rx_kernel<8, 4, 8, false, 0, true, ", "large": "rx_kernel<8, 8, 4, false, 1, false, ",
+                "jumbo": "rx_kernel<8, 64, 9, true, 0, false, "}
+
+
+@pytest.mark.parametrize("hint", [0, "large", "jumbo"])
+@pytest.mark.parametrize("rxflags", [0, "vlan_ext"])
+def test_descriptor_size_hints_any_batch(hint, rxflags):
+    """A size hint only picks the tail shape: any descriptor batch (random and
+    malformed frames up to 9,100 B, IPv6, VLAN tags and extension headers, at
+    any alignment, full and compact descriptors) under either hint gives the
+    oracle's records and counters, receive and TX fill alike, and the launch
+    names the hinted instantiation."""
+    fl = {0: 0, "large": lp.DESC_HINT_LARGE, "jumbo": lp.DESC_HINT_JUMBO}[hint]
+    rx = 0 if not rxflags else lp.engine.RX_VLAN | lp.engine.RX_IPV6_EXT
+    rng = np.random.default_rng(900 + fl + rx)
+    frames = framegen.edge_frames(rng) + framegen.random_frames(rng, 3000, max_len=9100)
+    buf, offs, lens = framegen.pack(frames, gap=11, rng=rng)
+    rec = coracle.rx_batch(buf, len(offs), offsets=offs, lengths=lens, flags=rx, nthreads=NTHREADS)
+    d = to_dev(buf)
+    o32 = to_dev(offs.astype(np.uint32).view(np.int32))
+    l16 = to_dev(lens.astype(np.uint16).view(np.int16))
+    for compact in (False, True):
+        o, ln = (o32, l16) if compact else (to_dev(offs.astype(np.int64)), to_dev(lens.astype(np.int32)))
+        res = lp.rx_process(d, offsets=o, lengths=ln, columns=ALL_COLUMNS,
+                            flags=fl | rx | (lp.DESC_COMPACT if compact else 0))
+        torch.cuda.synchronize()
+        compare(res, rec)
+        assert res.counter_dict() == oracle_counters(rec, lens), (hint, compact)
+        assert lp.last_rx_kernel().startswith(_HINT_KERNEL[hint]), lp.last_rx_kernel()
+    # TX fill under the hint: the patched buffer equals the oracle's
+    dt = to_dev(buf.copy())
+    lp.tx_fill_checksums(dt, offsets=to_dev(offs.astype(np.int64)), lengths=to_dev(lens.astype(np.int32)),
+                         flags=fl | rx)
+    want_buf, _ = coracle.tx_fill(buf, len(offs), offsets=offs, lengths=lens, flags=rx)
+    torch.cuda.synchronize()
+    assert np.array_equal(dt.cpu().numpy(), want_buf)
+
+
+def test_hints_on_the_bench_batches():
+    """The hint the rule picks for each workload's lengths, and the records
+    under it: 1500-B UDP frames as a descriptor batch (LARGE -> the MTU shape),
+    9000-B IPv6 frames (JUMBO), IMIX (no hint)."""
+    for name, n, want in (("udp1500", 1 << 14, lp.DESC_HINT_LARGE), ("udp6_jumbo", 1 << 11, lp.DESC_HINT_JUMBO),
+                          ("imix", 1 << 16, 0)):
+        w = lp.synth.make(name, n, seed=17, corrupt_ppm=20000)
+        if w.stride:
+            offs = np.arange(n, dtype=np.uint64) * np.uint64(w.stride)
+            lens = np.full(n, w.frame_len, np.uint32)
+        else:
+            offs, lens = w.offsets, w.lengths
+        hint = lp.desc_size_hint(lens)
+        assert hint == want, name
+        res = lp.rx_process(to_dev(w.buf), offsets=to_dev(offs.astype(np.int64)), lengths=to_dev(lens.astype(np.int32)),
+                            flags=hint)
+        torch.cuda.synchronize()
+        rec = oracle_desc(w.buf, offs, lens)
+        compare(res, rec)
+        c = res.counter_dict()
+        assert c["l4_csum_bad"] == w.expect["l4_bad"] and c["ip_csum_bad"] == w.expect["ip_bad"]

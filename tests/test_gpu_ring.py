@@ -199,3 +199,29 @@ def test_ring_slot_count_bounds():
     r = lp.Ring(batch_bytes=1 << 16, batch_frames=64)
     assert r.slots == lp.DEFS["PNETGPU_RING_DEFAULT_SLOTS"] >= 4
     r.close()
+
+
+@pytest.mark.parametrize("name,n,head", [("udp1500", 3000, "rx_kernel<8, 8, 4, false, 1, false, "),
+                                         ("imix", 20000, "rx_kernel<8, 4, 8, false, 0, true, "),
+                                         ("udp6_jumbo", 300, "rx_kernel<8, 64, 9, true, 0, false, ")])
+def test_ring_batches_carry_their_size_hint(name, n, head):
+    """The ring counts each batch's large and jumbo frames as it fills it and
+    ships the batch with its PNETGPU_DESC_HINT_*: MTU traffic runs the MTU
+    shape, jumbo traffic the jumbo shape, IMIX the mixed one — records equal
+    the oracle's either way."""
+    w = lp.synth.make(name, n, seed=23, corrupt_ppm=20000)
+    if w.stride:
+        offs = np.arange(n, dtype=np.uint64) * np.uint64(w.stride)
+        lens = np.full(n, w.frame_len, np.uint32)
+    else:
+        offs, lens = w.offsets, w.lengths
+    frames = [bytes(w.buf[int(o):int(o) + int(l)]) for o, l in zip(offs, lens)]
+    for region in (False, True):
+        ring = lp.Ring(batch_bytes=16 << 20, batch_frames=1 << 15)
+        out = list(ring.feed_region(w.buf, offs, lens) if region else ring.feed_many(w.buf, offs, lens))
+        if not region:
+            ring.submit()
+        assert lp.last_rx_kernel().startswith(head), (region, lp.last_rx_kernel())
+        out += list(ring.drain())
+        ring.close()
+        check_batches(out, frames)
