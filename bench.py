@@ -515,6 +515,34 @@ def tx_fill_rate(sh, steps, warmup, device):
     return out
 
 
+def descriptor_rate(sh, steps, warmup, device):
+    """The same fixed-size frames handed over as a descriptor batch (compact
+    descriptors, as the ring and the AF_PACKET path ship them): kernel time with
+    no size hint (the mixed shape) and with the hint pnetgpu_desc_size_hint
+    gives for their lengths (DESC_HINT_LARGE -> the MTU shape). Algorithmic
+    bytes = frames + 26-B record + 6-B descriptor per frame."""
+    w = sh.w
+    if not w.stride or w.buf is None:
+        return None
+    n = sh.n
+    offs = torch.arange(n, dtype=torch.int64, device=device).mul_(w.stride).to(torch.int32)
+    lens = torch.full((n,), w.frame_len, dtype=torch.int16, device=device)
+    hint = lp.desc_size_hint(np.full(n, w.frame_len, np.uint32))
+    res = lp.RxResult(n, device, lp.IPV4_COLUMNS, counters=False)
+    stream = torch.cuda.Stream(device)
+    alg = sh.frame_bytes + n * (26 + 6)
+    out = {"hint_flag": {0: "none", lp.DESC_HINT_LARGE: "DESC_HINT_LARGE", lp.DESC_HINT_JUMBO: "DESC_HINT_JUMBO"}[hint]}
+    for label, fl in (("no_hint", 0), ("with_hint", hint)):
+        ms = time_launches(lambda s: lp.rx_process(sh.data, offsets=offs, lengths=lens, out=res, stream=s,
+                                                   flags=lp.DESC_COMPACT | fl), steps, warmup, stream)
+        out[label] = {"kernel": lp.last_rx_kernel(), "kernel_avg_ms": round(ms, 4),
+                      "mpkts_s": round(n / (ms * 1e-3) / 1e6, 1),
+                      "frac": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+    out["note"] = (f"{n} frames of {w.frame_len} B as a compact-descriptor batch; alg bytes = frames + 32 B/frame "
+                   "(26-B record + 6-B descriptor)")
+    return out
+
+
 def slices_rate(sh, steps, warmup, device):
     """Batched util::ipv4_checksum (pnetgpu_ipv4_checksum_slices, the
     tcp::ipv4_checksum call of tcp.rs:239-248) over every TCP segment of the
@@ -885,6 +913,9 @@ def main():
                 if name in results and name != primary:
                     line["workloads"][name]["tx_fill"] = tx_fill_rate(results[name]["sh"], args.steps, args.warmup,
                                                                       device)
+            if "udp1500" in results:
+                line["workloads"]["udp1500"]["descriptor_mode"] = descriptor_rate(results["udp1500"]["sh"], args.steps,
+                                                                                 args.warmup, device)
             if "tcp1500" in results:
                 line["workloads"]["tcp1500"]["ipv4_checksum_slices"] = slices_rate(results["tcp1500"]["sh"], args.steps,
                                                                                    args.warmup, device)
