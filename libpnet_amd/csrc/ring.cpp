@@ -259,7 +259,7 @@ int pnetgpu_ring_push_many(pnetgpu_ring* r, const uint8_t* buf, const uint64_t* 
     uint8_t* dst = s.h_frames;
     // frames [lo, hi) with their slot byte offsets starting at `at`: descriptors,
     // then the bytes (runs of frames adjacent in the source go in one memcpy);
-    // returns the chunk's largest length
+    // returns the chunk's largest length and its size-hint counts
     struct Stats {
         uint32_t mx = 0;
         uint64_t large = 0, jumbo = 0;
