@@ -4,8 +4,11 @@
  * synthetic batch of 64-B Eth/IPv4/UDP frames with planted corruptions, then
  *   1. device-resident: hipMemcpy H2D -> pnetgpu_rx_process -> counters;
  *   2. zero-copy producer: the host buffer registered (pnetgpu_host_register)
- *      and shipped by pnetgpu_ring_submit_region, records waited batch by batch;
- * and checks that exactly the planted corruptions were flagged both ways.
+ *      and shipped by pnetgpu_ring_submit_region through a 6-slot ring
+ *      (pnetgpu_ring_create_ex), each batch released once its records are read;
+ *   3. a descriptor batch of 1500-B UDP frames (compact u32/u16 descriptors)
+ *      with the size hint pnetgpu_desc_size_hint gives for their lengths;
+ * and checks that exactly the planted corruptions were flagged every way.
  * Build: make -C libpnet_amd examples    Run: libpnet_amd/build/rx_verify [n_frames]
  */
 #include <hip/hip_runtime_api.h>
@@ -93,7 +96,7 @@ int main(int argc, char** argv) {
     }
     CHECK(pnetgpu_host_register(host, bytes));
     pnetgpu_ring* ring = NULL;
-    CHECK(pnetgpu_ring_create(ctx, 16u << 20, 1u << 18, 0, &ring));
+    CHECK(pnetgpu_ring_create_ex(ctx, 16u << 20, 1u << 18, 0, 6, &ring));
     CHECK(pnetgpu_ring_set_columns(ring, 0x0FFFu));   /* the IPv4 record */
     uint64_t done = 0, seen = 0, ipbad = 0, l4bad = 0;
     for (;;) {
@@ -113,6 +116,7 @@ int main(int argc, char** argv) {
         seen += rb.n_frames;
         ipbad += rb.cols.counters[PNETGPU_CTR_IP_CSUM_BAD];
         l4bad += rb.cols.counters[PNETGPU_CTR_L4_CSUM_BAD];
+        CHECK(pnetgpu_ring_release(ring));   /* done with it: its slot refills now */
     }
     printf("zero-copy ring: frames %llu ip_csum_bad %llu l4_csum_bad %llu\n", (unsigned long long)seen,
            (unsigned long long)ipbad, (unsigned long long)l4bad);
@@ -120,6 +124,61 @@ int main(int argc, char** argv) {
 
     pnetgpu_ring_destroy(ring);
     CHECK(pnetgpu_host_unregister(host));
+
+    /* 3. 1500-B UDP frames as a compact-descriptor batch with their size hint */
+    const uint64_t m = n / 16 ? n / 16 : 1;
+    uint64_t mbytes = 0, mexp[PNETGPU_SYNTH_NEXP];
+    uint32_t mstride = 0, mlen = 0;
+    CHECK(pnetgpu_synth_layout(PNETGPU_SYNTH_UDP1500, m, 8, &mbytes, &mstride, &mlen));
+    uint8_t* mh = (uint8_t*)malloc(mbytes);
+    uint32_t* moff = (uint32_t*)malloc(4 * m);
+    uint16_t* mlen16 = (uint16_t*)malloc(2 * m);
+    uint32_t* mlen32 = (uint32_t*)malloc(4 * m);
+    if (!mh || !moff || !mlen16 || !mlen32) return 1;
+    CHECK(pnetgpu_synth_fill(PNETGPU_SYNTH_UDP1500, m, 8, 20000, mh, mbytes, NULL, NULL, mexp, 8));
+    for (uint64_t i = 0; i < m; ++i) {
+        moff[i] = (uint32_t)(i * mstride);
+        mlen16[i] = (uint16_t)mlen;
+        mlen32[i] = mlen;
+    }
+    const uint32_t hint = pnetgpu_desc_size_hint(mlen32, m);
+    uint8_t* dm = NULL;
+    void *dmo = NULL, *dml = NULL;
+    HCHECK(hipMalloc((void**)&dm, mbytes));
+    HCHECK(hipMalloc(&dmo, 4 * m));
+    HCHECK(hipMalloc(&dml, 2 * m));
+    HCHECK(hipMemcpy(dm, mh, mbytes, hipMemcpyHostToDevice));
+    HCHECK(hipMemcpy(dmo, moff, 4 * m, hipMemcpyHostToDevice));
+    HCHECK(hipMemcpy(dml, mlen16, 2 * m, hipMemcpyHostToDevice));
+    HCHECK(hipMemset(d_ctr, 0, 8 * PNETGPU_NCOUNTERS));
+    memset(&b, 0, sizeof b);
+    b.data = dm;
+    b.data_bytes = mbytes;
+    b.n_frames = m;
+    b.offsets = (const uint64_t*)dmo;   /* PNETGPU_DESC_COMPACT: u32 offsets, u16 lengths */
+    b.lengths = (const uint32_t*)dml;
+    b.flags = PNETGPU_DESC_COMPACT | hint;
+    CHECK(pnetgpu_rx_process(ctx, &b, &cols, NULL));
+    HCHECK(hipMemcpy(ctr, d_ctr, sizeof ctr, hipMemcpyDeviceToHost));
+    printf("1500-B descriptor batch (hint 0x%x, %s): frames %llu ip_csum_bad %llu (planted %llu) l4_csum_bad %llu "
+           "(planted %llu)\n", hint, pnetgpu_last_rx_kernel(), (unsigned long long)ctr[PNETGPU_CTR_FRAMES],
+           (unsigned long long)ctr[PNETGPU_CTR_IP_CSUM_BAD], (unsigned long long)mexp[PNETGPU_SYNTH_EXP_IP_BAD],
+           (unsigned long long)ctr[PNETGPU_CTR_L4_CSUM_BAD], (unsigned long long)mexp[PNETGPU_SYNTH_EXP_L4_BAD]);
+    ok = ok && hint == PNETGPU_DESC_HINT_LARGE && ctr[PNETGPU_CTR_FRAMES] == m &&
+         ctr[PNETGPU_CTR_IP_CSUM_BAD] == mexp[PNETGPU_SYNTH_EXP_IP_BAD] &&
+         ctr[PNETGPU_CTR_L4_CSUM_BAD] == mexp[PNETGPU_SYNTH_EXP_L4_BAD];
+    uint64_t st[PNETGPU_NSCHED_STATS];
+    CHECK(pnetgpu_ctx_sched_stats(ctx, st));
+    printf("run scheduling: %llu launches claimed, %llu static (busy), %llu static (captured), pool %llu\n",
+           (unsigned long long)st[PNETGPU_SCHED_CLAIMED], (unsigned long long)st[PNETGPU_SCHED_STATIC_BUSY],
+           (unsigned long long)st[PNETGPU_SCHED_STATIC_CAPTURED], (unsigned long long)st[PNETGPU_SCHED_BLOCKS]);
+    (void)hipFree(dm);
+    (void)hipFree(dmo);
+    (void)hipFree(dml);
+    free(mh);
+    free(moff);
+    free(mlen16);
+    free(mlen32);
     pnetgpu_ctx_destroy(ctx);
     (void)hipFree(d_frames);
     (void)hipFree(d_status);

@@ -135,12 +135,12 @@ struct RunQueue {
     bool inflight, finished;
     unsigned long long* groups_done;
     uint32_t* done_host;
-    uint32_t seq, nctr;
+    uint32_t seq, ngroups;
 
     __device__ RunQueue(const RunSched& s, uint64_t n_units, uint64_t wave_id, uint64_t wave_stride)
         : next_static(wave_id), stride(wave_stride), nstatic(s.ctr ? s.nstatic : n_units), nruns(n_units), lo(0),
           hi(0), ctr(s.ctr), pend(n_units), kraw(0), gwaves(0), inflight(false), finished(false),
-          groups_done(s.groups_done), done_host(s.done_host), seq(s.seq), nctr(s.nctr) {
+          groups_done(s.groups_done), done_host(s.done_host), seq(s.seq), ngroups(0) {
         if (ctr) {
             const uint64_t h = (wave_id >> 5) % s.nctr, d = nruns - nstatic;
             lo = nstatic + d * h / s.nctr;
@@ -152,6 +152,9 @@ struct RunQueue {
             uint64_t g = h < nch ? ((nch - 1 - h) / s.nctr + 1) * 32 : 0;
             if (rem && full % s.nctr == h) g -= 32 - rem;
             gwaves = (uint32_t)g;
+            // groups that have waves (all nctr when the host sized nctr from this
+            // grid, as plan_sched does): the last of them hands the block back
+            ngroups = (uint32_t)(nch < s.nctr ? nch : s.nctr);
             if (next_static >= nstatic) claim();   // no static share: the first claim now
         }
     }
@@ -180,7 +183,7 @@ struct RunQueue {
             const unsigned long long old = atomicAdd(ctr, 1ull << 32);
             if ((uint32_t)(old >> 32) + 1 == gwaves) {
                 (void)atomicExch(ctr, 0ull);
-                if (atomicAdd(groups_done, 1ull) + 1 == nctr) {
+                if (atomicAdd(groups_done, 1ull) + 1 == ngroups) {
                     (void)atomicExch(groups_done, 0ull);
                     __threadfence_system();
                     __hip_atomic_store(done_host, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);

@@ -1,8 +1,9 @@
 """The plain-C example (examples/rx_verify.c) against the C-ABI: built by
 libpnet_amd/Makefile with gcc, linked only to libpnetgpu.so and the HIP runtime.
-CPU: the binary exists and resolves its libraries. GPU: it runs both the
-device-resident and the zero-copy ring path and finds exactly the planted
-corruptions (its exit status)."""
+CPU: the binary exists and resolves its libraries. GPU: it runs the
+device-resident path, the zero-copy ring path (6 slots, batches released as
+read) and a 1500-B descriptor batch with its size hint, and finds exactly the
+planted corruptions every way (its exit status)."""
 import os
 import subprocess
 
