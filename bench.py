@@ -525,7 +525,11 @@ def descriptor_rate(sh, steps, warmup, device):
     if not w.stride or w.buf is None:
         return None
     n = sh.n
-    offs = torch.arange(n, dtype=torch.int64, device=device).mul_(w.stride).to(torch.int32)
+    if n * w.stride > 0xFFFFFFFF or w.frame_len > 0xFFFF:
+        return None                                     # compact descriptors cannot describe it
+    # u32 offsets held in an int32 tensor (the kernel reads them unsigned)
+    offs = torch.from_numpy((np.arange(n, dtype=np.uint64) * np.uint64(w.stride)).astype(np.uint32).view(np.int32))
+    offs = offs.to(device)
     lens = torch.full((n,), w.frame_len, dtype=torch.int16, device=device)
     hint = lp.desc_size_hint(np.full(n, w.frame_len, np.uint32))
     res = lp.RxResult(n, device, lp.IPV4_COLUMNS, counters=False)
