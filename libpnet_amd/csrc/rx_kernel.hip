@@ -108,13 +108,19 @@ static int resident_blocks(const void* fn, int block_threads) {
 #define PNET_MIXED_NW 8
 #endif
 #define PNET_MIXED_FN(EXT, TX) rx_kernel<PNET_MIXED_NW, PNET_MIXED_CFG, EXT, TX>
+// window granules of the MTU shape's plain instantiations (the EXT ones, with
+// the VLAN / extension-header / field-column code, keep 8: at 6 they spill)
+#ifndef PNET_MTU_NW
+#define PNET_MTU_NW 8
+#endif
+#define PNET_MTU_FN(EXT, TX) rx_kernel<((EXT) ? 8 : PNET_MTU_NW), PNET_MTU_CFG, EXT, TX>
 #define PNET_JUMBO_FN(EXT, TX) rx_kernel<8, PNET_JUMBO_CFG, EXT, TX>
 
 template <bool EXT, bool TX>
 const void* pick_fn(int kind) {
     switch (kind) {
     case kKindSmall: return reinterpret_cast<const void*>(rx_small_kernel<TX, EXT>);
-    case kKindMtu: return reinterpret_cast<const void*>(rx_kernel<8, PNET_MTU_CFG, EXT, TX>);
+    case kKindMtu: return reinterpret_cast<const void*>(PNET_MTU_FN(EXT, TX));
     case kKindJumbo: return reinterpret_cast<const void*>(PNET_JUMBO_FN(EXT, TX));
     default: return reinterpret_cast<const void*>(PNET_MIXED_FN(EXT, TX));
     }
@@ -127,7 +133,7 @@ void launch_t(const RxArgs& args, int kind, int blocks, hipStream_t stream) {
         hipLaunchKernelGGL((rx_small_kernel<TX, EXT>), dim3(blocks), dim3(kBlock), 0, stream, args);
         break;
     case kKindMtu:
-        hipLaunchKernelGGL((rx_kernel<8, PNET_MTU_CFG, EXT, TX>), dim3(blocks), dim3(kBlock), 0, stream, args);
+        hipLaunchKernelGGL((PNET_MTU_FN(EXT, TX)), dim3(blocks), dim3(kBlock), 0, stream, args);
         break;
     case kKindJumbo:
         hipLaunchKernelGGL((PNET_JUMBO_FN(EXT, TX)), dim3(blocks), dim3(kBlock), 0, stream, args);
@@ -169,7 +175,10 @@ const char* rx_kernel_name(int kind, bool ext, bool tx) {
 #define PNET_NAMES(HEAD)                                                                       \
     {HEAD ", false, false>", HEAD ", false, true>", HEAD ", true, false>", HEAD ", true, true>"}
     static const char* const mixed[4] = PNET_NAMES("rx_kernel<" PNET_STR(PNET_MIXED_NW) ", " PNET_STR(PNET_MIXED_CFG));
-    static const char* const mtu[4] = PNET_NAMES("rx_kernel<8, " PNET_STR(PNET_MTU_CFG));
+    static const char* const mtu[4] = {"rx_kernel<" PNET_STR(PNET_MTU_NW) ", " PNET_STR(PNET_MTU_CFG) ", false, false>",
+                                       "rx_kernel<" PNET_STR(PNET_MTU_NW) ", " PNET_STR(PNET_MTU_CFG) ", false, true>",
+                                       "rx_kernel<8, " PNET_STR(PNET_MTU_CFG) ", true, false>",
+                                       "rx_kernel<8, " PNET_STR(PNET_MTU_CFG) ", true, true>"};
     static const char* const jumbo[4] = PNET_NAMES("rx_kernel<8, " PNET_STR(PNET_JUMBO_CFG));
     static const char* const small[4] = {"rx_small_kernel<false, false>", "rx_small_kernel<true, false>",
                                          "rx_small_kernel<false, true>", "rx_small_kernel<true, true>"};
