@@ -309,6 +309,9 @@ int pnetgpu_ctx_sched_stats(const pnetgpu_ctx* ctx, uint64_t stats[PNETGPU_NSCHE
 void pnetgpu_ctx_destroy(pnetgpu_ctx* ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
+    // launches still in flight write their counter block and host word: let
+    // them finish before the pool goes away
+    if (ctx->d_sched) (void)hipDeviceSynchronize();
     if (ctx->d_sched) (void)hipFree(ctx->d_sched);
     if (ctx->done_host) (void)hipHostFree(ctx->done_host);
     delete ctx;

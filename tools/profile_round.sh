@@ -23,6 +23,7 @@ for W in $WLS; do
 done
 PMC=$WLS
 if [ -n "${KN[tcp1500]}" ]; then KN[tx_tcp1500]="${KN[tcp1500]%, false>}, true>"; PMC="$PMC tx_tcp1500"; fi
+if [ -n "${KN[udp1500]}" ]; then KN[tx_udp1500]="${KN[udp1500]%, false>}, true>"; PMC="$PMC tx_udp1500"; fi
 if [ -n "${KN[udp64]}" ]; then KN[tx_udp64]="rx_small_kernel<true, false>"; PMC="$PMC tx_udp64"; fi
 for W in $PMC; do
   WL=${W#tx_}; TX=""; [ "$W" != "$WL" ] && TX="--tx"
@@ -30,7 +31,7 @@ for W in $PMC; do
     timeout -s KILL 120 rocprofv3 --pmc $C --kernel-trace --output-format csv -d $O/pmc_${W}_$C -o run -- \
         python3 $R/tools/kbench.py --workloads $WL --reps 3 --rounds 1 $TX > $O/pmc_${W}_$C.log 2>&1
   done
-  if [ "$W" = tx_tcp1500 ]; then
+  if [ "$W" = tx_tcp1500 ] || [ "$W" = tx_udp1500 ]; then
     ALG=$(python3 -c "print(1500 * 2**20 + 6 * 2**20)")
   elif [ "$W" = tx_udp64 ]; then
     ALG=$(python3 -c "print(64 * 2**24 + 6 * 2**24)")
