@@ -1,5 +1,5 @@
 /*
- * pcapdump.c — libpnet's examples/packetdump.rs over a pcap file, with the
+ * pcapdump.c — libpnet's examples/packetdump.rs over a pcap or pcapng file, with the
  * per-packet work (Ethernet -> IPv4/IPv6 -> UDP/TCP/ICMP/ICMPv6 dispatch, the
  * views' bounds, header fields and checksums) done on the GPU through the
  * C-ABI. The host only indexes the file (pnetgpu_pcap_scan), ships the records
@@ -28,7 +28,7 @@
  * to the GPU in one submit, are printed once the batch is waited, and the
  * block is then given back to the kernel. Needs CAP_NET_RAW.
  *
- * usage: pcapdump [-i NAME] [-c] FILE.pcap
+ * usage: pcapdump [-i NAME] [-c] FILE.pcap|FILE.pcapng
  *        pcapdump [-i NAME] [-c] -l IFACE [-n COUNT] [-w MS]
  *   -i NAME  the "[interface]" label (default: pcap, or IFACE in live mode)
  *   -c       append the checksum verdicts to every IP line

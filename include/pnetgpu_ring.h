@@ -32,7 +32,7 @@ extern "C" {
 #define PNETGPU_EFULL   (-5)   /* push: frame does not fit the filling batch -> submit first   */
 #define PNETGPU_EBUSY   (-6)   /* push/submit: every slot is in flight or held -> wait first     */
 #define PNETGPU_EEMPTY  (-7)   /* wait: nothing in flight; pcap_next: end of file               */
-#define PNETGPU_EFORMAT (-8)   /* pcap: not a classic pcap file with Ethernet link type         */
+#define PNETGPU_EFORMAT (-8)   /* pcap/pcapng: malformed, or an unsupported link type          */
 
 typedef struct pnetgpu_ring pnetgpu_ring;
 
@@ -135,19 +135,26 @@ int pnetgpu_ring_wait(pnetgpu_ring* ring, pnetgpu_ring_batch* out);
  * when nothing is held. */
 int pnetgpu_ring_release(pnetgpu_ring* ring);
 
-/* Classic pcap reader (the pcap.rs:92 from_file receiver): LINKTYPE_ETHERNET,
- * microsecond or nanosecond magic, either byte order. next() returns the
- * captured bytes of each record (incl_len), valid until the following call. */
+/* Capture-file reader (the pcap.rs:92 from_file receiver, which reads through
+ * libpcap's offline reader): classic pcap (microsecond or nanosecond magic,
+ * either byte order) and pcapng (sections in either byte order; Enhanced,
+ * Simple and obsolete Packet Blocks; every interface of the file with the first
+ * one's link type, as libpcap requires; other block types skipped). The
+ * streaming reader takes LINKTYPE_ETHERNET. next() returns the captured bytes
+ * of each record, valid until the following call. */
 typedef struct pnetgpu_pcap pnetgpu_pcap;
 int  pnetgpu_pcap_open(const char* path, pnetgpu_pcap** out);
 int  pnetgpu_pcap_next(pnetgpu_pcap* p, const uint8_t** frame, uint32_t* len);
 void pnetgpu_pcap_close(pnetgpu_pcap* p);
-/* Index an in-memory classic pcap image (e.g. an mmap of the whole file) for
+/* Index an in-memory capture image, classic pcap or pcapng (e.g. an mmap of the whole file) for
  * pnetgpu_ring_submit_region: from byte *pos (0 = start of file) fill up to cap
- * record descriptors (offset of each record's captured bytes in img, incl_len),
- * *n = records found, *pos = where the next call resumes (img_bytes at the end).
- * PNETGPU_EFORMAT for a bad header, an unsupported link type or a truncated
- * record. Link types: Ethernet (1) and raw IP (101, 228, 229) — check
+ * record descriptors (offset of each record's captured bytes in img, its
+ * captured length), *n = records found, *pos = where the next call resumes
+ * (img_bytes at the end; for pcapng a block boundary — each call re-reads the
+ * block headers before it for the section state). PNETGPU_EFORMAT for a bad
+ * header, an unsupported link type, a truncated record or block, or (pcapng)
+ * a block whose two length fields differ or a packet naming an undescribed
+ * interface. Link types: Ethernet (1) and raw IP (101, 228, 229) — check
  * pnetgpu_pcap_info for the receive flags the records need. */
 int pnetgpu_pcap_scan(const uint8_t* img, uint64_t img_bytes, uint64_t* pos, uint64_t* offsets, uint32_t* lengths,
                       uint64_t cap, uint64_t* n);

@@ -1,6 +1,6 @@
 // ring.cpp — host batch producer (include/pnetgpu_ring.h): pinned host batches
-// filled frame by frame, shipped and verified asynchronously on the GPU, plus a
-// dependency-free classic pcap reader (the pnet_datalink pcap.rs:92 receiver).
+// filled frame by frame, shipped and verified asynchronously on the GPU (the
+// capture-file readers that feed it are in pcap.cpp).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -95,11 +95,6 @@ struct pnetgpu_ring {
     uint64_t next_id = 0;
 };
 
-struct pnetgpu_pcap {
-    FILE* f = nullptr;
-    bool swap = false;
-    std::vector<uint8_t> buf;
-};
 
 static void free_slot(Slot& s) {
     if (s.h_frames) (void)hipHostFree(s.h_frames);
@@ -566,116 +561,6 @@ int pnetgpu_host_unregister(void* p) {
     pnetgpu::set_last_hip_error(0);
     const hipError_t e = hipHostUnregister(p);
     return e == hipSuccess ? PNETGPU_OK : pnetgpu::hip_fail(e);
-}
-
-// ---- classic pcap reader -----------------------------------------------------
-
-static uint32_t rd32(const uint8_t* p, bool swap) {
-    uint32_t v;
-    std::memcpy(&v, p, 4);
-    return swap ? __builtin_bswap32(v) : v;
-}
-
-int pnetgpu_pcap_open(const char* path, pnetgpu_pcap** out) {
-    if (!path || !out) return PNETGPU_EINVAL;
-    *out = nullptr;
-    FILE* f = std::fopen(path, "rb");
-    if (!f) return PNETGPU_EINVAL;
-    uint8_t gh[24];
-    if (std::fread(gh, 1, 24, f) != 24) {
-        std::fclose(f);
-        return PNETGPU_EFORMAT;
-    }
-    uint32_t magic;
-    std::memcpy(&magic, gh, 4);
-    bool swap;
-    if (magic == 0xa1b2c3d4u || magic == 0xa1b23c4du) swap = false;
-    else if (magic == 0xd4c3b2a1u || magic == 0x4d3cb2a1u) swap = true;
-    else {
-        std::fclose(f);
-        return PNETGPU_EFORMAT;
-    }
-    if (rd32(gh + 20, swap) != 1u) {             // LINKTYPE_ETHERNET
-        std::fclose(f);
-        return PNETGPU_EFORMAT;
-    }
-    auto* p = new (std::nothrow) pnetgpu_pcap;
-    if (!p) {
-        std::fclose(f);
-        return PNETGPU_ENOMEM;
-    }
-    p->f = f;
-    p->swap = swap;
-    *out = p;
-    return PNETGPU_OK;
-}
-
-int pnetgpu_pcap_next(pnetgpu_pcap* p, const uint8_t** frame, uint32_t* len) {
-    if (!p || !frame || !len) return PNETGPU_EINVAL;
-    uint8_t rh[16];
-    const size_t got = std::fread(rh, 1, 16, p->f);
-    if (got == 0) return PNETGPU_EEMPTY;
-    if (got != 16) return PNETGPU_EFORMAT;
-    const uint32_t incl = rd32(rh + 8, p->swap);
-    if (incl > (1u << 26)) return PNETGPU_EFORMAT;
-    p->buf.resize(incl ? incl : 1);
-    if (incl && std::fread(p->buf.data(), 1, incl, p->f) != incl) return PNETGPU_EFORMAT;
-    *frame = p->buf.data();
-    *len = incl;
-    return PNETGPU_OK;
-}
-
-// Global header of an in-memory image: byte order, and the receive flags its
-// link type needs (LINKTYPE_ETHERNET 1 -> 0; LINKTYPE_RAW 101, LINKTYPE_IPV4 228,
-// LINKTYPE_IPV6 229 -> PNETGPU_RX_L3); any other link type is EFORMAT.
-static int pcap_header(const uint8_t* img, uint64_t img_bytes, bool* swap, uint32_t* linktype, uint32_t* flags) {
-    if (img_bytes < 24) return PNETGPU_EFORMAT;
-    uint32_t magic;
-    std::memcpy(&magic, img, 4);
-    if (magic == 0xa1b2c3d4u || magic == 0xa1b23c4du) *swap = false;
-    else if (magic == 0xd4c3b2a1u || magic == 0x4d3cb2a1u) *swap = true;
-    else return PNETGPU_EFORMAT;
-    *linktype = rd32(img + 20, *swap);
-    if (*linktype == 1u) *flags = 0;
-    else if (*linktype == 101u || *linktype == 228u || *linktype == 229u) *flags = PNETGPU_RX_L3;
-    else return PNETGPU_EFORMAT;
-    return PNETGPU_OK;
-}
-
-int pnetgpu_pcap_info(const uint8_t* img, uint64_t img_bytes, uint32_t* linktype, uint32_t* rx_flags) {
-    if (!img || !linktype || !rx_flags) return PNETGPU_EINVAL;
-    bool swap;
-    return pcap_header(img, img_bytes, &swap, linktype, rx_flags);
-}
-
-int pnetgpu_pcap_scan(const uint8_t* img, uint64_t img_bytes, uint64_t* pos, uint64_t* offsets, uint32_t* lengths,
-                      uint64_t cap, uint64_t* n) {
-    if (!img || !pos || !n || (cap && (!offsets || !lengths))) return PNETGPU_EINVAL;
-    *n = 0;
-    bool swap;
-    uint32_t linktype, flags;
-    const int rc = pcap_header(img, img_bytes, &swap, &linktype, &flags);
-    if (rc) return rc;
-    uint64_t p = *pos < 24 ? 24 : *pos;
-    uint64_t k = 0;
-    while (k < cap && p < img_bytes) {
-        if (img_bytes - p < 16) return PNETGPU_EFORMAT;      // truncated record header
-        const uint32_t incl = rd32(img + p + 8, swap);
-        if (incl > (1u << 26) || incl > img_bytes - p - 16) return PNETGPU_EFORMAT;
-        offsets[k] = p + 16;
-        lengths[k] = incl;
-        p += 16ull + incl;
-        ++k;
-    }
-    *n = k;
-    *pos = p;
-    return PNETGPU_OK;
-}
-
-void pnetgpu_pcap_close(pnetgpu_pcap* p) {
-    if (!p) return;
-    if (p->f) std::fclose(p->f);
-    delete p;
 }
 
 }  // extern "C"

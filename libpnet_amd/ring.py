@@ -263,7 +263,7 @@ class HostRegistration:
 
 
 def pcap_index(img, batch=1 << 16):
-    """Record descriptors of an in-memory classic pcap image (e.g. np.fromfile or
+    """Record descriptors of an in-memory pcap or pcapng image (e.g. np.fromfile or
     np.memmap of the file): (offsets uint64, lengths uint32) of every record's
     captured bytes within img, for Ring.feed_region (pnetgpu_pcap_scan)."""
     img = np.ascontiguousarray(img, np.uint8)
@@ -293,7 +293,7 @@ def pcap_info(img):
 
 
 def pcap_frames(path):
-    """Frames of a classic Ethernet pcap file, as bytes (pcap.rs:92,168-179 receiver)."""
+    """Frames of an Ethernet pcap or pcapng file, as bytes (pcap.rs:92,168-179 receiver)."""
     h = ctypes.c_void_p()
     check(lib.pnetgpu_pcap_open(str(path).encode(), ctypes.byref(h)), "pnetgpu_pcap_open")
     try:

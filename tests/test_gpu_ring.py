@@ -225,3 +225,22 @@ def test_ring_batches_carry_their_size_hint(name, n, head):
         out += list(ring.drain())
         ring.close()
         check_batches(out, frames)
+
+
+@pytest.mark.parametrize("big", [False, True])
+def test_ring_zero_copy_pcapng_image(tmp_path, big):
+    """A pcapng capture (the other format libpcap's offline reader — and so
+    pnet_datalink's pcap::from_file — takes), indexed in memory by
+    pnetgpu_pcap_scan and shipped zero-copy: records equal the oracle's."""
+    from tests.pcaputil import write_pcapng
+    rng = np.random.default_rng(12)
+    frames = framegen.edge_frames(rng) + framegen.random_frames(rng, 3000, max_len=9000)
+    p = tmp_path / "replay.pcapng"
+    write_pcapng(p, frames, big_endian=big, kinds=(["epb", "spb", "pb"] * len(frames))[:len(frames)], sections=3)
+    img = np.fromfile(p, dtype=np.uint8)
+    offs, lens = lp.pcap_index(img, batch=1000)
+    ring = lp.Ring(batch_bytes=1 << 20, batch_frames=600)
+    with lp.HostRegistration(img):
+        out = list(ring.feed_region(img, offs, lens)) + list(ring.drain())
+    check_batches(out, frames)
+    assert list(lp.pcap_frames(p)) == frames

@@ -1,5 +1,5 @@
 """Host code under AddressSanitizer + UBSan (CPU only): the synthetic-frame
-producer, the classic-pcap reader and the C-ABI argument validation, built from
+producer, the classic-pcap and pcapng readers (fuzzed) and the C-ABI argument validation, built from
 sanitized objects into one executable (libpnet_amd/Makefile `asan-test`)."""
 import os
 import shutil

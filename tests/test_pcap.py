@@ -8,7 +8,7 @@ import pytest
 import libpnet_amd as lp
 from libpnet_amd._lib import PnetGpuError
 from tests import framegen
-from tests.pcaputil import write_pcap
+from tests.pcaputil import pcapng_bytes, write_pcap, write_pcapng
 
 
 @pytest.mark.parametrize("nanos", [False, True])
@@ -72,3 +72,79 @@ def test_pcap_info_link_types(tmp_path, linktype, flags):
     assert flags == 0 or flags == lp.engine.RX_L3
     offs, lens = lp.pcap_index(img)
     assert [bytes(img[o:o + n]) for o, n in zip(offs, lens)] == frames
+
+
+# ---- pcapng (libpcap's other offline format, pcap.rs:92 from_file) ---------
+
+@pytest.mark.parametrize("big", [False, True])
+@pytest.mark.parametrize("kinds", ["epb", "spb", "pb", "mixed"])
+def test_pcapng_roundtrip(tmp_path, big, kinds):
+    """Streaming reader and in-memory indexer over pcapng: every byte order,
+    Enhanced / Simple / obsolete Packet Blocks, several interfaces and sections,
+    options and skipped block types; the frames come back as written."""
+    frames = framegen.random_frames(np.random.default_rng(7), 400) + [b""]
+    k = (["epb", "spb", "pb"] * len(frames))[:len(frames)] if kinds == "mixed" else [kinds] * len(frames)
+    n_if = 1 if kinds in ("spb", "mixed") else 3
+    p = tmp_path / "t.pcapng"
+    write_pcapng(p, frames, big_endian=big, kinds=k, n_if=n_if, sections=1 if kinds == "spb" else 3)
+    assert list(lp.pcap_frames(p)) == frames
+    img = np.fromfile(p, dtype=np.uint8)
+    offs, lens = lp.pcap_index(img, batch=37)                 # many resumed calls
+    assert [bytes(img[o:o + n]) for o, n in zip(offs, lens)] == frames
+    assert lp.pcap_info(img) == (1, 0)
+
+
+def test_pcapng_simple_packet_blocks_honour_the_snap_length(tmp_path):
+    """An SPB carries no captured length: it is min(original length, the
+    interface's snap length) (the data past it is padding)."""
+    frames = [bytes(range(256)) * 2, b"\x07" * 90]
+    img = np.frombuffer(pcapng_bytes(frames, kinds=["spb", "spb"], snaplen=100), np.uint8)
+    offs, lens = lp.pcap_index(img)
+    assert list(lens) == [100, 90]
+    assert bytes(img[offs[0]:offs[0] + 100]) == frames[0][:100]
+
+
+def test_pcapng_raw_ip_link_type(tmp_path):
+    frames = [f[14:] for f in framegen.random_frames(np.random.default_rng(8), 40)]
+    img = np.frombuffer(pcapng_bytes(frames, linktype=101, n_if=2), np.uint8)
+    assert lp.pcap_info(img) == (101, lp.engine.RX_L3)
+    offs, lens = lp.pcap_index(img)
+    assert [bytes(img[o:o + n]) for o, n in zip(offs, lens)] == frames
+    p = tmp_path / "raw.pcapng"
+    p.write_bytes(img.tobytes())
+    with pytest.raises(PnetGpuError):                         # the streaming reader is Ethernet-only
+        list(lp.pcap_frames(p))
+
+
+def test_pcapng_rejects_malformed(tmp_path):
+    frames = [b"\x01" * 100, b"\x02" * 61]
+    good = pcapng_bytes(frames)
+    img = np.frombuffer(good, np.uint8)
+    for bad in (img[:-6],                                     # last block cut short
+                np.concatenate([img, np.zeros(8, np.uint8)])):   # trailing garbage shorter than a block
+        with pytest.raises(PnetGpuError):
+            lp.pcap_index(bad)
+    b = bytearray(good)
+    b[len(b) - 4] ^= 1                                        # trailing length != leading length
+    with pytest.raises(PnetGpuError):
+        lp.pcap_index(np.frombuffer(bytes(b), np.uint8))
+    b = bytearray(good)
+    struct.pack_into("<I", b, 8, 0x11223344)                  # bad byte-order magic
+    with pytest.raises(PnetGpuError):
+        lp.pcap_index(np.frombuffer(bytes(b), np.uint8))
+    # interfaces of different link types (libpcap refuses them too)
+    two = pcapng_bytes(frames, n_if=1) + pcapng_bytes(frames, linktype=101, n_if=1)
+    with pytest.raises(PnetGpuError):
+        lp.pcap_index(np.frombuffer(two, np.uint8))
+    # an EPB naming an interface that was never described
+    lonely = pcapng_bytes(frames, n_if=1)
+    epb_if = lonely.find(struct.pack("<II", 6, 12 + 20 + 100)) + 8
+    b = bytearray(lonely)
+    struct.pack_into("<I", b, epb_if, 5)
+    with pytest.raises(PnetGpuError):
+        lp.pcap_index(np.frombuffer(bytes(b), np.uint8))
+    for path, data in (("a.pcapng", two), ("b.pcapng", bytes(b))):
+        q = tmp_path / path
+        q.write_bytes(data)
+        with pytest.raises(PnetGpuError):
+            list(lp.pcap_frames(q))

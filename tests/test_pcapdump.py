@@ -12,7 +12,7 @@ import pytest
 
 from tests import framegen
 from tests.packetdump_fmt import line, v6
-from tests.pcaputil import write_pcap
+from tests.pcaputil import write_pcap, write_pcapng
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 EXE = os.path.join(ROOT, "libpnet_amd", "build", "pcapdump")
@@ -84,12 +84,18 @@ def special_frames(rng):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("csum", [False, True])
-def test_pcapdump_matches_packetdump_lines(tmp_path, csum):
+@pytest.mark.parametrize("csum,fmt", [(False, "pcap"), (True, "pcap"), (True, "pcapng")])
+def test_pcapdump_matches_packetdump_lines(tmp_path, csum, fmt):
+    """pcapng captures (Enhanced / Simple / obsolete Packet Blocks over two
+    interfaces and two sections) print the same lines as classic pcap ones."""
     rng = np.random.default_rng(77)
     frames = special_frames(rng) + framegen.edge_frames(rng) + framegen.random_frames(rng, 3000)
-    p = tmp_path / "dump.pcap"
-    write_pcap(p, frames)
+    p = tmp_path / f"dump.{fmt}"
+    if fmt == "pcap":
+        write_pcap(p, frames)
+    else:
+        write_pcapng(p, frames, kinds=(["epb", "pb", "epb", "spb"] * len(frames))[:len(frames)], n_if=2,
+                     sections=2)
     args = [EXE, "-i", "eth7"] + (["-c"] if csum else []) + [str(p)]
     r = subprocess.run(args, capture_output=True, text=True, timeout=100)
     assert r.returncode == 0, r.stderr

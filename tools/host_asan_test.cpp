@@ -1,6 +1,6 @@
 // host_asan_test.cpp — AddressSanitizer/UBSan run of the library's HOST code
-// (no GPU needed): the synthetic-frame producer, the classic-pcap reader and
-// in-memory indexer, the TPACKET_V3 block walk (fuzzed: it parses memory the
+// (no GPU needed): the synthetic-frame producer, the classic-pcap and pcapng
+// readers and in-memory indexers (fuzzed), the TPACKET_V3 block walk (fuzzed: it parses memory the
 // OS kernel writes) and the C-ABI's argument validation. Linked from objects built with
 // -fsanitize=address,undefined (libpnet_amd/Makefile target `asan-test`), so
 // the sanitizer runtime comes with the executable itself.
@@ -231,12 +231,114 @@ static void test_scan_fuzz() {
     }
 }
 
+// pcapng image: SHB, two IDBs, EPB / SPB / PB packets, a skipped block
+static std::vector<uint8_t> pcapng_image(bool be, const std::vector<std::vector<uint8_t>>& frames) {
+    std::vector<uint8_t> b;
+    auto block = [&](uint32_t type, const std::vector<uint8_t>& body) {
+        std::vector<uint8_t> padded = body;
+        while (padded.size() % 4) padded.push_back(0);
+        const uint32_t n = 12 + (uint32_t)padded.size();
+        put32(b, type, be);
+        put32(b, n, be);
+        b.insert(b.end(), padded.begin(), padded.end());
+        put32(b, n, be);
+    };
+    std::vector<uint8_t> shb;
+    put32(shb, 0x1A2B3C4Du, be);
+    put16(shb, 1, be);
+    put16(shb, 0, be);
+    put32(shb, 0xFFFFFFFFu, be);
+    put32(shb, 0xFFFFFFFFu, be);
+    block(0x0A0D0D0Au, shb);
+    for (int i = 0; i < 2; ++i) {
+        std::vector<uint8_t> idb;
+        put16(idb, 1, be);
+        put16(idb, 0, be);
+        put32(idb, i ? 0u : 150u, be);
+        block(1, idb);
+    }
+    block(0x40000BADu, std::vector<uint8_t>(7, 0x5A));
+    for (size_t i = 0; i < frames.size(); ++i) {
+        const auto& f = frames[i];
+        std::vector<uint8_t> body;
+        const uint32_t kind = (uint32_t)(i % 3);
+        if (kind == 0) {                                   // EPB
+            put32(body, (uint32_t)(i % 2), be);
+            put32(body, 0, be);
+            put32(body, (uint32_t)i, be);
+            put32(body, (uint32_t)f.size(), be);
+            put32(body, (uint32_t)f.size(), be);
+            body.insert(body.end(), f.begin(), f.end());
+            block(6, body);
+        } else if (kind == 1) {                            // SPB
+            put32(body, (uint32_t)f.size(), be);
+            body.insert(body.end(), f.begin(), f.end());
+            block(3, body);
+        } else {                                           // obsolete PB
+            put16(body, (uint16_t)(i % 2), be);
+            put16(body, 0, be);
+            put32(body, 0, be);
+            put32(body, (uint32_t)i, be);
+            put32(body, (uint32_t)f.size(), be);
+            put32(body, (uint32_t)f.size(), be);
+            body.insert(body.end(), f.begin(), f.end());
+            block(2, body);
+        }
+    }
+    return b;
+}
+
+// The pcapng indexer and streaming reader over mutated and truncated images:
+// every descriptor stays inside the image, nothing reads past it (ASan).
+static void test_pcapng_fuzz() {
+    std::vector<std::vector<uint8_t>> frames;
+    for (int i = 0; i < 40; ++i) frames.push_back(std::vector<uint8_t>(rnd() % 200, (uint8_t)i));
+    for (int be = 0; be < 2; ++be) {
+        const std::vector<uint8_t> img = pcapng_image(be != 0, frames);
+        uint64_t pos = 0, n = 0, offs[64];
+        uint32_t lens[64];
+        CHECK(pnetgpu_pcap_scan(img.data(), img.size(), &pos, offs, lens, 64, &n) == PNETGPU_OK);
+        CHECK(n == frames.size() && pos == img.size());
+        for (uint64_t k = 0; k < n; ++k)
+            CHECK(lens[k] == std::min<uint32_t>((uint32_t)frames[k].size(), k % 3 == 1 ? 150u : 0xFFFFFFFFu));
+        for (int iter = 0; iter < 3000; ++iter) {
+            std::vector<uint8_t> m = img;
+            const int flips = 1 + (int)(rnd() % 3);
+            for (int k = 0; k < flips; ++k) m[rnd() % m.size()] = (uint8_t)rnd();
+            const uint64_t cut = rnd() % 3 == 0 ? rnd() % m.size() : m.size();
+            uint64_t p = 0, got = 0;
+            for (int guard = 0; guard < 100 && p < cut; ++guard) {
+                if (pnetgpu_pcap_scan(m.data(), cut, &p, offs, lens, 7, &got) != 0) break;
+                for (uint64_t k = 0; k < got; ++k) CHECK(offs[k] + lens[k] <= cut);
+                if (got == 0) break;
+            }
+            uint32_t lt = 0, fl = 0;
+            (void)pnetgpu_pcap_info(m.data(), cut, &lt, &fl);
+            if (iter % 30 == 0) {                            // the streaming reader on the same bytes
+                const std::string path = "/tmp/pnet_asan_ng.pcapng";
+                FILE* f = std::fopen(path.c_str(), "wb");
+                std::fwrite(m.data(), 1, cut, f);
+                std::fclose(f);
+                pnetgpu_pcap* r = nullptr;
+                if (pnetgpu_pcap_open(path.c_str(), &r) == PNETGPU_OK) {
+                    const uint8_t* fr;
+                    uint32_t len;
+                    for (int guard = 0; guard < 200 && pnetgpu_pcap_next(r, &fr, &len) == PNETGPU_OK; ++guard)
+                        if (len) CHECK(fr[len - 1] == fr[len - 1]);   // touches the last byte (ASan)
+                    pnetgpu_pcap_close(r);
+                }
+            }
+        }
+    }
+}
+
 int main() {
     test_synth();
     test_pcap();
     test_abi_validation();
     test_walk_fuzz();
     test_scan_fuzz();
+    test_pcapng_fuzz();
     std::printf("%s (%d failures)\n", failures ? "FAILED" : "ok", failures);
     return failures ? 1 : 0;
 }
