@@ -927,9 +927,21 @@ def main():
             # every e2e line ships the same 26-B IPv4 record, so they differ only
             # in the producer; the verify-only line (status + both checksums,
             # 6 B/frame back) shows the H2D-bound rate
-            line["e2e_pcie"] = e2e_rate(sh, device)
-            line["e2e_ring"] = e2e_ring_rate(sh)
-            line["e2e_zero_copy"] = e2e_zero_copy_rate(sh)
+            # the three producers of the same record, interleaved twice: the link's
+            # rate drifts within a box, so each line keeps its better run and
+            # lists both (runs_link_gb_s)
+            runs = {"e2e_pcie": [], "e2e_zero_copy": [], "e2e_ring": []}
+            for _ in range(2):
+                runs["e2e_pcie"].append(e2e_rate(sh, device))
+                runs["e2e_zero_copy"].append(e2e_zero_copy_rate(sh))
+                runs["e2e_ring"].append(e2e_ring_rate(sh))
+            for key, rs in runs.items():
+                if rs[0] is None:
+                    line[key] = None
+                    continue
+                best = dict(max(rs, key=lambda x: x["link_gb_s"]))
+                best["runs_link_gb_s"] = [x["link_gb_s"] for x in rs]
+                line[key] = best
             line["e2e_pcie_verify"] = e2e_rate(sh, device, columns=VERIFY_COLUMNS)
             # the 1500-B batches over the same pipeline (the link's large-frame rate)
             for name in ("udp1500", "tcp1500"):
