@@ -353,12 +353,12 @@ def e2e_ring_rate(sh, seconds=3.0, columns=None, slots=None):
     while time.perf_counter() - t0 < seconds:
         for b in ring.feed_many(w.buf, offs, lens):
             frames += b.n
-            nbytes += int(b.lengths.sum())
+            nbytes += b.counters["bytes"]          # the GPU counted them
             nb += 1
             del b
     for b in ring.drain():
         frames += b.n
-        nbytes += int(b.lengths.sum())
+        nbytes += b.counters["bytes"]          # the GPU counted them
         nb += 1
     el = time.perf_counter() - t0
     ring.close()
@@ -396,12 +396,12 @@ def e2e_zero_copy_rate(sh, seconds=3.0, columns=None, slots=None):
         while time.perf_counter() - t0 < seconds:
             for b in ring.feed_region(buf, offs, lens):
                 frames += b.n
-                nbytes += int(b.lengths.sum())
+                nbytes += b.counters["bytes"]          # the GPU counted them
                 nb += 1
                 del b
         for b in ring.drain():
             frames += b.n
-            nbytes += int(b.lengths.sum())
+            nbytes += b.counters["bytes"]          # the GPU counted them
             nb += 1
         el = time.perf_counter() - t0
     finally:

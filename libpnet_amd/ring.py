@@ -64,34 +64,72 @@ def _setup():
 _setup()
 
 
+class _Mem:
+    """A raw memory range as a numpy array without building a ctypes array type
+    per call (np.ctypeslib.as_array does, which cost ~1 ms per waited batch
+    over its 20 arrays: a quarter of the ring's link rate at 78 GB/s)."""
+
+    __slots__ = ("__array_interface__",)
+
+    def __init__(self, ptr, shape, dtype):
+        self.__array_interface__ = {"data": (ptr, False), "shape": shape, "typestr": np.dtype(dtype).str,
+                                    "version": 3}
+
+
+def _view(ptr, shape, dtype):
+    if not ptr or not int(np.prod(shape)):
+        return np.zeros(shape, dtype)
+    return np.asarray(_Mem(ptr, shape, dtype))
+
+
 class Batch:
     """A finished ring batch. With copy=False the arrays are views of the ring's
     pinned memory, valid until the ring's next wait or release (the C-ABI
     contract): the generators below release a batch when they resume after
-    yielding it, so views must not outlive the consumer's loop iteration."""
+    yielding it, so views must not outlive the consumer's loop iteration.
+    The views are made on first use (offsets, lengths, frames, records): a
+    consumer that reads only the counters costs one small view per batch, which
+    keeps the ring at the link's rate (tools/ring_probe.py)."""
 
     def __init__(self, rb, copy=True):
         n = int(rb.n_frames)
         self.id, self.n = int(rb.id), n
-        cp = (lambda a: a.copy()) if copy else (lambda a: a)
-        self.offsets = cp(np.ctypeslib.as_array(ctypes.cast(rb.offsets, ctypes.POINTER(ctypes.c_uint64)), (n,)))
-        self.lengths = cp(np.ctypeslib.as_array(ctypes.cast(rb.lengths, ctypes.POINTER(ctypes.c_uint32)), (n,)))
-        nbytes = int(self.offsets[-1] + self.lengths[-1]) if n else 0
-        self.frames = cp(np.ctypeslib.as_array(ctypes.cast(rb.frames, ctypes.POINTER(ctypes.c_uint8)),
-                                               (max(nbytes, 1),))[:nbytes])
-        self.records = {}
-        for c, (_, npdt, shape) in COLUMNS.items():
-            ptr = getattr(rb.cols, c)
-            if not ptr:                     # not selected (Ring(columns=...))
-                continue
-            itemsize = np.dtype(npdt).itemsize
-            ct = {1: ctypes.c_uint8, 2: ctypes.c_uint16, 4: ctypes.c_uint32, 8: ctypes.c_uint64}[itemsize]
-            a = np.ctypeslib.as_array(ctypes.cast(ptr, ctypes.POINTER(ct)), (n,) + shape) if n else np.zeros(
-                (0,) + shape, npdt)
-            self.records[c] = cp(a).view(npdt)
-        ctr = np.ctypeslib.as_array(ctypes.cast(rb.cols.counters, ctypes.POINTER(ctypes.c_uint64)),
-                                    (len(COUNTER_NAMES),))
+        self._ptr = (rb.offsets, rb.lengths, rb.frames)
+        self._cols = {c: getattr(rb.cols, c) for c in COLUMNS}
+        self._cache = {}
+        ctr = _view(rb.cols.counters, (len(COUNTER_NAMES),), np.uint64)
         self.counters = dict(zip(COUNTER_NAMES, (int(x) for x in ctr)))
+        if copy:                            # owned arrays, valid after the ring moves on
+            self._cache = {"offsets": self.offsets.copy(), "lengths": self.lengths.copy()}
+            self._cache["frames"] = self.frames.copy()
+            self._cache["records"] = {c: v.copy() for c, v in self.records.items()}
+
+    @property
+    def offsets(self):
+        if "offsets" not in self._cache:
+            self._cache["offsets"] = _view(self._ptr[0], (self.n,), np.uint64)
+        return self._cache["offsets"]
+
+    @property
+    def lengths(self):
+        if "lengths" not in self._cache:
+            self._cache["lengths"] = _view(self._ptr[1], (self.n,), np.uint32)
+        return self._cache["lengths"]
+
+    @property
+    def frames(self):
+        if "frames" not in self._cache:
+            nbytes = int(self.offsets[-1] + self.lengths[-1]) if self.n else 0
+            self._cache["frames"] = _view(self._ptr[2], (nbytes,), np.uint8)
+        return self._cache["frames"]
+
+    @property
+    def records(self):
+        """Host record columns by name (only the ones the ring computed)."""
+        if "records" not in self._cache:
+            self._cache["records"] = {c: _view(ptr, (self.n,) + COLUMNS[c][2], COLUMNS[c][1])
+                                      for c, ptr in self._cols.items() if ptr}
+        return self._cache["records"]
 
 
 class Ring:
