@@ -3,9 +3,11 @@ small batches, each with a random batch form (fixed stride at a random
 alignment — which is what routes 64-B frames to rx_small_kernel —, full or
 compact descriptors), a random frame mix (valid / corrupted / truncated /
 padded, VLAN and IPv6 extension frames when the flags ask for them), random
-dispatch flags, a random subset of the result columns (which picks the plain,
-FIELDS and EXT instantiations and the small kernel's linear-slot paths), a
-misaligned data pointer, and receive or TX. Every column, the counters and
+dispatch flags, a random frame-size hint (which picks the mixed, MTU or jumbo
+tail shape for descriptor batches and must be ignored in stride mode), a
+random subset of the result columns (which picks the plain, FIELDS and EXT
+instantiations and the small kernel's linear-slot paths), a misaligned data
+pointer, and receive or TX. Every column, the counters and
 (TX) the patched bytes must equal the oracle's."""
 import numpy as np
 import pytest
@@ -52,7 +54,7 @@ def test_random_batches_soak(seed):
         cols = tuple(c for c in ALL_COLUMNS if c in set(rng.choice(ALL_COLUMNS, ncols, replace=False)))
         n = int(rng.integers(1, 900))
         mis = int(rng.integers(0, 16))
-        what = (seed, it, form, flags, tx, cols)
+        what = (seed, it, form, flags, tx, cols)   # (the hint is drawn below)
         if form == "stride":
             flen = int(rng.choice([40, 54, 60, 64, 64, 64, 100, 576, 1500]))
             stride = flen + int(rng.choice([0, 0, 0, 4, 16, 64]))
@@ -82,7 +84,8 @@ def test_random_batches_soak(seed):
                 fl = flags
             okw = dict(offsets=offs, lengths=lens)
             want_src = buf
-        call_flags = fl if form != "stride" else flags
+        hint = int(rng.choice([0, 0, lp.DESC_HINT_LARGE, lp.DESC_HINT_JUMBO]))
+        call_flags = (fl if form != "stride" else flags) | hint
         if tx:
             want_buf, rec = coracle.tx_fill(want_src, n, flags=flags, **okw)
             res = lp.tx_fill_checksums(d, columns=cols, counters=True, flags=call_flags, **kw)
