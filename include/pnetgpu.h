@@ -238,10 +238,11 @@ const char* pnetgpu_strerror(int code);
 /* The hipError_t behind the last PNETGPU_EHIP a kernel launch returned on the
  * calling thread (0 if none); PNETGPU_DEBUG=1 also prints it to stderr. */
 int         pnetgpu_last_hip_error(void);
-/* The receive kernel the last pnetgpu_rx_process / pnetgpu_tx_fill_checksums
- * launch on the calling thread used, named as rocprofv3 names it (e.g.
- * "rx_kernel<8, 4, 8, false, 0, true, false, false>"; "" before any launch):
- * what a profile's kernel row is, for measurement records. Static storage. */
+/* The kernel the last pnetgpu_rx_process / pnetgpu_tx_fill_checksums /
+ * pnetgpu_*_slices launch on the calling thread used, named as rocprofv3 names
+ * it (e.g. "rx_kernel<8, 4, 8, false, 0, true, false, false>",
+ * "slice_tiny_kernel<true>"; "" before any launch): what a profile's kernel
+ * row is, for measurement records. Static storage. */
 const char* pnetgpu_last_rx_kernel(void);
 int         pnetgpu_device_count(int* count);
 
@@ -259,7 +260,8 @@ void pnetgpu_ctx_destroy(pnetgpu_ctx* ctx);
 #define PNETGPU_TUNE_STATIC_PCT          2  /* share of runs taken in grid-stride order, 0..100 (100: no claims; default 88) */
 #define PNETGPU_TUNE_CLAIM_COUNTERS      3  /* claim counters per launch, 1..128 (default 64)              */
 #define PNETGPU_TUNE_SLICE_BLOCKS_PER_CU 4  /* slice grids: resident blocks per CU (> 0)                   */
-#define PNETGPU_TUNE_SLICE_KERNEL        5  /* descriptor slices: 1 slice_run_kernel, 2 slice_kernel       */
+#define PNETGPU_TUNE_SLICE_KERNEL        5  /* descriptor slices: 1 slice_run_kernel, 2 slice_kernel,
+                                             * 3 slice_tiny_kernel (util::checksum batches; others: 1)    */
 #define PNETGPU_TUNE_SLICE_DENSE_SPAN    6  /* bytes a run of small slices must span to be LDS-staged (default 2048) */
 #define PNETGPU_TUNE_DEBUG               7  /* 1: log each receive call's kernel and grid to stderr        */
 #define PNETGPU_TUNE_SCHED_EPOCH         8  /* retired (per-stream epochs, ABI v3 before the counter pool):

@@ -32,8 +32,9 @@ struct pnetgpu_ctx {
     int cus;
     // resident blocks per CU of each receive kernel (kind x EXT), queried once
     int per_cu[8][2] = {};
-    // of each slice kernel: [strided, run, group] x pseudo {0, 4, 16} x extra
-    int slice_per_cu[3][8][2] = {};
+    // of each slice kernel: [strided, run, group, tiny] x pseudo {0, 4, 16} x extra
+    // (strided: its variant; tiny: compact descriptors or not)
+    int slice_per_cu[4][8][2] = {};
     // run-claim counter blocks (RunSched): kSchedBlocks blocks of kSchedStride
     // u64. Block b is free when done_host[b] (pinned, written by the last wave
     // of the launch that held it) equals seq[b], the sequence number the host
@@ -73,7 +74,7 @@ int64_t tuning(const pnetgpu_ctx* ctx, int key) { return ctx->tune[key]; }
 // persistent slice grid: one resident wave of blocks (at most `want`)
 int slice_grid(pnetgpu_ctx* ctx, int which, int pseudo, bool extra, uint64_t want) {
     // which 0 (strided): pseudo = strided_variant() in 0..7
-    const int k = which == 0 ? pseudo : (pseudo == 0 ? 0 : pseudo == 4 ? 1 : 2);
+    const int k = which == 0 || which == 3 ? pseudo : (pseudo == 0 ? 0 : pseudo == 4 ? 1 : 2);
     int& c = ctx->slice_per_cu[which][k][extra ? 1 : 0];
     if (c <= 0) c = pnetgpu::slice_blocks_per_cu(which, pseudo, extra);
     const int64_t v = tuning(ctx, PNETGPU_TUNE_SLICE_BLOCKS_PER_CU);
@@ -175,7 +176,7 @@ bool tuning_valid(int key, int64_t v) {
     case PNETGPU_TUNE_SLICE_BLOCKS_PER_CU: return v >= 1 && v <= 64;
     case PNETGPU_TUNE_STATIC_PCT: return v >= 0 && v <= 100;
     case PNETGPU_TUNE_CLAIM_COUNTERS: return v >= 1 && v <= (int64_t)kMaxCtrs;
-    case PNETGPU_TUNE_SLICE_KERNEL: return v == 1 || v == 2;
+    case PNETGPU_TUNE_SLICE_KERNEL: return v >= 1 && v <= 3;
     case PNETGPU_TUNE_SLICE_DENSE_SPAN: return v >= 0 && v <= 65536;
     case PNETGPU_TUNE_DEBUG: return v == 0 || v == 1;
     case PNETGPU_TUNE_SCHED_EPOCH: return v >= 0 && v <= (int64_t)UINT32_MAX;   // retired: accepted, ignored
@@ -189,7 +190,8 @@ void tuning_from_env(pnetgpu_ctx* c) {
         const char* e = std::getenv(kTuneEnv[k]);
         if (!e || !*e) continue;
         int64_t v;
-        if (k == PNETGPU_TUNE_SLICE_KERNEL && (e[0] == 'r' || e[0] == 'g')) v = e[0] == 'r' ? 1 : 2;
+        if (k == PNETGPU_TUNE_SLICE_KERNEL && (e[0] == 'r' || e[0] == 'g' || e[0] == 't'))
+            v = e[0] == 'r' ? 1 : e[0] == 'g' ? 2 : 3;   // run, group, tiny
         else v = std::strtoll(e, nullptr, 10);
         if (tuning_valid(k, v)) c->tune[k] = v;
     }
@@ -439,11 +441,17 @@ static uint32_t dense_span(const pnetgpu_ctx* ctx) {
     return v >= 0 ? (uint32_t)std::min<int64_t>(v, UINT32_MAX) : 2048u;
 }
 
-// slice_run_kernel for buffers of at most 512 B per slice unless the tuning
-// names the kernel (1 run, 2 group)
-static bool slice_run_choice(const pnetgpu_ctx* ctx, uint64_t data_bytes, uint64_t n) {
+// The descriptor slice kernel of a batch (1 slice_run_kernel, 2 slice_kernel,
+// 3 slice_tiny_kernel), by the buffer bytes per slice unless the tuning names
+// one: tiny for util::checksum batches of at most kTinyBytesPerSlice, run up
+// to 512, group above. Tiny takes util::checksum only (no pseudo-header, no
+// extra slice); a tuned 3 elsewhere means run.
+static int slice_choice(const pnetgpu_ctx* ctx, uint64_t data_bytes, uint64_t n, bool plain) {
     const int64_t k = tuning(ctx, PNETGPU_TUNE_SLICE_KERNEL);
-    return k == 1 ? true : k == 2 ? false : data_bytes / n <= 512;
+    if (k == 3) return plain ? 3 : 1;
+    if (k == 1 || k == 2) return (int)k;
+    const uint64_t per = data_bytes / n;
+    return plain && per <= pnetgpu::kTinyBytesPerSlice ? 3 : per <= 512 ? 1 : 2;
 }
 
 static int slices_common(pnetgpu_ctx* ctx, const uint8_t* data, uint64_t data_bytes, uint64_t n,
@@ -483,16 +491,18 @@ static int slices_common(pnetgpu_ctx* ctx, const uint8_t* data, uint64_t data_by
     // take slice_kernel; callers that know their slice sizes set
     // PNETGPU_TUNE_SLICE_KERNEL (1 run, 2 group), and uniform slices have
     // pnetgpu_checksum_slices_strided, which decides by the slice length itself.
-    const bool run = slice_run_choice(ctx, data_bytes, n);
+    const int which = slice_choice(ctx, data_bytes, n, pseudo == 0 && !extra_offsets);
+    const bool run = which != 2;
     const uint64_t per_block = run ? kBlock : kBlock / 16;
-    const int blocks = slice_grid(ctx, run ? 1 : 2, pseudo, extra_offsets != nullptr, (n + per_block - 1) / per_block);
-    // scheduled units: slice_run_kernel's runs of 64 slices, slice_kernel's 4
+    const int blocks = slice_grid(ctx, which, which == 3 ? 0 : pseudo, extra_offsets != nullptr,
+                                  (n + per_block - 1) / per_block);
+    // scheduled units: slice_run_kernel's / slice_tiny_kernel's runs of 64 slices, slice_kernel's 4
     int blk;
     uint32_t prev;
     if ((rc = plan_sched(ctx, run ? (n + 63) / 64 : (n + 3) / 4, (uint64_t)blocks * 4, stream, &a.sched, &blk,
                          &prev)))
         return rc;
-    if (const int e = pnetgpu::launch_slices(a, pseudo, run, blocks, static_cast<hipStream_t>(stream))) {
+    if (const int e = pnetgpu::launch_slices(a, pseudo, which, blocks, static_cast<hipStream_t>(stream))) {
         sched_undo(ctx, blk, prev);
         pnetgpu::set_last_hip_error(e);
         return PNETGPU_EHIP;
@@ -540,7 +550,7 @@ int pnetgpu_checksum_slices_strided(pnetgpu_ctx* ctx, const uint8_t* data, uint6
                          &blk, &prev)))
         return rc;
     const int e = small ? pnetgpu::launch_slices_strided_small(a, blocks, static_cast<hipStream_t>(stream))
-                        : pnetgpu::launch_slices(a, 0, run, blocks, static_cast<hipStream_t>(stream));
+                        : pnetgpu::launch_slices(a, 0, run ? 1 : 2, blocks, static_cast<hipStream_t>(stream));
     if (e) {
         sched_undo(ctx, blk, prev);
         return pnetgpu::hip_fail((hipError_t)e);
@@ -564,15 +574,16 @@ int pnetgpu_checksum_slices_compact(pnetgpu_ctx* ctx, const uint8_t* data, uint6
     a.out = out;
     a.dense_min = dense_span(ctx);
     // the same choice as pnetgpu_checksum_slices (by the buffer bytes per slice)
-    const bool run = slice_run_choice(ctx, data_bytes, n);
+    const int which = slice_choice(ctx, data_bytes, n, true);
+    const bool run = which != 2;
     const uint64_t per_block = run ? kBlock : kBlock / 16;
-    const int blocks = slice_grid(ctx, run ? 1 : 2, 0, false, (n + per_block - 1) / per_block);
+    const int blocks = slice_grid(ctx, which, which == 3 ? 1 : 0, false, (n + per_block - 1) / per_block);
     int blk;
     uint32_t prev;
     if ((rc = plan_sched(ctx, run ? (n + 63) / 64 : (n + 3) / 4, (uint64_t)blocks * 4, stream, &a.sched, &blk,
                          &prev)))
         return rc;
-    if (const int e = pnetgpu::launch_slices(a, 0, run, blocks, static_cast<hipStream_t>(stream))) {
+    if (const int e = pnetgpu::launch_slices(a, 0, which, blocks, static_cast<hipStream_t>(stream))) {
         sched_undo(ctx, blk, prev);
         return pnetgpu::hip_fail((hipError_t)e);
     }

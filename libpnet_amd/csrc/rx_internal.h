@@ -115,9 +115,13 @@ int rx_waves_per_block(int kind);
 // both return the hipError_t of the launch (0 = hipSuccess); errors pending
 // from earlier, unrelated HIP calls are cleared first
 int launch_rx(const RxArgs& args, int kind, int blocks, bool tx, hipStream_t stream);
-int launch_slices(const SliceArgs& args, int pseudo, bool run, int blocks, hipStream_t stream);
+// buffers of at most this many bytes per slice take slice_tiny_kernel
+// (util::checksum batches; rx_slices.h)
+constexpr uint32_t kTinyBytesPerSlice = 32;
+// which: 1 slice_run_kernel, 2 slice_kernel, 3 slice_tiny_kernel (util::checksum only, no extra)
+int launch_slices(const SliceArgs& args, int pseudo, int which, int blocks, hipStream_t stream);
 // resident blocks per CU of slice kernel `which` (0 strided: `pseudo` = its
-// strided_variant(), 1 run, 2 group)
+// strided_variant(), 1 run, 2 group, 3 tiny: `pseudo` = 1 for compact descriptors)
 int slice_blocks_per_cu(int which, int pseudo, bool extra);
 int strided_variant(uint32_t slice_len, uint32_t stride);
 // uniform slices of at most 64 B at a stride of at most 64 B (util::checksum)

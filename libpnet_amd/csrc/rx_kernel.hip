@@ -230,12 +230,14 @@ static const void* strided_pick(int v) {
     }
 }
 
-// Resident 256-thread blocks per CU of a slice kernel (0 strided, 1 run, 2 group),
+// Resident 256-thread blocks per CU of a slice kernel (0 strided, 1 run, 2 group, 3 tiny),
 // so that the persistent grid is exactly one resident wave of blocks (a grid
 // larger than what fits runs its last blocks after the first ones finish).
 int slice_blocks_per_cu(int which, int pseudo, bool extra) {
     // which 0 (strided): pseudo holds strided_variant() of the instantiation
     const void* fn = which == 0 ? strided_pick(pseudo)
+                   : which == 3 ? (pseudo ? reinterpret_cast<const void*>(slice_tiny_kernel<true>)
+                                          : reinterpret_cast<const void*>(slice_tiny_kernel<false>))
                    : which == 1 ? (pseudo == 0 ? reinterpret_cast<const void*>(slice_run_kernel<0, false>)
                                   : pseudo == 4 ? (extra ? reinterpret_cast<const void*>(slice_run_kernel<4, true>)
                                                          : reinterpret_cast<const void*>(slice_run_kernel<4, false>))
@@ -249,8 +251,15 @@ int slice_blocks_per_cu(int which, int pseudo, bool extra) {
     return resident_blocks(fn, kBlock);
 }
 
+static const char* const kStridedNames[8] = {
+    "slice_strided_kernel<6, true, false>", "slice_strided_kernel<6, true, true>",
+    "slice_strided_kernel<17, true, false>", "slice_strided_kernel<17, true, true>",
+    "slice_strided_kernel<2, false, true>", "slice_strided_kernel<6, false, true>",
+    "slice_strided_kernel<10, false, true>", "slice_strided_kernel<17, false, true>"};
+
 int launch_slices_strided_small(const SliceArgs& args, int blocks, hipStream_t stream) {
     (void)hipGetLastError();
+    set_last_rx_kernel(kStridedNames[strided_variant(args.slice_len, args.stride)]);
     // one launch per instantiation (hipLaunchKernelGGL needs the template at compile time)
 #define PNET_STRIDED(ND, EX, PAD) \
     hipLaunchKernelGGL((slice_strided_kernel<ND, EX, PAD>), dim3(blocks), dim3(kBlock), 0, stream, args)
@@ -268,10 +277,25 @@ int launch_slices_strided_small(const SliceArgs& args, int blocks, hipStream_t s
     return (int)hipGetLastError();
 }
 
-int launch_slices(const SliceArgs& args, int pseudo, bool run, int blocks, hipStream_t stream) {
+int launch_slices(const SliceArgs& args, int pseudo, int which, int blocks, hipStream_t stream) {
     const bool extra = args.extra_offsets != nullptr;
     (void)hipGetLastError();
     if (pseudo == 0 && extra) return -1;   // util::checksum has no extra slice
+    if (which == 3) {
+        if (pseudo || extra || args.strided) return -1;
+        set_last_rx_kernel(args.compact ? "slice_tiny_kernel<true>" : "slice_tiny_kernel<false>");
+        if (args.compact) hipLaunchKernelGGL((slice_tiny_kernel<true>), dim3(blocks), dim3(kBlock), 0, stream, args);
+        else hipLaunchKernelGGL((slice_tiny_kernel<false>), dim3(blocks), dim3(kBlock), 0, stream, args);
+        return (int)hipGetLastError();
+    }
+    const bool run = which == 1;
+    // rocprofv3's names: [run / group][pseudo 0, 4, 16][extra]
+    static const char* const kNames[2][3][2] = {
+        {{"slice_run_kernel<0, false>", ""}, {"slice_run_kernel<4, false>", "slice_run_kernel<4, true>"},
+         {"slice_run_kernel<16, false>", "slice_run_kernel<16, true>"}},
+        {{"slice_kernel<0, false>", ""}, {"slice_kernel<4, false>", "slice_kernel<4, true>"},
+         {"slice_kernel<16, false>", "slice_kernel<16, true>"}}};
+    set_last_rx_kernel(kNames[run ? 0 : 1][pseudo == 0 ? 0 : pseudo == 4 ? 1 : 2][extra ? 1 : 0]);
 #define PNET_RUN(P, X) hipLaunchKernelGGL((slice_run_kernel<P, X>), dim3(blocks), dim3(kBlock), 0, stream, args)
     if (run) {
         if (pseudo == 0) PNET_RUN(0, false);

@@ -404,6 +404,196 @@ __global__ __launch_bounds__(kBlock, PNET_RUN_MINWAVES) void slice_run_kernel(Sl
     }
 }
 
+// slice_tiny_kernel<COMPACT> (round 5): util::checksum over descriptor
+// batches of tiny slices — the host takes it when the buffer holds at most
+// kTinyBytesPerSlice bytes per slice, which is the reference's own bench shape
+// (20-B slices, checksum_benchmarks.rs:8-12) given with 16-B or 8-B
+// descriptors. slice_run_kernel's mapping (one wave per run of 64 slices,
+// lane l <-> slice l, a slice of at most 3 granules — 33 B at any alignment —
+// summed by its own lane) without its LDS stage and size classes, software-pipelined across the
+// wave's runs: while run r is summed and stored, the granules and
+// skipped-word bytes of run r+1 and the descriptors of run r+2 are in
+// flight. slice_run_kernel waited for a descriptor load and then for its
+// granule loads in every run — two memory latencies per 64 slices, at 4
+// waves/SIMD (108 VGPRs). Every prefetch load is unconditional (addresses
+// clamped to the slice's last granule, or a zero pad for empty and invalid
+// slices) so that the compiler's memory counter waits stay exact across the
+// loop; the sum reads every granule whole and subtracts the bytes outside
+// the slice, so the clamped duplicates cancel. A longer slice (rare at <= 32
+// B per slice) is finished by its own lane from the granules it holds when
+// it spans at most kTinyLaneGranules, else by the whole wave, one slice at a
+// time, after the run's own lanes.
+__device__ __attribute__((aligned(16))) uint32_t tiny_pad[4];   // zero: the loads of empty slices
+
+struct TinyDesc {
+    uint64_t off;
+    uint32_t w, skip;   // compact: w = the packed length | skipword << 16; full: w = length
+    bool in;
+};
+constexpr int kTinyGranules = 3;
+constexpr int kTinyLaneGranules = 15;   // 3 held + 3 rounds of 4; longer slices: the whole wave
+struct TinyStage {
+    uint4 v[kTinyGranules];
+    uint64_t off;      // + delta, 0 for an empty or invalid slice
+    uint32_t len, skip;
+    bool in;
+};
+
+// lane's raw descriptor in run `run` (loads only: decoded and checked by
+// tiny_issue, where they are waited for anyway)
+template <bool COMPACT>
+__device__ __forceinline__ TinyDesc tiny_desc(const SliceArgs& a, uint64_t run, uint64_t nruns, int lane) {
+    TinyDesc d;
+    const uint64_t i = run * kWave + (uint64_t)lane;
+    d.in = run < nruns && i < a.n;
+    const uint64_t k = d.in ? i : a.n - 1;   // a valid index either way (n >= 1)
+    if (COMPACT) {
+        const uint2 x = reinterpret_cast<const uint2*>(a.offsets)[k];
+        d.off = x.x;
+        d.w = x.y;
+        d.skip = 0;
+    } else {
+        d.off = a.offsets[k];
+        d.w = a.lengths[k];
+        d.skip = a.skipwords[k];
+    }
+    return d;
+}
+
+// the run's loads: kTinyGranules granules from the slice's first, clamped to
+// its last (the zero pad for an empty or invalid slice)
+template <bool COMPACT>
+__device__ __forceinline__ TinyStage tiny_issue(const SliceArgs& a, const TinyDesc& d) {
+    TinyStage s;
+    uint64_t off = d.off + a.delta;
+    uint32_t len = COMPACT ? d.w & 0xFFFFu : d.w;
+    if (!d.in || off > a.limit || (uint64_t)len > a.limit - off) {
+        off = 0;
+        len = 0;
+    }
+    const uint32_t sh = (uint32_t)(off & 15);
+    const uint32_t last = len ? (sh + len - 1) >> 4 : 0u;
+    const uint8_t* fb = len ? a.data + (off - sh) : reinterpret_cast<const uint8_t*>(tiny_pad);
+#pragma unroll
+    for (int c = 0; c < kTinyGranules; ++c) s.v[c] = load16(fb + 16u * min((uint32_t)c, last));
+    s.off = off;
+    s.len = len;
+    s.skip = COMPACT ? d.w >> 16 : d.skip;
+    s.in = d.in;
+    return s;
+}
+
+// bytes y and y + 1 (y < 47) of the 48-B window g0..g2 as b0 | b1 << 8 (and
+// higher bytes): the two dwords holding them picked by selects (an indexed
+// read of a register array becomes scratch), then a funnel shift
+__device__ __forceinline__ uint32_t window_bytes(const uint4& g0, const uint4& g1, const uint4& g2, uint32_t y) {
+    const uint32_t w[13] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w, g2.x, g2.y, g2.z, g2.w, 0u};
+    const uint32_t d = y >> 2;
+    uint32_t lo = w[0], hi = w[1];
+#pragma unroll
+    for (int k = 1; k < 12; ++k) {
+        lo = d == (uint32_t)k ? w[k] : lo;
+        hi = d == (uint32_t)k ? w[k + 1] : hi;
+    }
+    return __builtin_amdgcn_alignbyte(hi, lo, y & 3u);
+}
+
+// sums run `run` from its stage and stores its 64 results
+__device__ __forceinline__ void tiny_finish(const SliceArgs& a, const TinyStage& s, uint64_t run, int lane) {
+    const int sh = (int)(s.off & 15);
+    const int e = sh + (int)s.len;
+    const uint32_t nneed = s.len ? (uint32_t)((e + 15) >> 4) : 0u;
+    const bool small = nneed <= (uint32_t)kTinyGranules;
+#ifdef PNET_TINY_AB_NOCHUNK   // A/B: whole granules only (wrong sums: the VALU cost of the edges)
+    uint32_t acc = granule_sum(s.v[1], granule_sum(s.v[0], 0u));
+#else
+    uint32_t acc = chunk_sum(s.v[0], s.v[1], s.v[2], make_uint4(0, 0, 0, 0), 0, sh, e, nneed,
+                             __ballot(nneed > 2u) == 0ull);
+#endif
+    // skipped word: its bytes [2 skip, 2 skip + 2) that lie in the slice
+    // (util.rs:166-178), from the granules (a small slice's lie in them)
+    const uint64_t q = 2ull * s.skip;
+    const bool s0 = q < s.len, s1 = q + 1 < s.len;
+#ifdef PNET_TINY_AB_NOWINDOW   // A/B: no skipped-word extraction (wrong sums)
+    uint32_t pair = s.v[0].x;
+#else
+    uint32_t pair = window_bytes(s.v[0], s.v[1], s.v[2], small && s0 ? (uint32_t)sh + (uint32_t)q : 0u);
+#endif
+    if (__ballot(!small)) {   // wave-uniform: a run with longer slices
+        // up to kTinyLaneGranules granules: the slice's own lane goes on from
+        // the 3 granules it holds (summed whole above), 4 more per round
+        if (!small && nneed <= (uint32_t)kTinyLaneGranules) {
+            const uint8_t* fb = a.data + (s.off - (uint64_t)sh);
+            for (uint32_t c0 = kTinyGranules; c0 < nneed; c0 += 4) {
+                uint4 g[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    g[k] = c0 + k < nneed ? load16(fb + 16u * (c0 + k)) : make_uint4(0, 0, 0, 0);
+                acc += chunk_sum(g[0], g[1], g[2], g[3], (int)c0, sh, e, nneed, false);
+            }
+        }
+        // longer ones: the whole wave per slice (wave-uniform loop)
+        for (uint64_t big = __ballot(nneed > (uint32_t)kTinyLaneGranules); big; big &= big - 1) {
+            const int sl = __builtin_ctzll(big);
+            const uint64_t soff = (uint64_t)__shfl((unsigned long long)s.off, sl);
+            const uint32_t slen = (uint32_t)__shfl((int)s.len, sl);
+            const uint32_t t = group_range_sum<kWave, 1>(a.data, soff, slen, lane);
+            if (lane == sl) acc = t;
+        }
+        if (!small && s0) pair = a.data[s.off + q] | (s1 ? (uint32_t)a.data[s.off + q + 1] << 8 : 0u);
+    }
+    const uint32_t sw = s0 ? pair & (s1 ? 0xFFFFu : 0xFFu) : 0u;   // b0 at byte weight 1, b1 at 256
+    acc -= ((s.off + q) & 1) ? bswap16(sw) : sw;                    // odd address: the weights swap
+    uint32_t p = fold16(acc);
+    if (!(s.off & 1)) p = bswap16(p);
+    if (s.in) a.out[run * kWave + (uint64_t)lane] = (uint16_t)(s.len ? ((~p) & 0xFFFFu) : 0u);   // util.rs:76-82
+}
+
+// a wave-uniform 64-bit value in scalar registers (so that loop conditions on
+// it are scalar branches, not exec-mask updates)
+__device__ __forceinline__ uint64_t uniform64(uint64_t x) {
+    return ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(x >> 32)) << 32) |
+           (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)x);
+}
+
+#ifndef PNET_TINY_MINWAVES
+#define PNET_TINY_MINWAVES 1   // A/B: waves per SIMD the register allocation must allow
+#endif
+template <bool COMPACT>
+__global__ __launch_bounds__(kBlock, PNET_TINY_MINWAVES) void slice_tiny_kernel(SliceArgs a) {
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wv = threadIdx.x / kWave;
+    const uint64_t nruns = (a.n + kWave - 1) / kWave;
+    RunQueue q(a.sched, nruns, (uint64_t)blockIdx.x * kWavesPerBlock + wv, (uint64_t)gridDim.x * kWavesPerBlock);
+    // Takes are monotone: once one returns >= nruns, so do all later ones.
+    // Unrolled by two so that the stages alternate between two register sets:
+    // a stage is issued while the other is summed, and the one summed dies
+    // before the next is issued into its registers (a single-step loop copies
+    // the new stage over the old at its back edge, and a copy of a register a
+    // load has not filled yet waits for that load).
+    // The prologue issues in the loop's order (ry's descriptors before rx's
+    // granules), so that the waits the compiler derives for the loop hold for
+    // its first pass too and need not be conservative.
+    uint64_t rx = uniform64(q.take());
+    const TinyDesc dx = tiny_desc<COMPACT>(a, rx, nruns, lane);
+    uint64_t ry = uniform64(q.take());
+    TinyDesc dy = tiny_desc<COMPACT>(a, ry, nruns, lane);
+    TinyStage sx = tiny_issue<COMPACT>(a, dx);
+    while (rx < nruns) {
+        const uint64_t rz = uniform64(q.take());
+        const TinyDesc dz = tiny_desc<COMPACT>(a, rz, nruns, lane);   // in flight for two runs
+        const TinyStage sy = tiny_issue<COMPACT>(a, dy);                        // in flight while rx is summed
+        tiny_finish(a, sx, rx, lane);
+        if (ry >= nruns) break;
+        const uint64_t rw = uniform64(q.take());
+        dy = tiny_desc<COMPACT>(a, rw, nruns, lane);
+        sx = tiny_issue<COMPACT>(a, dz);
+        tiny_finish(a, sy, ry, lane);
+        rx = rz;
+        ry = rw;
+    }
+}
+
 // slice_strided_kernel: util::checksum over uniform slices, slice i = [first +
 // i * stride, +slice_len) with stride and slice_len at most 64 B (the
 // reference's own bench shape: 20-B slices, checksum_benchmarks.rs:8-12, here

@@ -103,7 +103,7 @@ def column_bytes(columns):
 
 #: tuning keys of pnetgpu_ctx_set_tuning (PNETGPU_TUNE_<NAME>), by lower-case name
 TUNING_KEYS = {k[len("PNETGPU_TUNE_"):].lower(): v for k, v in DEFS.items() if k.startswith("PNETGPU_TUNE_")}
-_SLICE_KERNELS = {"run": 1, "group": 2}
+_SLICE_KERNELS = {"run": 1, "group": 2, "tiny": 3}
 
 
 class Context:
@@ -118,7 +118,7 @@ class Context:
     def set_tuning(self, name, value):
         """pnetgpu_ctx_set_tuning: override a kernel default on this context
         (name: a TUNING_KEYS key, e.g. "static_pct"; value None or -1 restores
-        the default; slice_kernel also takes "run" / "group")."""
+        the default; slice_kernel also takes "run" / "group" / "tiny")."""
         if name not in TUNING_KEYS:
             raise KeyError(f"unknown tuning key {name!r} (one of {sorted(TUNING_KEYS)})")
         v = -1 if value is None else _SLICE_KERNELS.get(value, value)
@@ -289,8 +289,9 @@ _I64, _I32, _U8 = (torch.int64, torch.uint64), (torch.int32, torch.uint32), (tor
 
 
 def last_rx_kernel():
-    """The receive kernel instantiation the calling thread's last rx_process /
-    tx_fill_checksums launched, named as rocprofv3 names it (pnetgpu_last_rx_kernel)."""
+    """The kernel instantiation the calling thread's last rx_process /
+    tx_fill_checksums / *_slices call launched, named as rocprofv3 names it
+    (pnetgpu_last_rx_kernel)."""
     return lib.pnetgpu_last_rx_kernel().decode()
 
 

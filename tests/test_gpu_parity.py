@@ -424,9 +424,9 @@ def test_idempotent_and_stream_ordered():
         assert torch.equal(a.columns[c], b.columns[c])
 
 
-@pytest.mark.parametrize("kernel", ["run", "group"])
+@pytest.mark.parametrize("kernel", ["run", "group", "tiny"])
 def test_random_slices_vs_oracle(kernel, tune):
-    tune("slice_kernel", kernel)   # slice_run_kernel / slice_kernel
+    tune("slice_kernel", kernel)   # slice_run_kernel / slice_kernel / slice_tiny_kernel (util::checksum)
     rng = np.random.default_rng(21)
     n = 20000
     buf = rng.integers(0, 256, 1 << 22, dtype=np.uint8)
@@ -451,7 +451,7 @@ def test_random_slices_vs_oracle(kernel, tune):
                                  int(protos[i])), i
 
 
-@pytest.mark.parametrize("kernel", ["run", "group"])
+@pytest.mark.parametrize("kernel", ["run", "group", "tiny"])
 @pytest.mark.parametrize("seed", [0, 1])
 def test_small_and_large_slices_mixed_in_runs(seed, kernel, tune):
     """slice_run_kernel: tiny slices (0-70 B, summed by their own lane) and long
@@ -819,7 +819,7 @@ def test_compact_slices_kats_and_random_vs_oracle():
     want = coracle.checksum_slices(buf, offs, lens, skips)
     desc = lp.slice_descriptors(offs, lens, skips, device=DEV)
     d = to_dev(np.concatenate([buf, np.zeros(32, np.uint8)]))[: buf.size]
-    for kern in ("run", "group"):
+    for kern in ("run", "group", "tiny"):
         with lp.engine.tuning(0, slice_kernel=kern):
             got = lp.checksum_slices_compact(d, desc).cpu().numpy().view(np.uint16)
         assert np.array_equal(got, want), kern
@@ -897,8 +897,9 @@ def test_dense_runs_of_packed_slices(seed, span, tune):
                                  int(protos[i])), (alen, i)
 
 
+@pytest.mark.parametrize("kernel", ["run", "tiny"])
 @pytest.mark.parametrize("seed", [0, 1, 2])
-def test_runs_of_small_slices_vs_oracle(seed, tune):
+def test_runs_of_small_slices_vs_oracle(seed, kernel, tune):
     """slice_run_kernel on runs whose 64 slices are all small (each summed by its
     own lane): short slices at every alignment with the skipped word inside /
     straddling / past the slice, empty and out-of-bounds descriptors, batch
@@ -906,8 +907,9 @@ def test_runs_of_small_slices_vs_oracle(seed, tune):
     hundred slices (its run takes the group path), and packed 64-B runs (dense)
     between them; 16-B and compact descriptors, against the oracle. (Written
     for a two-runs-at-once variant, measured slower and not kept:
-    profiles/r03/slices/ab_run_pairs.txt.)"""
-    tune("slice_kernel", "run")
+    profiles/r03/slices/ab_run_pairs.txt.) slice_tiny_kernel too: its own
+    lanes sum slices of at most 3 granules, the long ones go to its wave loop."""
+    tune("slice_kernel", kernel)
     rng = np.random.default_rng(900 + seed)
     n = 64 * (201 + 2 * seed) + 13 + seed
     buf = rng.integers(0, 256, 1 << 21, dtype=np.uint8)
@@ -937,6 +939,54 @@ def test_runs_of_small_slices_vs_oracle(seed, tune):
     c_len = np.where((co > buf.size) | (co + cl > buf.size), 0, cl).astype(np.uint32)
     want_c = coracle.checksum_slices(buf, np.where(co > buf.size, 0, co), c_len, cs.astype(np.uint32))
     assert np.array_equal(got, want_c)
+
+
+@pytest.mark.parametrize("compact", [False, True])
+def test_tiny_kernel_reference_shape_and_choice(compact):
+    """slice_tiny_kernel (software-pipelined runs of 64 slices): the reference's
+    20-B util::checksum bench shape (checksum_benchmarks.rs:8-12) packed back
+    to back with random bytes, skipword 5, at every start alignment, with a
+    ragged last run, through the default choice (<= 32 buffer bytes per slice
+    takes the tiny kernel: pnetgpu_last_rx_kernel names it); then slices of
+    0..33 B at any alignment with the skipped word anywhere (its two bytes
+    read from the granule registers: inside, straddling the end, past it),
+    each slice's neighbours overlapping, and a few long slices (the wave loop)
+    in a buffer still <= 32 B per slice. Against the oracle."""
+    rng = np.random.default_rng(31 + compact)
+    for first in (0, 1, 7, 15):
+        n = 64 * 411 + 37
+        buf = rng.integers(0, 256, first + 20 * n, dtype=np.uint8)
+        offs = first + 20 * np.arange(n, dtype=np.uint64)
+        lens = np.full(n, 20, np.uint32)
+        skips = np.full(n, 5, np.uint32)
+        want = coracle.checksum_slices(buf, offs, lens, skips)
+        d = to_dev(np.concatenate([buf, np.zeros(32, np.uint8)]))[: buf.size]
+        if compact:
+            got = lp.checksum_slices_compact(d, lp.slice_descriptors(offs, lens, skips, device=DEV))
+        else:
+            got = lp.checksum_slices(d, to_dev(offs.astype(np.int64)), to_dev(lens.astype(np.int32)),
+                                     to_dev(skips.astype(np.int32)))
+        assert lp.last_rx_kernel() == f"slice_tiny_kernel<{'true' if compact else 'false'}>"
+        assert np.array_equal(got.cpu().numpy().view(np.uint16), want), first
+    n = 64 * 700 + 5
+    buf = rng.integers(0, 256, 32 * n, dtype=np.uint8)
+    lens = rng.integers(0, 34, n).astype(np.uint32)
+    offs = rng.integers(0, buf.size - 6000, n).astype(np.uint64)
+    skips = np.where(rng.random(n) < 0.8, rng.integers(0, 18, n), rng.integers(0, 70000, n)).astype(np.uint32)
+    big = rng.choice(n, 40, replace=False)
+    lens[big] = rng.integers(34, 5000, big.size)
+    skips[big[:20]] = rng.integers(0, 2500, 20)
+    if compact:
+        skips = np.minimum(skips, 0xFFFF)
+    want = coracle.checksum_slices(buf, offs, lens, skips)
+    d = to_dev(buf)
+    if compact:
+        got = lp.checksum_slices_compact(d, lp.slice_descriptors(offs, lens, skips, device=DEV))
+    else:
+        got = lp.checksum_slices(d, to_dev(offs.astype(np.int64)), to_dev(lens.astype(np.int32)),
+                                 to_dev(skips.astype(np.int32)))
+    assert lp.last_rx_kernel().startswith("slice_tiny_kernel")
+    assert np.array_equal(got.cpu().numpy().view(np.uint16), want)
 
 
 def run_desc_form(buf, offs, lens, compact, columns=RECORD_COLUMNS):
