@@ -612,6 +612,7 @@ def refshapes_block(steps, warmup, device):
         res = {}
         ms = time_launches(lambda s: res.__setitem__("o", lp.checksum_slices(d, do, dl, ds, stream=s)), steps, warmup,
                            stream)
+        kern = lp.last_rx_kernel()
         got = res["o"].cpu().numpy().view(np.uint16)
         want = coracle.checksum(bytes([fill] * size), 5)
         alg = n * (size + 16 + 2)
@@ -626,23 +627,25 @@ def refshapes_block(steps, warmup, device):
         dc = lp.slice_descriptors(offs, lens, skips, device=device)
         ms_c = time_launches(lambda s: res.__setitem__("c", lp.checksum_slices_compact(d, dc, stream=s)),
                              steps, warmup, stream)
+        kern_c = lp.last_rx_kernel()
         got_c = res["c"].cpu().numpy().view(np.uint16)
         alg_c = n * (size + 8 + 2)
         compact = {"kernel_avg_ms": round(ms_c, 4), "mslices_s": round(n / (ms_c * 1e-3) / 1e6, 1),
                    "achieved_gbs": round(alg_c / (ms_c * 1e-3) / 1e9, 1),
                    "frac": round(alg_c / (ms_c * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                   "parity": bool((got_c == want).all()), "alg_bytes_per_slice": size + 8 + 2}
+                   "parity": bool((got_c == want).all()), "alg_bytes_per_slice": size + 8 + 2, "kernel": kern_c}
         del dc
         # the same slices without descriptor arrays (pnetgpu_checksum_slices_strided)
         ms_st = time_launches(lambda s: res.__setitem__("s", lp.checksum_slices_strided(d, n, size, size, 5, stream=s)),
                               steps, warmup, stream)
+        kern_st = lp.last_rx_kernel()
         got_st = res["s"].cpu().numpy().view(np.uint16)
         alg_st = n * (size + 2)
         strided = {"kernel_avg_ms": round(ms_st, 4), "mslices_s": round(n / (ms_st * 1e-3) / 1e6, 1),
                    "achieved_gbs": round(alg_st / (ms_st * 1e-3) / 1e9, 1),
                    "frac": round(alg_st / (ms_st * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                   "parity": bool((got_st == want).all()), "alg_bytes_per_slice": size + 2}
-        out[name] = {"slices": n, "slice_bytes": size, "skipword": 5, "kernel_avg_ms": round(ms, 4),
+                   "parity": bool((got_st == want).all()), "alg_bytes_per_slice": size + 2, "kernel": kern_st}
+        out[name] = {"slices": n, "slice_bytes": size, "skipword": 5, "kernel": kern, "kernel_avg_ms": round(ms, 4),
                      "mslices_s": round(n / (ms * 1e-3) / 1e6, 1),
                      "achieved_gbs": round(alg / (ms * 1e-3) / 1e9, 1),
                      "frac": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
