@@ -11,8 +11,8 @@
 #   smoke                      __graft_entry__.smoke()
 #   bench[:W,W...]             bench.py (default workloads, or --workloads W,.. --no-extra)
 #   profile[:W+W...]           tools/profile_round.sh (rocprofv3 stats + PMC) for those workloads
-#   variant:V:K                tests/test_gpu_parity.py -k K on libpnetgpu_V.so (PNETGPU_LIB)
-#   ab:W:ROUNDS:V+V...         tools/abvar.sh interleaved A/B of library variants
+#   variant:V:K[:FILE+FILE]    tests/test_gpu_parity.py (or FILEs) -k K on libpnetgpu_V.so (PNETGPU_LIB)
+#   ab:W:ROUNDS:V+V...         tools/abvar.sh interleaved A/B of library variants (KB_ARGS passes through)
 #   e2e:W:SLOTS                tools/e2e_slots.py (ring slot sweep, e.g. 3,4,6)
 #   py:SCRIPT[:ARGS]           python -u SCRIPT ARGS ('+' for spaces), output in the step log
 set -o pipefail
@@ -36,8 +36,8 @@ for S in "$@"; do
              timeout -k 10 600 python -u bench.py > $O/bench.json 2> $L
            fi ;;
     profile) WLS="${A1//+/ }" timeout -k 10 900 bash tools/profile_round.sh $TAG > $L 2>&1 ;;
-    variant) PNETGPU_LIB=$R/libpnet_amd/build/libpnetgpu_$A1.so timeout -k 10 400 \
-               $PYT tests/test_gpu_parity.py -k "$A2" > $L 2>&1 ;;
+    variant) A3=${A3//+/ }; PNETGPU_LIB=$R/libpnet_amd/build/libpnetgpu_$A1.so timeout -k 10 400 \
+               $PYT ${A3:-tests/test_gpu_parity.py} -k "$A2" > $L 2>&1 ;;
     ab) timeout -k 10 1200 bash tools/abvar.sh $A1 $A2 ${A3//+/ } > $L 2>&1 ;;
     e2e) timeout -k 10 400 python -u tools/e2e_slots.py --workload $A1 --slots $A2 > $O/e2e_$A1.json 2> $L ;;
     py) timeout -k 10 600 python -u $A1 ${A2//+/ } > $L 2>&1 ;;
