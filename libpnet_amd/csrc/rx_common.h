@@ -653,6 +653,44 @@ __device__ __forceinline__ void store_columns(const pnetgpu_rx_columns& C, uint6
     }
 }
 
+// A frame's record packed in 8 dwords, for stores deferred past later runs
+// (rx_kernel, PNET_DEFER): every column of store_columns except the IPv6
+// address columns (read from the LDS slot at store time).
+struct Rec {
+    uint32_t w[8];
+};
+__device__ __forceinline__ Rec pack_rec(const Parsed& P, uint32_t ipc, uint32_t l4c) {
+    Rec r;
+    r.w[0] = (P.st & 0xFFFFu) | (ipc << 16);
+    r.w[1] = (l4c & 0xFFFFu) | (P.et << 16);
+    r.w[2] = (P.proto & 0xFFu) | ((P.ttl & 0xFFu) << 8) | (P.l4off << 16);
+    r.w[3] = (P.l4len & 0xFFFFu) | (P.sp << 16);
+    r.w[4] = (P.dp & 0xFFFFu) | (P.vlan_tci << 16);
+    r.w[5] = P.s4;
+    r.w[6] = P.d4;
+    r.w[7] = P.l3;
+    return r;
+}
+__device__ __forceinline__ void store_rec(const pnetgpu_rx_columns& C, uint64_t f0, int lane, bool in_batch,
+                                          const Rec& r) {
+    if (!in_batch) return;
+    const uint64_t i = opaque_index(f0 + (uint64_t)lane);
+    if (C.status) put<uint16_t>(C.status, i, (uint16_t)r.w[0]);
+    if (C.ip_csum) put<uint16_t>(C.ip_csum, i, (uint16_t)(r.w[0] >> 16));
+    if (C.l4_csum) put<uint16_t>(C.l4_csum, i, (uint16_t)r.w[1]);
+    if (C.ethertype) put<uint16_t>(C.ethertype, i, (uint16_t)(r.w[1] >> 16));
+    if (C.ip_proto) put<uint8_t>(C.ip_proto, i, (uint8_t)r.w[2]);
+    if (C.ttl) put<uint8_t>(C.ttl, i, (uint8_t)(r.w[2] >> 8));
+    if (C.l4_offset) put<uint16_t>(C.l4_offset, i, (uint16_t)(r.w[2] >> 16));
+    if (C.l4_length) put<uint16_t>(C.l4_length, i, (uint16_t)r.w[3]);
+    if (C.src_port) put<uint16_t>(C.src_port, i, (uint16_t)(r.w[3] >> 16));
+    if (C.dst_port) put<uint16_t>(C.dst_port, i, (uint16_t)r.w[4]);
+    if (C.src_ipv4) put<uint32_t>(C.src_ipv4, i, r.w[5]);
+    if (C.dst_ipv4) put<uint32_t>(C.dst_ipv4, i, r.w[6]);
+    if (C.vlan_tci) put<uint16_t>(C.vlan_tci, i, (uint16_t)(r.w[4] >> 16));
+    if (C.l3_offset) put<uint8_t>(C.l3_offset, i, (uint8_t)r.w[7]);
+}
+
 // Header-field columns (ABI v3): the remaining generated getters of the views
 // the dispatch constructed, read from the frame's bytes (LDS window, or HBM past
 // it) only for the columns a caller requested; 0 for a view that was not

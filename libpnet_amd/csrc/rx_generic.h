@@ -173,6 +173,9 @@ __device__ __forceinline__ void tail_sums(const uint8_t* data, WaveLds<NW>& L, i
 #ifndef PNET_SHORT_RUNS
 #define PNET_SHORT_RUNS 1   // A/B: short-run fast path in the mixed shape
 #endif
+#ifndef PNET_DEFER
+#define PNET_DEFER 3   // runs whose records the unified (MTU) shape holds back (A/B: 0 = store each run's at once)
+#endif
 template <int NW, int G, int U, bool NT, int PASS, bool DYN, bool EXT, bool TX>
 __global__ __launch_bounds__(kBlock, NW < 8 ? 5 : 4) void rx_kernel(RxArgs a) {
     // the window must hold every field the parse reads near (Ethernet + 2 VLAN
@@ -217,6 +220,20 @@ __global__ __launch_bounds__(kBlock, NW < 8 ? 5 : 4) void rx_kernel(RxArgs a) {
     PNET_WT_BEGIN;
     uint32_t run_count = 0;
     (void)run_count;
+    // Deferred record stores (PNET_DEFER): a small write stream inside a read
+    // stream costs out of proportion to its bytes; the unified shape
+    // keeps the last kDefer runs' records in registers (8 dwords per run) and
+    // stores a run's record only when a newer one needs its place, or at the
+    // wave's end - with the MTU shape's few runs per wave (4 at 2^20 frames),
+    // the record stores of a launch then go out together at its end instead
+    // of between reads. 1500-B batches -1.6 % at 3 runs (128 VGPRs, still 4
+    // waves/SIMD); 1 or 2 runs measured even (profiles/r05/defer/).
+    constexpr int kDefer = (PNET_DEFER > 0 && PASS == 1 && !EXT && !TX) ? PNET_DEFER : 0;
+    constexpr int kDq = kDefer > 0 ? kDefer : 1;
+    const bool defer = kDefer > 0 && !a.cols.src_ipv6 && !a.cols.dst_ipv6;
+    Rec dq[kDq];
+    uint64_t dqf[kDq];
+    int dqn = 0;
     RunQueue q(a.sched, a.nruns, (uint64_t)blockIdx.x * kWavesPerBlock + wv, wave_stride);
     uint64_t run = q.take();
     fetch_desc(run);
@@ -380,7 +397,20 @@ __global__ __launch_bounds__(kBlock, NW < 8 ? 5 : 4) void rx_kernel(RxArgs a) {
             else
                 tx_write(const_cast<uint8_t*>(a.data) + off, P, ipc, l4c);
         }
-        store_columns(a.cols, f0, lane, in_batch, P, ipc, l4c, slot, sh);
+        if (kDefer > 0 && defer) {
+            const Rec cur = pack_rec(P, ipc, l4c);
+            if (dqn == kDefer) store_rec(a.cols, dqf[kDq - 1], lane, dqf[kDq - 1] + lane < a.n, dq[kDq - 1]);
+#pragma unroll
+            for (int k = kDq - 1; k > 0; --k) {
+                dq[k] = dq[k - 1];
+                dqf[k] = dqf[k - 1];
+            }
+            dq[0] = cur;
+            dqf[0] = f0;
+            dqn = dqn < kDefer ? dqn + 1 : kDefer;
+        } else {
+            store_columns(a.cols, f0, lane, in_batch, P, ipc, l4c, slot, sh);
+        }
 #ifndef PNET_NO_FIELD_COLUMNS   // A/B: the header-field stores compiled out
         if (EXT && a.field_cols && in_batch)   // header-field columns: EXT instantiations only
             store_field_columns(a.cols, f0 + lane, P, FrameBytes{slot + sh, a.data + off, kWin - sh}, EXT && a.l3mode);
@@ -389,6 +419,11 @@ __global__ __launch_bounds__(kBlock, NW < 8 ? 5 : 4) void rx_kernel(RxArgs a) {
         wave_sync();   // slots and lists are rewritten by the next run
         PNET_PH(3);   // probe: stores, counters
         run = nrun;
+    }
+    if (kDefer > 0) {
+#pragma unroll
+        for (int k = 0; k < kDq; ++k)
+            if (k < dqn) store_rec(a.cols, dqf[k], lane, dqf[k] + lane < a.n, dq[k]);
     }
     if (a.cols.counters) K.flush(a.cols.counters, blk_ctr, wv, lane);
     PNET_WT_END((uint64_t)blockIdx.x * kWavesPerBlock + wv);

@@ -7,7 +7,7 @@
 #
 # STEP is one of
 #   suite                      the whole GPU suite (pytest -m gpu)
-#   tests:FILE[+FILE...][:K]   those test files, -m gpu, optionally -k K
+#   tests:FILE[+FILE...][:K]   those test files, -m gpu, optionally -k K ('+' for spaces)
 #   smoke                      __graft_entry__.smoke()
 #   bench[:W,W...]             bench.py (default workloads, or --workloads W,.. --no-extra)
 #   profile[:W+W...]           tools/profile_round.sh (rocprofv3 stats + PMC) for those workloads
@@ -28,7 +28,7 @@ for S in "$@"; do
   L=$O/$(printf %02d $n)_$K.log
   case $K in
     suite) timeout -k 10 900 $PYT tests -m gpu > $L 2>&1 ;;
-    tests) timeout -k 10 600 $PYT ${A1//+/ } -m gpu ${A2:+-k "$A2"} > $L 2>&1 ;;
+    tests) A2=${A2//+/ }; timeout -k 10 600 $PYT ${A1//+/ } -m gpu ${A2:+-k "$A2"} > $L 2>&1 ;;
     smoke) timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > $L 2>&1 ;;
     bench) if [ -n "$A1" ]; then
              timeout -k 10 500 python -u bench.py --workloads $A1 --no-extra > $O/bench_$n.json 2> $L
@@ -36,7 +36,7 @@ for S in "$@"; do
              timeout -k 10 600 python -u bench.py > $O/bench.json 2> $L
            fi ;;
     profile) WLS="${A1//+/ }" timeout -k 10 900 bash tools/profile_round.sh $TAG > $L 2>&1 ;;
-    variant) A3=${A3//+/ }; PNETGPU_LIB=$R/libpnet_amd/build/libpnetgpu_$A1.so timeout -k 10 400 \
+    variant) A2=${A2//+/ }; A3=${A3//+/ }; PNETGPU_LIB=$R/libpnet_amd/build/libpnetgpu_$A1.so timeout -k 10 400 \
                $PYT ${A3:-tests/test_gpu_parity.py} -k "$A2" > $L 2>&1 ;;
     ab) timeout -k 10 1200 bash tools/abvar.sh $A1 $A2 ${A3//+/ } > $L 2>&1 ;;
     e2e) timeout -k 10 400 python -u tools/e2e_slots.py --workload $A1 --slots $A2 > $O/e2e_$A1.json 2> $L ;;
