@@ -490,8 +490,15 @@ int pnetgpu_ring_submit_region(pnetgpu_ring* r, const uint8_t* base, const uint6
     s.n_large = large;
     s.jumbo_bytes = jumbo;
     s.frames_view = base + o0;
+    const int rc = ship_slot(r, s, base + o0, id);
+    if (rc) {   // nothing shipped: the slot is empty again (its pinned batch never held these frames)
+        s.n = 0;
+        s.bytes = s.frame_bytes = s.n_large = s.jumbo_bytes = 0;
+        s.max_len = 0;
+        return rc;
+    }
     *taken = k;
-    return ship_slot(r, s, base + o0, id);
+    return PNETGPU_OK;
 }
 static void release_held(pnetgpu_ring* r) {
     if (r->held >= 0) {
@@ -513,9 +520,10 @@ int pnetgpu_ring_wait(pnetgpu_ring* r, pnetgpu_ring_batch* out) {
     release_held(r);                             // the previous batch is released now
     if (r->inflight.empty()) return PNETGPU_EEMPTY;
     const int i = r->inflight.front();
-    r->inflight.pop_front();
     Slot& s = r->slots[i];
+    // a failed wait leaves the batch in flight (the next wait tries it again)
     if (const hipError_t e = hipEventSynchronize(s.done)) return pnetgpu::hip_fail(e);
+    r->inflight.pop_front();
     s.state = kHeld;
     r->held = i;
     out->id = s.id;
