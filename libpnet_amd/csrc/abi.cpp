@@ -147,8 +147,8 @@ int plan_sched(pnetgpu_ctx* ctx, uint64_t nunits, uint64_t nwaves, void* stream,
     s->seq = ctx->seq[b];
     const int64_t tn = tuning(ctx, PNETGPU_TUNE_CLAIM_COUNTERS);
     const uint64_t nctr = tn > 0 ? (uint64_t)tn : PNET_CLAIM_COUNTERS;
-    // every counter needs home waves: wave ids [0, 32 nctr) cover them all
-    const uint64_t homes = std::max<uint64_t>(1, nwaves / 32);
+    // every counter needs home waves: wave ids [0, kClaimChunk nctr) cover them all
+    const uint64_t homes = std::max<uint64_t>(1, nwaves / pnetgpu::kClaimChunk);
     s->nctr = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>({nctr, kMaxCtrs, homes}));
     s->ctr_stride = (uint32_t)kCtrStride;
     return PNETGPU_OK;

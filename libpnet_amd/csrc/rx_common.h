@@ -118,9 +118,9 @@ __device__ __forceinline__ void rotate_prio(uint32_t step) {
 
 // The runs one wave processes (RxArgs::sched): its grid-stride share of
 // [0, nstatic), then runs claimed from one of the launch's nctr counters (the
-// wave's home counter, (wave id / 32) % nctr, owns an equal slice of
-// [nstatic, nruns); 32 consecutive wave ids are 8 blocks, which the dispatcher
-// spreads over the 8 XCDs, so every counter balances work across them),
+// wave's home counter, (wave id / kClaimChunk) % nctr, owns an equal slice of
+// [nstatic, nruns); its group holds waves of every dispatch round, so every
+// counter's group runs at the same mean speed: rx_internal.h),
 // one claim kept in flight ahead of its use so the atomic's round trip
 // overlaps a whole run: claim() issues the atomic, and its value is read
 // (and waited for) only at the next take(). take() returns the next run;
@@ -142,15 +142,17 @@ struct RunQueue {
           hi(0), ctr(s.ctr), pend(n_units), kraw(0), gwaves(0), inflight(false), finished(false),
           groups_done(s.groups_done), done_host(s.done_host), seq(s.seq), ngroups(0) {
         if (ctr) {
-            const uint64_t h = (wave_id >> 5) % s.nctr, d = nruns - nstatic;
+            const uint64_t h = (wave_id / kClaimChunk) % s.nctr, d = nruns - nstatic;
             lo = nstatic + d * h / s.nctr;
             hi = nstatic + d * (h + 1) / s.nctr;
             ctr += h * s.ctr_stride;
-            // the group's size: 32-wave chunks c < ceil(W / 32) with c % nctr == h,
-            // the last chunk holding W % 32 waves when W is not a multiple of 32
-            const uint64_t nch = (wave_stride + 31) / 32, full = wave_stride / 32, rem = wave_stride % 32;
-            uint64_t g = h < nch ? ((nch - 1 - h) / s.nctr + 1) * 32 : 0;
-            if (rem && full % s.nctr == h) g -= 32 - rem;
+            // the group's size: kClaimChunk-wave chunks c < ceil(W / kClaimChunk)
+            // with c % nctr == h, the last chunk holding W % kClaimChunk waves
+            // when W is not a multiple of kClaimChunk
+            constexpr uint64_t C = kClaimChunk;
+            const uint64_t nch = (wave_stride + C - 1) / C, full = wave_stride / C, rem = wave_stride % C;
+            uint64_t g = h < nch ? ((nch - 1 - h) / s.nctr + 1) * C : 0;
+            if (rem && full % s.nctr == h) g -= C - rem;
             gwaves = (uint32_t)g;
             // groups that have waves (all nctr when the host sized nctr from this
             // grid, as plan_sched does): the last of them hands the block back
