@@ -119,8 +119,8 @@ int ng_block(NgState& st, uint32_t type, const uint8_t* body, uint32_t body_len,
 // block boundary, or img_bytes).
 template <class F>
 int ng_walk(const uint8_t* img, uint64_t img_bytes, uint64_t from, uint64_t cap, bool want_info, NgState& st,
-            uint64_t* next, F fn) {
-    uint64_t p = 0, taken = 0;
+            uint64_t* next, F fn, uint64_t start = 0) {
+    uint64_t p = start, taken = 0;
     while (p < img_bytes) {
         if (img_bytes - p < 12) return PNETGPU_EFORMAT;              // truncated block header
         const uint32_t type = rd32(img + p, st.swap);
@@ -156,6 +156,18 @@ int ng_walk(const uint8_t* img, uint64_t img_bytes, uint64_t from, uint64_t cap,
     *next = img_bytes;
     return want_info && !st.have_linktype ? PNETGPU_EFORMAT : PNETGPU_OK;
 }
+
+// The state a pcapng scan stopped with, so that the next call of a scan in
+// batches (*pos = where the previous call stopped, same image) resumes there
+// instead of walking the block headers from byte 0 again (which made a scan of
+// n packets in batches of k cost n^2 / k block reads). Per thread: a scan's
+// calls come from one thread; any other call walks from byte 0 as before.
+struct NgResume {
+    const uint8_t* img = nullptr;
+    uint64_t img_bytes = 0, pos = 0;
+    NgState st;
+};
+thread_local NgResume g_resume;
 
 // Classic pcap global header of an in-memory image: byte order and link type.
 int classic_header(const uint8_t* img, uint64_t img_bytes, bool* swap, uint32_t* linktype) {
@@ -289,14 +301,24 @@ int pnetgpu_pcap_scan(const uint8_t* img, uint64_t img_bytes, uint64_t* pos, uin
         // the walk starts at byte 0 and takes packets from *pos on (block
         // headers only until then)
         NgState st;
+        uint64_t start = 0;
+        if (*pos && g_resume.img == img && g_resume.img_bytes == img_bytes && g_resume.pos == *pos) {
+            st = g_resume.st;     // *pos is a block boundary this thread's last scan of the image stopped at
+            start = *pos;
+        }
         uint64_t k = 0, next = 0;
         const int rc = ng_walk(img, img_bytes, *pos, cap, false, st, &next, [&](uint64_t off, uint32_t len) {
             offsets[k] = off;
             lengths[k] = len;
             ++k;
-        });
+        }, start);
+        g_resume.img = nullptr;
         if (rc) return rc;
         if (k && linktype_flags(st.linktype, &flags)) return PNETGPU_EFORMAT;
+        g_resume.img = img;
+        g_resume.img_bytes = img_bytes;
+        g_resume.pos = next;
+        g_resume.st = st;
         *n = k;
         *pos = next;
         return PNETGPU_OK;

@@ -148,3 +148,42 @@ def test_pcapng_rejects_malformed(tmp_path):
         q.write_bytes(data)
         with pytest.raises(PnetGpuError):
             list(lp.pcap_frames(q))
+
+
+def _scan(img, pos, cap):
+    import ctypes
+    from libpnet_amd._lib import check, lib
+    p, n = ctypes.c_uint64(pos), ctypes.c_uint64()
+    o, ln = np.empty(cap, np.uint64), np.empty(cap, np.uint32)
+    check(lib.pnetgpu_pcap_scan(ctypes.c_void_p(img.ctypes.data), img.nbytes, ctypes.byref(p),
+                                ctypes.c_void_p(o.ctypes.data), ctypes.c_void_p(ln.ctypes.data), cap,
+                                ctypes.byref(n)), "pnetgpu_pcap_scan")
+    return p.value, list(zip(o[:n.value].tolist(), ln[:n.value].tolist()))
+
+
+def test_pcapng_scan_resumes_and_restarts():
+    """A pcapng scan in batches resumes where the thread's previous call of the
+    same image stopped (no re-walk from byte 0); scans of two images interleaved,
+    and a scan restarted at an earlier block boundary, still see each position's
+    own section state (byte order, interfaces)."""
+    rng = np.random.default_rng(8)
+    fa = framegen.random_frames(rng, 120)
+    fb = framegen.random_frames(rng, 90)
+    a = np.frombuffer(pcapng_bytes(fa, big_endian=True, n_if=2, sections=3), np.uint8).copy()
+    b = np.frombuffer(pcapng_bytes(fb, big_endian=False, n_if=3, sections=2), np.uint8).copy()
+    want_a = list(zip(*[x.tolist() for x in lp.pcap_index(a, batch=1000)]))
+    want_b = list(zip(*[x.tolist() for x in lp.pcap_index(b, batch=1000)]))
+    got_a, got_b, pa, pb, stops = [], [], 0, 0, []
+    while pa < a.nbytes or pb < b.nbytes:
+        if pa < a.nbytes:
+            stops.append(pa)
+            pa, r = _scan(a, pa, 7)
+            got_a += r
+        if pb < b.nbytes:
+            pb, r = _scan(b, pb, 5)
+            got_b += r
+    assert got_a == want_a and got_b == want_b
+    # restarts at earlier stops of image a (not where the last call ended)
+    for s in stops[::-1][:6]:
+        _, r = _scan(a, s, 10 ** 6)
+        assert r == [x for x in want_a if x[0] >= s]
