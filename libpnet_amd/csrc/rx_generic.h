@@ -173,6 +173,9 @@ __device__ __forceinline__ void tail_sums(const uint8_t* data, WaveLds<NW>& L, i
 #ifndef PNET_SHORT_RUNS
 #define PNET_SHORT_RUNS 1   // A/B: short-run fast path in the mixed shape
 #endif
+#ifndef PNET_TX_DEFER
+#define PNET_TX_DEFER 3   // runs whose in-place TX writes the unified (MTU) shape holds back (A/B: 0)
+#endif
 #ifndef PNET_DEFER
 #define PNET_DEFER 3   // runs whose records the unified (MTU) shape holds back (A/B: 0 = store each run's at once)
 #endif
@@ -234,6 +237,27 @@ __global__ __launch_bounds__(kBlock, NW < 8 ? 5 : 4) void rx_kernel(RxArgs a) {
     Rec dq[kDq];
     uint64_t dqf[kDq];
     int dqn = 0;
+    // TX (PNET_TX_DEFER): the in-place checksum writes of the last kTxDefer
+    // runs held back the same way (frame offset, field positions, values: 4
+    // dwords per run): 1500-B TX fill -1 % at 3 runs, same box, three
+    // interleaved rounds (profiles/r05/defer/ab_tx_defer.txt)
+    constexpr int kTxDefer = (PNET_TX_DEFER > 0 && PASS == 1 && TX) ? PNET_TX_DEFER : 0;
+    constexpr int kTq = kTxDefer > 0 ? kTxDefer : 1;
+    uint64_t tqo[kTq];
+    uint32_t tqp[kTq], tqv[kTq];
+    int tqn = 0;
+    auto tx_flush = [&](uint64_t o, uint32_t pos, uint32_t v) {
+        uint8_t* fr = const_cast<uint8_t*>(a.data) + o;
+        const uint32_t ip = pos & 0xFFFFu, l4 = pos >> 16;
+        if (ip != 0xFFFFu) {
+            fr[ip] = (uint8_t)(v >> 8);
+            fr[ip + 1] = (uint8_t)v;
+        }
+        if (l4 != 0xFFFFu) {
+            fr[l4] = (uint8_t)(v >> 24);
+            fr[l4 + 1] = (uint8_t)(v >> 16);
+        }
+    };
     RunQueue q(a.sched, a.nruns, (uint64_t)blockIdx.x * kWavesPerBlock + wv, wave_stride);
     uint64_t run = q.take();
     fetch_desc(run);
@@ -391,7 +415,25 @@ __global__ __launch_bounds__(kBlock, NW < 8 ? 5 : 4) void rx_kernel(RxArgs a) {
             finalize(P, tA, tB, (off & 1) != 0, ipc, l4c);
         }
         PNET_PH(2);   // probe: parse, window sums, tail trims, finalize
-        if (TX && in_batch && !desc_bad) {
+        if (kTxDefer > 0) {
+            // field offsets fit 16 bits: they lie within the first ~8.4 KB of a frame
+            // (two VLAN tags, four IPv6 extension headers of at most 2 KB)
+            const bool v4 = TX && in_batch && !desc_bad && P.is_v4;
+            const bool l4 = TX && in_batch && !desc_bad && (P.st & PNET_ST_L4_CSUM_DONE);
+            const uint32_t pos = (v4 ? (P.l3 + 10u) & 0xFFFFu : 0xFFFFu) | ((l4 ? (uint32_t)P.l4csum_at : 0xFFFFu) << 16);
+            const uint32_t val = (ipc & 0xFFFFu) | (l4c << 16);
+            if (tqn == kTxDefer) tx_flush(tqo[kTq - 1], tqp[kTq - 1], tqv[kTq - 1]);
+#pragma unroll
+            for (int k = kTq - 1; k > 0; --k) {
+                tqo[k] = tqo[k - 1];
+                tqp[k] = tqp[k - 1];
+                tqv[k] = tqv[k - 1];
+            }
+            tqo[0] = off;
+            tqp[0] = pos;
+            tqv[0] = val;
+            tqn = tqn < kTxDefer ? tqn + 1 : kTxDefer;
+        } else if (TX && in_batch && !desc_bad) {
             if (PNET_TX_GRANULES)
                 tx_write_window(const_cast<uint8_t*>(a.data) + base, slot, sh, len, kWin, P, ipc, l4c);
             else
@@ -419,6 +461,11 @@ __global__ __launch_bounds__(kBlock, NW < 8 ? 5 : 4) void rx_kernel(RxArgs a) {
         wave_sync();   // slots and lists are rewritten by the next run
         PNET_PH(3);   // probe: stores, counters
         run = nrun;
+    }
+    if (kTxDefer > 0) {
+#pragma unroll
+        for (int k = 0; k < kTq; ++k)
+            if (k < tqn) tx_flush(tqo[k], tqp[k], tqv[k]);
     }
     if (kDefer > 0) {
 #pragma unroll
