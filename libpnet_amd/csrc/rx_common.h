@@ -119,8 +119,8 @@ __device__ __forceinline__ void rotate_prio(uint32_t step) {
 // The runs one wave processes (RxArgs::sched): its grid-stride share of
 // [0, nstatic), then runs claimed from one of the launch's nctr counters (the
 // wave's home counter, (wave id / kClaimChunk) % nctr, owns an equal slice of
-// [nstatic, nruns); its group holds waves of every dispatch round, so every
-// counter's group runs at the same mean speed: rx_internal.h),
+// [nstatic, nruns); kClaimChunk = 32 consecutive wave ids are 8 blocks, which
+// the dispatcher spreads over the 8 XCDs: rx_internal.h),
 // one claim kept in flight ahead of its use so the atomic's round trip
 // overlaps a whole run: claim() issues the atomic, and its value is read
 // (and waited for) only at the next take(). take() returns the next run;

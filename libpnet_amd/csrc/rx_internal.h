@@ -19,17 +19,17 @@ namespace pnetgpu {
 // `seq` to the pinned host word done_host, which frees the block for another
 // launch (the host reuses a block only once its word shows the seq it issued).
 // Waves per claim chunk: a counter's group is the chunks c with c % nctr == h.
-// A chunk of 16 waves is 4 consecutive blocks; the dispatcher places blocks
-// in rounds of one block per CU (256 blocks = 64 chunks per round), and a
-// round's waves are younger on their SIMDs than the previous round's and run
-// slower (4.37 vs 3.76 us per 64-B run from round 3 to round 0), so with 64
-// counters every group holds one chunk of each round and the groups run at
-// one speed. (32-wave chunks gave counters h < 32 rounds 0 + 2 and the rest
-// rounds 1 + 3: two group speeds, their median ends 251-265 us apart in a 64-B
-// launch; 16-wave chunks 254-261 us. The launch's end is set by its last few
-// blocks either way - kernel times even, profiles/r05/wave_ends/.)
+// 32 waves = 8 consecutive blocks, one per XCD. The dispatcher places blocks in
+// rounds of one block per CU (256 blocks = 32 chunks per round), and a round's
+// waves are younger on their SIMDs and run slower (4.37 vs 3.76 us per 64-B
+// run from round 3 to round 0), so with 64 counters, counters h < 32 hold
+// rounds 0 + 2 and the others rounds 1 + 3: two group speeds (median ends
+// 251-265 us). 16-wave chunks give every group one chunk per round (254-261
+// us) but do not end the launch sooner - its last few blocks set the end
+// either way - and measured even to 1 % slower over 8 interleaved rounds
+// (profiles/r05/wave_ends/), so 32 stays.
 #ifndef PNET_CLAIM_CHUNK
-#define PNET_CLAIM_CHUNK 16
+#define PNET_CLAIM_CHUNK 32
 #endif
 constexpr uint32_t kClaimChunk = PNET_CLAIM_CHUNK;
 
