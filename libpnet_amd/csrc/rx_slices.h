@@ -50,6 +50,26 @@ __device__ __forceinline__ uint32_t granule_sum(uint4 g, uint32_t acc) {
     return sad(g.w, sad(g.z, sad(g.y, sad(g.x, acc))));
 }
 
+// ---- slices the reference's u32 sums wrap on --------------------------------
+// sum_be_words and the *_checksum functions add into a u32 with `+=`
+// (util.rs:103-114,139-149,158-181), which in a release build wraps modulo
+// 2^32 once a slice is long enough: the result is finalize((exact sum) mod
+// 2^32). The kernels' folded weighted sums equal the reference's only while
+// nothing wraps — guaranteed for len + extra_len <= kExactMax (32768 words of
+// at most 0xFFFF plus the largest pseudo-header stay below 2^32). For a longer
+// one the kernels also sum its plain bytes T (v_sad_u8): with S the weighted
+// sum (v_sad_u16: bytes at even addresses weigh 1, at odd ones 256) the
+// reference's big-endian word sum is S for a slice at an odd address and
+// 257 T - S at an even one, and both hold modulo 2^32, which the u32 sums
+// keep — so the wrapped sum is exact with 32-bit arithmetic.
+constexpr uint64_t kExactMax = 65536;
+__device__ __forceinline__ uint32_t sad8(uint32_t d, uint32_t acc) { return __builtin_amdgcn_sad_u8(d, 0u, acc); }
+// the reference's big-endian word sum modulo 2^32 of a range at byte offset
+// `off`, from its weighted sum S and plain sum T (both modulo 2^32)
+__device__ __forceinline__ uint32_t be_word_sum(uint32_t S, uint32_t T, uint64_t off) {
+    return (off & 1) ? S : 257u * T - S;
+}
+
 // Weighted byte sum of [off, off+len) (absolute offsets into a.data) by one
 // G-lane group (G-aligned lanes): coalesced aligned granules, U loads in
 // flight per lane (the group covers 16 G U B per load round), byte masks only
@@ -88,10 +108,57 @@ __device__ __forceinline__ uint32_t group_range_sum(const uint8_t* data, uint64_
     return acc;
 }
 
+// group_range_sum with the plain byte sum beside it, in *tsum, for sums past
+// kExactMax (rare: every granule masked to the slice, simple code with few
+// registers beside the kernels' own paths).
+template <int G, int U>
+__device__ __forceinline__ uint32_t group_range_sum_t(const uint8_t* data, uint64_t off, uint32_t len, int j,
+                                                      uint32_t* tsum) {
+    const int sh = (int)(off & 15);
+    const uint8_t* fb = data + (off - (uint64_t)sh);
+    const int64_t e = sh + (int64_t)len;
+    const uint32_t nneed = len ? (uint32_t)((e + 15) >> 4) : 0u;
+    uint32_t acc = 0, tacc = 0;
+#pragma unroll 1
+    for (uint32_t c0 = j; c0 < nneed; c0 += G * U) {
+        uint4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t c = c0 + u * G;
+            v[u] = c < nneed ? *reinterpret_cast<const uint4*>(fb + 16ull * c) : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t c = c0 + u * G;
+            uint32_t d[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+            if (__ballot(c == 0 || c + 1 >= nneed)) {   // wave-uniform: edge granules masked to the slice
+                const int lo = c == 0 ? sh : 0;
+                const int hi = (int)min<int64_t>(max<int64_t>(e - 16 * (int64_t)c, 0), 16);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) d[k] &= first_bytes(clamp04(hi - 4 * k)) & ~first_bytes(clamp04(lo - 4 * k));
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                acc = sad(d[k], acc);
+                tacc = sad8(d[k], tacc);
+            }
+        }
+    }
+#pragma unroll
+    for (int o = G / 2; o >= 1; o >>= 1) {
+        acc += __shfl_xor(acc, o);
+        tacc += __shfl_xor(tacc, o);
+    }
+    *tsum = tacc;
+    return acc;
+}
+
 // PSEUDO: 0 = util::checksum, 4 = util::ipv4_checksum, 16 = util::ipv6_checksum.
 // EXTRA: the *_checksum_adv form with an extra_data slice (util.rs:109-114).
+// Waves/SIMD its registers must allow: what it had before the exact path
+// (61 / 69 VGPRs), so that path costs no occupancy.
 template <int PSEUDO, bool EXTRA>
-__global__ __launch_bounds__(kBlock) void slice_kernel(SliceArgs a) {
+__global__ __launch_bounds__(kBlock, EXTRA ? 7 : 8) void slice_kernel(SliceArgs a) {
     constexpr int G = 16, kPerWave = kWave / G;
     const int lane = threadIdx.x & (kWave - 1);
     const int j = lane % G;
@@ -123,18 +190,24 @@ __global__ __launch_bounds__(kBlock) void slice_kernel(SliceArgs a) {
         }
         off += a.delta;
         if (off > a.limit || (uint64_t)len > a.limit - off) len = 0;
-        uint32_t acc = group_range_sum<G, PNET_SLICE_U>(a.data, off, len, j);
-        uint32_t pe = 0, elen = 0;
+        uint64_t eoff = 0;
+        uint32_t elen = 0;
+        if (EXTRA) {
+            eoff = a.extra_offsets[i] + a.delta;
+            elen = a.extra_lengths[i];
+            if (eoff > a.limit || (uint64_t)elen > a.limit - eoff) elen = 0;
+        }
+        // group-uniform: a slice the reference's u32 sum may wrap on (kExactMax)
+        const bool lng = (uint64_t)len + elen > kExactMax;
+        uint32_t acc, tacc = 0, te = 0, tte = 0;
+        if (lng) acc = group_range_sum_t<G, 1>(a.data, off, len, j, &tacc);   // group-uniform, rare
+        else acc = group_range_sum<G, PNET_SLICE_U>(a.data, off, len, j);
         if (EXTRA) {
             // sum_be_words(extra, extra.len() / 2): every whole word, never the odd
             // trailing byte (util.rs:114; the quirk documented at udp.rs:42-44); the
             // extra slice starts its own word alignment
-            const uint64_t eoff = a.extra_offsets[i] + a.delta;
-            elen = a.extra_lengths[i];
-            if (eoff > a.limit || (uint64_t)elen > a.limit - eoff) elen = 0;
-            const uint32_t te = group_range_sum<G, PNET_SLICE_U>(a.data, eoff, elen & ~1u, j);
-            pe = fold16(te);
-            if (!(eoff & 1)) pe = bswap16(pe);
+            if (lng) te = group_range_sum_t<G, 1>(a.data, eoff, elen & ~1u, j, &tte);
+            else te = group_range_sum<G, PNET_SLICE_U>(a.data, eoff, elen & ~1u, j);
         }
         if (j == 0) {
             // skipped word: bytes [2*skip, 2*skip+2) of the slice that exist (util.rs:166-178)
@@ -143,22 +216,29 @@ __global__ __launch_bounds__(kBlock) void slice_kernel(SliceArgs a) {
                 const uint64_t q = 2ull * skip;
                 const uint32_t b0 = sb[q];
                 acc -= ((off + q) & 1) ? (b0 << 8) : b0;
+                tacc -= b0;
                 if (q + 1 < len) {
                     const uint32_t b1 = sb[q + 1];
                     acc -= ((off + q + 1) & 1) ? (b1 << 8) : b1;
+                    tacc -= b1;
                 }
             }
-            uint32_t p = fold16(acc);
+            uint32_t p = fold16(acc), pe = fold16(te);
             if (!(off & 1)) p = bswap16(p);
+            if (!(eoff & 1)) pe = bswap16(pe);
+            if (lng) {   // the reference's wrapped word sums (be_word_sum), not their folds
+                p = be_word_sum(acc, tacc, off);
+                pe = EXTRA ? be_word_sum(te, tte, eoff) : 0u;
+            }
             uint32_t r;
             if (PSEUDO == 0) {
-                r = len ? ((~p) & 0xFFFFu) : 0u;            // util.rs:77-79
+                r = len ? ((~fold16(p)) & 0xFFFFu) : 0u;    // util.rs:77-79
             } else {
                 const uint8_t* ad = a.addrs + i * (2 * PSEUDO);
                 uint32_t s = 0;
 #pragma unroll
                 for (int k = 0; k < 2 * PSEUDO; k += 2) s += ((uint32_t)ad[k] << 8) | ad[k + 1];
-                s += a.protos[i] + len + elen + p + pe;     // util.rs:103-114
+                s += a.protos[i] + len + elen + p + pe;     // util.rs:103-114 (u32: wraps as a release build's)
                 r = (~fold16(s)) & 0xFFFFu;
             }
             a.out[i] = (uint16_t)r;
@@ -188,9 +268,11 @@ __device__ __forceinline__ uint32_t chunk_sum(uint4 g0, uint4 g1, uint4 g2, uint
 
 // Sums of the slices of a run listed in mask (a bit per lane), G lanes per
 // slice, 64 / G slices per pass: lane sl's slice total lands in gsum[sl].
-template <int G, int U>
+// PLAIN: also their plain byte sums, in gtsum (long slices, kExactMax).
+template <int G, int U, bool PLAIN = false>
 __device__ __forceinline__ void listed_sums(uint64_t mask, int lane, uint8_t* list, uint32_t* gsum,
-                                            const uint8_t* data, uint64_t off, uint32_t len) {
+                                            const uint8_t* data, uint64_t off, uint32_t len,
+                                            uint32_t* gtsum = nullptr) {
     if ((mask >> lane) & 1ull) list[__popcll(mask & ((1ull << lane) - 1ull))] = (uint8_t)lane;
     wave_sync();
     const int nb = __popcll(mask);
@@ -202,8 +284,13 @@ __device__ __forceinline__ void listed_sums(uint64_t mask, int lane, uint8_t* li
         // source lane with that lane masked off
         const uint64_t soff = (uint64_t)__shfl((unsigned long long)off, sl);
         const uint32_t sl_len = (uint32_t)__shfl((int)len, sl);
-        const uint32_t t = group_range_sum<G, U>(data, soff, k < nb ? sl_len : 0u, j);
-        if (k < nb && j == 0) gsum[sl] = t;
+        uint32_t tt = 0;
+        const uint32_t t = PLAIN ? group_range_sum_t<G, U>(data, soff, k < nb ? sl_len : 0u, j, &tt)
+                                 : group_range_sum<G, U>(data, soff, k < nb ? sl_len : 0u, j);
+        if (k < nb && j == 0) {
+            gsum[sl] = t;
+            if (PLAIN) gtsum[sl] = tt;
+        }
     }
     wave_sync();
 }
@@ -216,14 +303,18 @@ constexpr int kRunDense = 5 * kWave;   // granules a dense run may span (5 KiB)
 // empty or invalid one) without the skipped word's bytes (skip: word index, or
 // ~0 for none), with the wave's LDS stage, list and sums. Ends with the LDS
 // it used free for the next call.
+// exact: the lane's slice belongs to a sum the reference's u32 may wrap on
+// (kExactMax): summed by a 16-lane group with its plain byte sum, returned in
+// *tsum (the skipped word's bytes taken off it too).
 __device__ __forceinline__ uint32_t run_range_sum(const SliceArgs& a, uint64_t run, int lane, bool in, uint64_t off,
                                                   uint32_t len, uint32_t skip, uint4* stage, uint32_t* gsum,
-                                                  uint8_t* list) {
+                                                  uint8_t* list, bool exact, uint32_t* gtsum, uint32_t* tsum) {
     constexpr int kSmall = kRunSmall, kDense = kRunDense;
     const int sh = (int)(off & 15);
     const uint8_t* fb = a.data + (off - (uint64_t)sh);
-    const int e = sh + (int)len;
-    const uint32_t nneed = len ? (uint32_t)((e + 15) >> 4) : 0u;
+    const int e = sh + (int)len;   // small slices only
+    // granules; an exact lane's slice goes to its own 16-lane class whatever its size
+    const uint32_t nneed = exact ? 0xFFFFFFFFu : len ? (uint32_t)((e + 15) >> 4) : 0u;
     const bool small = nneed <= (uint32_t)kSmall;
     // skipped word: its bytes [2 skip, 2 skip + 2) that lie in the slice (util.rs:166-178)
     const uint64_t q = 2ull * skip;
@@ -258,11 +349,14 @@ __device__ __forceinline__ uint32_t run_range_sum(const SliceArgs& a, uint64_t r
     const bool med16 = in && !small && !med8 && nneed <= 16u;
     const bool med32 = in && !small && !med8 && !med16 && nneed <= 32u;
     const uint64_t m8 = __ballot(med8), m16 = __ballot(med16), m32 = __ballot(med32);
-    const uint64_t lmask = __ballot(in && !small && !med8 && !med16 && !med32);
+    const uint64_t lmask = __ballot(in && !exact && !small && !med8 && !med16 && !med32);
     if (m8) listed_sums<2, 4>(m8, lane, list, gsum, a.data, off, len);
     if (m16) listed_sums<4, 4>(m16, lane, list, gsum, a.data, off, len);
     if (m32) listed_sums<8, 4>(m32, lane, list, gsum, a.data, off, len);
     if (lmask) listed_sums<16, PNET_SLICE_U>(lmask, lane, list, gsum, a.data, off, len);
+    // slices of sums past kExactMax: with their plain byte sums (rare)
+    if (const uint64_t xmask = __ballot(in && exact))
+        listed_sums<16, 1, true>(xmask, lane, list, gsum, a.data, off, len, gtsum);
     uint32_t acc = 0;
     if (dense) {                             // wave-uniform
         uint4* st = stage;
@@ -296,10 +390,59 @@ __device__ __forceinline__ uint32_t run_range_sum(const SliceArgs& a, uint64_t r
     } else {
         acc = gsum[lane];
     }
+    if (__ballot(exact)) *tsum = exact ? gtsum[lane] - (s0 ? b0 : 0u) - (s1 ? b1 : 0u) : 0u;   // wave-uniform
     acc -= s0 ? (((off + q) & 1) ? (b0 << 8) : b0) : 0u;
     acc -= s1 ? (((off + q + 1) & 1) ? (b1 << 8) : b1) : 0u;
     wave_sync();   // list / gsum / stage are rewritten by the next call
     return acc;
+}
+
+// slice_run_kernel's sums, results and stores for one run (descriptors
+// decoded); lng lanes: a sum the reference's u32 may wrap on (exact wrapped
+// sums, kExactMax).
+template <int PSEUDO, bool EXTRA>
+__device__ __forceinline__ void run_finish(const SliceArgs& a, uint64_t run, int lane, bool in, uint64_t i, uint64_t off,
+                                           uint32_t len, uint32_t skip, uint64_t eoff, uint32_t elen, bool lng,
+                                           uint4* dstage, uint32_t* gsum, uint8_t* glist, uint32_t* gtsum) {
+    uint32_t tacc = 0, tte = 0;
+    const uint32_t acc = run_range_sum(a, run, lane, in, off, len, skip, dstage, gsum, glist, lng, gtsum, &tacc);
+    uint32_t p = fold16(acc);
+    if (!(off & 1)) p = bswap16(p);
+    if (lng) p = be_word_sum(acc, tacc, off);
+    uint32_t pe = 0;
+    if (EXTRA) {
+        // sum_be_words(extra, extra.len() / 2): every whole word, never the
+        // odd trailing byte (util.rs:114; the quirk documented at
+        // udp.rs:42-44); the extra slice starts its own word alignment
+        const uint32_t te = run_range_sum(a, run, lane, in, eoff, elen & ~1u, 0xFFFFFFFFu, dstage, gsum, glist, lng, gtsum,
+                                          &tte);
+        pe = fold16(te);
+        if (!(eoff & 1)) pe = bswap16(pe);
+        if (lng) pe = be_word_sum(te, tte, eoff);
+    }
+    uint32_t r;
+    if (PSEUDO == 0) {
+        r = len ? ((~fold16(p)) & 0xFFFFu) : 0u;            // util.rs:77-79
+    } else {
+        uint32_t s = 0;
+        if (in) {
+            const uint8_t* ad = a.addrs + i * (2 * PSEUDO);
+            if (!(reinterpret_cast<uintptr_t>(a.addrs) & 3u)) {   // wave-uniform
+#pragma unroll
+                for (int k = 0; k < 2 * PSEUDO; k += 4) {
+                    const uint32_t w = *reinterpret_cast<const uint32_t*>(ad + k);   // 4 octets, LE load
+                    s += bswap16(w & 0xFFFFu) + bswap16(w >> 16);
+                }
+            } else {
+#pragma unroll
+                for (int k = 0; k < 2 * PSEUDO; k += 2) s += ((uint32_t)ad[k] << 8) | ad[k + 1];
+            }
+            s += a.protos[i];
+        }
+        s += len + elen + p + pe;                            // util.rs:103-114 (u32: wraps as a release build's)
+        r = (~fold16(s)) & 0xFFFFu;
+    }
+    if (in) a.out[i] = (uint16_t)r;
 }
 
 // slice_run_kernel: the same results (util::checksum, ipv4_checksum,
@@ -324,6 +467,7 @@ template <int PSEUDO, bool EXTRA>
 __global__ __launch_bounds__(kBlock, PNET_RUN_MINWAVES) void slice_run_kernel(SliceArgs a) {
     __shared__ uint4 dstage[kWavesPerBlock][kRunDense];
     __shared__ uint32_t gsum[kWavesPerBlock][kWave];
+    __shared__ uint32_t gtsum[kWavesPerBlock][kWave];   // plain byte sums of long slices (kExactMax)
     __shared__ uint8_t glist[kWavesPerBlock][kWave];
     const int lane = threadIdx.x & (kWave - 1);
     const int wv = threadIdx.x / kWave;
@@ -356,51 +500,20 @@ __global__ __launch_bounds__(kBlock, PNET_RUN_MINWAVES) void slice_run_kernel(Sl
                 off = 0;
             }
         }
-        const uint32_t acc = run_range_sum(a, run, lane, in, off, len, skip, dstage[wv], gsum[wv], glist[wv]);
-        uint32_t p = fold16(acc);
-        if (!(off & 1)) p = bswap16(p);
-        uint32_t pe = 0, elen = 0;
-        if (EXTRA) {
-            // sum_be_words(extra, extra.len() / 2): every whole word, never the
-            // odd trailing byte (util.rs:114; the quirk documented at
-            // udp.rs:42-44); the extra slice starts its own word alignment
-            uint64_t eoff = 0;
-            if (in) {
-                eoff = a.extra_offsets[i] + a.delta;
-                elen = a.extra_lengths[i];
-                if (eoff > a.limit || (uint64_t)elen > a.limit - eoff) {
-                    elen = 0;
-                    eoff = 0;
-                }
+        uint64_t eoff = 0;
+        uint32_t elen = 0;
+        if (EXTRA && in) {
+            eoff = a.extra_offsets[i] + a.delta;
+            elen = a.extra_lengths[i];
+            if (eoff > a.limit || (uint64_t)elen > a.limit - eoff) {
+                elen = 0;
+                eoff = 0;
             }
-            const uint32_t te = run_range_sum(a, run, lane, in, eoff, elen & ~1u, 0xFFFFFFFFu, dstage[wv], gsum[wv],
-                                              glist[wv]);
-            pe = fold16(te);
-            if (!(eoff & 1)) pe = bswap16(pe);
         }
-        uint32_t r;
-        if (PSEUDO == 0) {
-            r = len ? ((~p) & 0xFFFFu) : 0u;                    // util.rs:77-79
-        } else {
-            uint32_t s = 0;
-            if (in) {
-                const uint8_t* ad = a.addrs + i * (2 * PSEUDO);
-                if (!(reinterpret_cast<uintptr_t>(a.addrs) & 3u)) {   // wave-uniform
-#pragma unroll
-                    for (int k = 0; k < 2 * PSEUDO; k += 4) {
-                        const uint32_t w = *reinterpret_cast<const uint32_t*>(ad + k);   // 4 octets, LE load
-                        s += bswap16(w & 0xFFFFu) + bswap16(w >> 16);
-                    }
-                } else {
-#pragma unroll
-                    for (int k = 0; k < 2 * PSEUDO; k += 2) s += ((uint32_t)ad[k] << 8) | ad[k + 1];
-                }
-                s += a.protos[i];
-            }
-            s += len + elen + p + pe;                            // util.rs:103-114
-            r = (~fold16(s)) & 0xFFFFu;
-        }
-        if (in) a.out[i] = (uint16_t)r;
+        // a sum the reference's u32 may wrap on (kExactMax): exact wrapped sums
+        const bool lng = in && (uint64_t)len + elen > kExactMax;
+        run_finish<PSEUDO, EXTRA>(a, run, lane, in, i, off, len, skip, eoff, elen, lng, dstage[wv], gsum[wv], glist[wv],
+                                  gtsum[wv]);
     }
 }
 
@@ -498,7 +611,9 @@ __device__ __forceinline__ uint32_t window_bytes(const uint4& g0, const uint4& g
     return __builtin_amdgcn_alignbyte(hi, lo, y & 3u);
 }
 
-// sums run `run` from its stage and stores its 64 results
+// sums run `run` from its stage and stores its 64 results (COMPACT: no slice
+// reaches kExactMax, its lengths being 16-bit)
+template <bool COMPACT>
 __device__ __forceinline__ void tiny_finish(const SliceArgs& a, const TinyStage& s, uint64_t run, int lane) {
     const int sh = (int)(s.off & 15);
     const int e = sh + (int)s.len;
@@ -519,6 +634,8 @@ __device__ __forceinline__ void tiny_finish(const SliceArgs& a, const TinyStage&
 #else
     uint32_t pair = window_bytes(s.v[0], s.v[1], s.v[2], small && s0 ? (uint32_t)sh + (uint32_t)q : 0u);
 #endif
+    uint32_t tsum = 0;        // a long slice's plain byte sum (kExactMax)
+    bool any_long = false;    // wave-uniform: the run holds one
     if (__ballot(!small)) {   // wave-uniform: a run with longer slices
         // up to kTinyLaneGranules granules: the slice's own lane goes on from
         // the 3 granules it holds (summed whole above), 4 more per round
@@ -537,8 +654,17 @@ __device__ __forceinline__ void tiny_finish(const SliceArgs& a, const TinyStage&
             const int sl = __builtin_ctzll(big);
             const uint64_t soff = (uint64_t)__shfl((unsigned long long)s.off, sl);
             const uint32_t slen = (uint32_t)__shfl((int)s.len, sl);
-            const uint32_t t = group_range_sum<kWave, 1>(a.data, soff, slen, lane);
-            if (lane == sl) acc = t;
+            uint32_t t, tt = 0;
+            if (COMPACT) {
+                t = group_range_sum<kWave, 1>(a.data, soff, slen, lane);
+            } else {   // and its plain byte sum (a slice past kExactMax needs it)
+                t = group_range_sum_t<kWave, 1>(a.data, soff, slen, lane, &tt);
+                any_long |= slen > kExactMax;   // wave-uniform
+            }
+            if (lane == sl) {
+                acc = t;
+                tsum = tt;
+            }
         }
         if (!small && s0) pair = a.data[s.off + q] | (s1 ? (uint32_t)a.data[s.off + q + 1] << 8 : 0u);
     }
@@ -546,6 +672,8 @@ __device__ __forceinline__ void tiny_finish(const SliceArgs& a, const TinyStage&
     acc -= ((s.off + q) & 1) ? bswap16(sw) : sw;                    // odd address: the weights swap
     uint32_t p = fold16(acc);
     if (!(s.off & 1)) p = bswap16(p);
+    if (!COMPACT && any_long && s.len > kExactMax)   // the reference's wrapped word sum (be_word_sum)
+        p = fold16(be_word_sum(acc, tsum - (sw & 0xFFu) - (sw >> 8), s.off));
     if (s.in) a.out[run * kWave + (uint64_t)lane] = (uint16_t)(s.len ? ((~p) & 0xFFFFu) : 0u);   // util.rs:76-82
 }
 
@@ -583,12 +711,12 @@ __global__ __launch_bounds__(kBlock, PNET_TINY_MINWAVES) void slice_tiny_kernel(
         const uint64_t rz = uniform64(q.take());
         const TinyDesc dz = tiny_desc<COMPACT>(a, rz, nruns, lane);   // in flight for two runs
         const TinyStage sy = tiny_issue<COMPACT>(a, dy);                        // in flight while rx is summed
-        tiny_finish(a, sx, rx, lane);
+        tiny_finish<COMPACT>(a, sx, rx, lane);
         if (ry >= nruns) break;
         const uint64_t rw = uniform64(q.take());
         dy = tiny_desc<COMPACT>(a, rw, nruns, lane);
         sx = tiny_issue<COMPACT>(a, dz);
-        tiny_finish(a, sy, ry, lane);
+        tiny_finish<COMPACT>(a, sy, ry, lane);
         rx = rz;
         ry = rw;
     }

@@ -13,7 +13,9 @@
 
 /* ---- pnet_packet/src/util.rs ------------------------------------------ */
 
-/* util.rs:158-181  fn sum_be_words(data: &[u8], skipword: usize) -> u32 */
+/* util.rs:158-181  fn sum_be_words(data: &[u8], skipword: usize) -> u32
+ * (u32 arithmetic: wraps modulo 2^32 as the reference does in a release
+ * build - overflow checks off; a debug build panics on such inputs) */
 uint32_t oracle_sum_be_words(const uint8_t* data, size_t len, size_t skipword) {
     if (len == 0) return 0;                       /* :159-161 */
     const uint8_t* cur = data;

@@ -58,3 +58,27 @@ def test_checksum_adv_extra_data():
             if len(e) % 2:
                 flipped = e[:-1] + bytes([e[-1] ^ 0xFF])
                 assert cfn(d, skip, flipped, src, dst, proto) == want
+
+
+def test_long_slices_wrap_like_a_release_build():
+    """Slices long enough for the reference's u32 sums to wrap (util.rs:158-181,
+    103-114: `sum += ...`, modulo 2^32 in a release build): both restatements
+    wrap the same way — the GPU long-slice path is checked against this."""
+    rng = np.random.default_rng(5)
+    for ln in (131070, 131071, 131072, 200001, 1 << 20):
+        for fill in (b"\xff", None):
+            d = fill * ln if fill else rng.integers(0, 256, ln, dtype=np.uint8).tobytes()
+            for skip in (0, 7, ln // 2, 1 << 30):
+                assert coracle.checksum(d, skip) == pyoracle.checksum(d, skip)
+            src, dst = b"\xff" * 16, bytes(range(16))
+            extra = d[: 70001]
+            assert coracle.ipv6_checksum(d, 3, extra, src, dst, 17) == pyoracle.ipv6_checksum(d, 3, extra, src, dst, 17)
+            assert coracle.ipv4_checksum(d, 3, extra, src[:4], dst[:4], 6) == \
+                pyoracle.ipv4_checksum(d, 3, extra, src[:4], dst[:4], 6)
+    # all 0xFF words: the exact sum passes 2^32 first at 65538 words (the wrap changes the result)
+    d = b"\xff" * 131076
+    exact = 65538 * 0xFFFF
+    s = exact & 0xFFFFFFFF
+    while s >> 16:
+        s = (s >> 16) + (s & 0xFFFF)
+    assert coracle.checksum(d, 1 << 30) == (~s) & 0xFFFF
