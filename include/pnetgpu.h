@@ -311,7 +311,10 @@ int pnetgpu_rx_process(pnetgpu_ctx* ctx, const pnetgpu_batch* batch,
 int pnetgpu_tx_fill_checksums(pnetgpu_ctx* ctx, const pnetgpu_batch* batch,
                               const pnetgpu_rx_columns* cols, void* stream);
 
-/* out[i] = util::checksum(data[offsets[i], +lengths[i]), skipwords[i]) */
+/* out[i] = util::checksum(data[offsets[i], +lengths[i]), skipwords[i]).
+ * Every *_slices entry point returns what a release build of the reference
+ * returns for any slice length: its u32 sums wrap modulo 2^32 once a slice
+ * (+ extra slice) passes 64 KiB (a debug build panics there instead). */
 int pnetgpu_checksum_slices(pnetgpu_ctx* ctx, const uint8_t* data, uint64_t data_bytes,
                             uint64_t n, const uint64_t* offsets, const uint32_t* lengths,
                             const uint32_t* skipwords, uint16_t* out, void* stream);
