@@ -330,7 +330,7 @@ __device__ __forceinline__ uint32_t run_range_sum(const SliceArgs& a, uint64_t r
     const uint64_t base = (uint64_t)__shfl((unsigned long long)off, 0) & ~15ull;
     const uint64_t top = (uint64_t)__shfl((unsigned long long)(off + len), last);
     const bool fits = !in || !len || (small && off >= base && off + len <= top);
-    const bool dense = __ballot(!fits) == 0ull && top > base && top - base <= 16ull * kDense &&
+    const bool dense = __ballot(!fits || exact) == 0ull && top > base && top - base <= 16ull * kDense &&
                        top - base >= a.dense_min;
     uint32_t b0 = 0, b1 = 0;                 // in flight across the group phase
     if (!dense) {

@@ -1,9 +1,9 @@
 """GPU parity of the batched util::* checksums on slices long enough for the
 reference's u32 sums to wrap (util.rs:103-114,139-149,158-181: `sum += ...` in a
 release build wraps modulo 2^32; the oracle restates that). Below kExactMax =
-65536 bytes (slice + extra) nothing can wrap; above it every slice kernel hands
-the slice to its whole wave with exact 64-bit byte sums (rx_slices.h,
-long_slice_checksum). Slices of 0xFF bytes (every word 0xFFFF: the most
+65536 bytes (slice + extra) nothing can wrap; above it the slice kernels also
+sum the plain bytes T and take the word sum as S or 257 T - S, exact modulo
+2^32 (rx_slices.h, group_range_sum_t). Slices of 0xFF bytes (every word 0xFFFF: the most
 wraps), random bytes, every alignment, skipped words anywhere (also inside a
 slice's last granule and its odd trailing byte), mixed with short slices in one
 batch, through each descriptor kernel (the slice_kernel tuning) and the strided
@@ -97,3 +97,31 @@ def test_long_strided_slices(slice_len):
         got = lp.checksum_slices_strided(to_dev(buf), n, stride, slice_len, 7)
         torch.cuda.synchronize()
         assert np.array_equal(got.cpu().numpy().view(np.uint16), want), (stride, n)
+
+
+@pytest.mark.parametrize("version", [4, 6])
+def test_long_extra_with_empty_data_in_a_dense_run(version, tune):
+    """An *_adv slice whose data is empty and whose extra slice is past
+    kExactMax, in a run of small packed slices (slice_run_kernel's dense LDS
+    stage would otherwise take the run)."""
+    rng = np.random.default_rng(47 + version)
+    buf = rng.integers(0, 256, 300000, dtype=np.uint8)
+    buf[100000:] = 0xFF
+    lens = rng.integers(30, 45, 64).astype(np.int32)
+    offs = np.concatenate([[16], 16 + np.cumsum(lens[:-1])]).astype(np.int64)
+    lens[17] = 0                                      # the empty data slice
+    skips = np.full(64, 3, np.int32)
+    eoffs = np.full(64, 8, np.int64)
+    elens = np.full(64, 10, np.int32)
+    eoffs[17], elens[17] = 100001, 150001             # its long extra slice
+    alen = 4 if version == 4 else 16
+    addrs = np.full((64, 2 * alen), 0xFF, np.uint8)
+    protos = np.full(64, 17, np.uint8)
+    tune("slice_kernel", "run")
+    fn = coracle.ipv4_checksum if version == 4 else coracle.ipv6_checksum
+    want = np.array([fn(buf[o:o + ln], sk, buf[eo:eo + el].tobytes(), a[:alen].tobytes(), a[alen:].tobytes(), int(p))
+                     for o, ln, sk, eo, el, a, p in zip(offs, lens, skips, eoffs, elens, addrs, protos)], np.uint16)
+    got = lp.checksum_adv_slices(version, to_dev(buf), to_dev(offs), to_dev(lens), to_dev(skips), to_dev(eoffs),
+                                 to_dev(elens), to_dev(addrs), to_dev(protos))
+    torch.cuda.synchronize()
+    assert np.array_equal(got.cpu().numpy().view(np.uint16), want)
