@@ -150,8 +150,12 @@ void pnetgpu_pcap_close(pnetgpu_pcap* p);
  * pnetgpu_ring_submit_region: from byte *pos (0 = start of file) fill up to cap
  * record descriptors (offset of each record's captured bytes in img, its
  * captured length), *n = records found, *pos = where the next call resumes
- * (img_bytes at the end; for pcapng a block boundary — each call re-reads the
- * block headers before it for the section state). PNETGPU_EFORMAT for a bad
+ * (img_bytes at the end; for pcapng a block boundary). pcapng's section state
+ * at *pos comes from the blocks before it: a call that continues the calling
+ * thread's previous scan (same img and img_bytes, *pos where that call
+ * stopped) resumes with the state it stopped with, any other call re-reads the
+ * block headers before *pos — so an image must not be rewritten in place
+ * between the calls of one scan. PNETGPU_EFORMAT for a bad
  * header, an unsupported link type, a truncated record or block, or (pcapng)
  * a block whose two length fields differ or a packet naming an undescribed
  * interface. Link types: Ethernet (1) and raw IP (101, 228, 229) — check
