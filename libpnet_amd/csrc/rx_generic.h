@@ -179,6 +179,10 @@ __device__ __forceinline__ void tail_sums(const uint8_t* data, WaveLds<NW>& L, i
 #ifndef PNET_DEFER
 #define PNET_DEFER 3   // runs whose records the unified (MTU) shape holds back (A/B: 0 = store each run's at once)
 #endif
+#ifndef PNET_MIXED_UNI
+#define PNET_MIXED_UNI 1   // the mixed shape streams runs of large frames in the unified order (A/B: 0)
+#endif
+constexpr uint32_t kUniMin = 768;   // every frame of such a run at least this long (PNETGPU_DESC_HINT_LARGE's bar)
 template <int NW, int G, int U, bool NT, int PASS, bool DYN, bool EXT, bool TX>
 __global__ __launch_bounds__(kBlock, NW < 8 ? 5 : 4) void rx_kernel(RxArgs a) {
     // the window must hold every field the parse reads near (Ethernet + 2 VLAN
@@ -310,7 +314,12 @@ __global__ __launch_bounds__(kBlock, NW < 8 ? 5 : 4) void rx_kernel(RxArgs a) {
         // (profiles/r03/short_runs/).
         const bool short_run = kShortRuns && __ballot(in_batch && !desc_bad && len > 64u) == 0ull;
         const bool four = short_run && __ballot(span > 4u) == 0ull;
-
+        // a run of large frames in the mixed shape (a descriptor batch of
+        // MTU-size traffic without PNETGPU_DESC_HINT_LARGE, or a burst of it
+        // inside a mix): each frame streamed once in the MTU shape's unified
+        // order instead of window first, then tail
+        constexpr bool kUniRuns = PNET_MIXED_UNI && PASS == 0 && DYN;
+        const bool uni = kUniRuns && __ballot(in_batch && (desc_bad || len < kUniMin)) == 0ull;
 
         // ---- 2. window: NW*64 granule loads, all in flight before any store --
         if (kShortRuns && four) {   // wave-uniform: 4 granules per frame
@@ -330,7 +339,7 @@ __global__ __launch_bounds__(kBlock, NW < 8 ? 5 : 4) void rx_kernel(RxArgs a) {
                 uint32_t* dst = reinterpret_cast<uint32_t*>(L.win + (q >> 2) * kSlot + 16 * (q & 3));
                 dst[0] = g[i].x; dst[1] = g[i].y; dst[2] = g[i].z; dst[3] = g[i].w;
             }
-        } else if (PASS != 1) {
+        } else if (PASS != 1 && !uni) {
             uint4 g[NW];
 #pragma unroll
             for (int i = 0; i < NW; ++i) {
@@ -358,7 +367,7 @@ __global__ __launch_bounds__(kBlock, NW < 8 ? 5 : 4) void rx_kernel(RxArgs a) {
         // flight); the parse then trims it to the L4 range B, which in every
         // well-formed frame already runs to the end of the frame. Unified pass:
         // the group loop also fills the window of every frame.
-        const bool has_tail = PASS == 1 ? in_batch : long_frame;
+        const bool has_tail = (PASS == 1 || uni) ? in_batch : long_frame;
         const uint64_t tmask = __ballot(has_tail);
         if (tmask) {
             // DYN: frames needing more than one group round go first
@@ -372,8 +381,11 @@ __global__ __launch_bounds__(kBlock, NW < 8 ? 5 : 4) void rx_kernel(RxArgs a) {
             }
             if (DYN && lane == 0) L.qhead = kWave / G;
             wave_sync();
-            tail_sums<NW, G, U, NT, (PASS != 0), DYN, (PNET_MTU_ALT && PASS == 1 && !DYN)>(
-                a.data, L, lane, __popcll(tmask) PNET_TAIL_STAT);
+            if (kUniRuns && uni)   // the MTU shape's tail configuration (PNET_MTU_CFG)
+                tail_sums<NW, 8, 4, false, true, false, PNET_MTU_ALT>(a.data, L, lane, __popcll(tmask) PNET_TAIL_STAT);
+            else
+                tail_sums<NW, G, U, NT, (PASS != 0), DYN, (PNET_MTU_ALT && PASS == 1 && !DYN)>(
+                    a.data, L, lane, __popcll(tmask) PNET_TAIL_STAT);
         }
         wave_sync();
 

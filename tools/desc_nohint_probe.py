@@ -1,0 +1,43 @@
+#!/usr/bin/env python3
+"""Kernel times of descriptor batches the mixed shape takes: the 1500-B UDP
+batch as compact descriptors without a size hint (bench.py's descriptor line),
+and the IMIX batch (full record and verify-only). Used with tools/abvar.sh
+(AB_SCRIPT) to compare library variants on one box.
+
+  PNETGPU_LIB=.../libpnetgpu_V.so python tools/desc_nohint_probe.py
+"""
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402
+bench.load_library()
+from bench import HBM_PEAK_GBS, Shard, descriptor_rate, time_launches  # noqa: E402
+
+
+def main():
+    dev = torch.device("cuda", 0)
+    steps, warmup = 20, 3
+    sh = Shard("udp1500", 1 << 20, 1000, dev)
+    d = descriptor_rate(sh, steps, warmup, dev)
+    for k in ("no_hint", "with_hint"):
+        print(f"udp1500_desc {k:9s}: {d[k]['kernel_avg_ms'] * 1e3:7.1f} us  frac {d[k]['frac']:.4f}  {d[k]['kernel']}",
+              flush=True)
+    del sh
+    torch.cuda.empty_cache()
+    for name in ("imix", "imix_verify"):
+        sh = Shard(name, 1 << 22, 1000, dev)
+        s = torch.cuda.Stream(dev)
+        ms = time_launches(lambda st: sh.step(st), steps, warmup, s)
+        print(f"{name:12s}          : {ms * 1e3:7.1f} us  frac {sh.alg_bytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS:.4f}",
+              flush=True)
+        del sh
+        torch.cuda.empty_cache()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
