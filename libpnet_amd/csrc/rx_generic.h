@@ -182,6 +182,9 @@ __device__ __forceinline__ void tail_sums(const uint8_t* data, WaveLds<NW>& L, i
 #ifndef PNET_MIXED_UNI
 #define PNET_MIXED_UNI 1   // the mixed shape streams runs of large frames in the unified order (A/B: 0)
 #endif
+#ifndef PNET_UNI_ROTATE
+#define PNET_UNI_ROTATE 1   // A/B: 0 = those runs keep the wave's issue priority
+#endif
 constexpr uint32_t kUniMin = 768;   // every frame of such a run at least this long (PNETGPU_DESC_HINT_LARGE's bar)
 template <int NW, int G, int U, bool NT, int PASS, bool DYN, bool EXT, bool TX>
 __global__ __launch_bounds__(kBlock, NW < 8 ? 5 : 4) void rx_kernel(RxArgs a) {
@@ -320,6 +323,9 @@ __global__ __launch_bounds__(kBlock, NW < 8 ? 5 : 4) void rx_kernel(RxArgs a) {
         // order instead of window first, then tail
         constexpr bool kUniRuns = PNET_MIXED_UNI && PASS == 0 && DYN;
         const bool uni = kUniRuns && __ballot(in_batch && (desc_bad || len < kUniMin)) == 0ull;
+        // such runs rotate their issue priority as the MTU shape does: no-hint
+        // 1500-B batches -2.6 %, IMIX even (profiles/r05/uni_runs/ab_rotate.txt)
+        if (PNET_UNI_ROTATE && kUniRuns && uni) rotate_prio(run_count++);
 
         // ---- 2. window: NW*64 granule loads, all in flight before any store --
         if (kShortRuns && four) {   // wave-uniform: 4 granules per frame
