@@ -185,7 +185,14 @@ __device__ __forceinline__ void tail_sums(const uint8_t* data, WaveLds<NW>& L, i
 #ifndef PNET_UNI_ROTATE
 #define PNET_UNI_ROTATE 1   // A/B: 0 = those runs keep the wave's issue priority
 #endif
-constexpr uint32_t kUniMin = 768;   // every frame of such a run at least this long (PNETGPU_DESC_HINT_LARGE's bar)
+#ifndef PNET_MIXED_JUMBO
+#define PNET_MIXED_JUMBO 1   // ... and runs of jumbo frames with the jumbo shape's tail (A/B: 0)
+#endif
+#ifndef PNET_MIXED_JUMBO_U
+#define PNET_MIXED_JUMBO_U 9   // its loads in flight per lane, as the jumbo shape (8 in the TX + EXT one: no spill)
+#endif
+constexpr uint32_t kUniMin = 768;     // every frame of such a run at least this long (PNETGPU_DESC_HINT_LARGE's bar)
+constexpr uint32_t kJumboMin = 4096;  // and shorter than this; runs of frames all this long: the jumbo tail
 template <int NW, int G, int U, bool NT, int PASS, bool DYN, bool EXT, bool TX>
 __global__ __launch_bounds__(kBlock, NW < 8 ? 5 : 4) void rx_kernel(RxArgs a) {
     // the window must hold every field the parse reads near (Ethernet + 2 VLAN
@@ -322,7 +329,11 @@ __global__ __launch_bounds__(kBlock, NW < 8 ? 5 : 4) void rx_kernel(RxArgs a) {
         // inside a mix): each frame streamed once in the MTU shape's unified
         // order instead of window first, then tail
         constexpr bool kUniRuns = PNET_MIXED_UNI && PASS == 0 && DYN;
-        const bool uni = kUniRuns && __ballot(in_batch && (desc_bad || len < kUniMin)) == 0ull;
+        const bool uni = kUniRuns && __ballot(in_batch && (desc_bad || len < kUniMin || len >= kJumboMin)) == 0ull;
+        // and a run of jumbo frames (every frame >= 4 KiB): the jumbo shape's
+        // tail, one frame per wave round
+        const bool jrun = kUniRuns && PNET_MIXED_JUMBO && !uni &&
+                          __ballot(in_batch && (desc_bad || len < kJumboMin)) == 0ull;
         // such runs rotate their issue priority as the MTU shape does: no-hint
         // 1500-B batches -2.6 %, IMIX even (profiles/r05/uni_runs/ab_rotate.txt)
         if (PNET_UNI_ROTATE && kUniRuns && uni) rotate_prio(run_count++);
@@ -389,6 +400,9 @@ __global__ __launch_bounds__(kBlock, NW < 8 ? 5 : 4) void rx_kernel(RxArgs a) {
             wave_sync();
             if (kUniRuns && uni)   // the MTU shape's tail configuration (PNET_MTU_CFG)
                 tail_sums<NW, 8, 4, false, true, false, PNET_MTU_ALT>(a.data, L, lane, __popcll(tmask) PNET_TAIL_STAT);
+            else if (kUniRuns && PNET_MIXED_JUMBO && jrun)   // the jumbo shape's (PNET_JUMBO_CFG)
+                tail_sums<NW, 64, (TX && EXT ? 8 : PNET_MIXED_JUMBO_U), true, false, false>(
+                    a.data, L, lane, __popcll(tmask) PNET_TAIL_STAT);
             else
                 tail_sums<NW, G, U, NT, (PASS != 0), DYN, (PNET_MTU_ALT && PASS == 1 && !DYN)>(
                     a.data, L, lane, __popcll(tmask) PNET_TAIL_STAT);

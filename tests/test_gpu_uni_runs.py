@@ -1,7 +1,8 @@
 """GPU parity of the mixed shape's large-frame runs (rx_generic.h, PNET_MIXED_UNI):
-a run of 64 frames whose every frame is at least 768 B is streamed in the MTU
-shape's unified order inside the mixed kernel (descriptor batches without a
-size hint). Bursts of such runs between mixed runs, at any alignment, with and
+a run of 64 frames whose every frame is at least 768 B (and under 4 KiB) is
+streamed in the MTU shape's unified order inside the mixed kernel, and a run of
+frames all at least 4 KiB with the jumbo shape's tail (descriptor batches
+without a size hint). Bursts of such runs between mixed runs, at any alignment, with and
 without the parse extensions, the header-field columns and TX; runs that just
 miss the bar (one 767-B frame, one invalid descriptor); and the bench's
 no-hint 1500-B descriptor batch at full size — every column and counter equal
@@ -20,18 +21,25 @@ pytestmark = pytest.mark.gpu
 
 
 def bursty_frames(rng, nruns):
-    """Runs of 64 frames: large-only (768..3000 B), mixed, or large with one
-    frame just under the bar."""
+    """Runs of 64 frames: large-only (768..3000 B), mixed, large with one
+    frame just under the bar, jumbo-only (>= 4096 B), and 4095-B frames with
+    one 4096-B frame."""
     frames = []
     for r in range(nruns):
-        kind = r % 4
+        kind = r % 6
         if kind in (0, 1):
             frames += framegen.random_frames(rng, 64, min_len=768, max_len=3000)
         elif kind == 2:
             frames += framegen.random_frames(rng, 64, max_len=1600)
-        else:
+        elif kind == 3:
             run = framegen.random_frames(rng, 64, min_len=768, max_len=1600)
             run[int(rng.integers(0, 64))] = framegen.random_frames(rng, 1, min_len=767, max_len=767)[0]
+            frames += run
+        elif kind == 4:                         # jumbo run (every frame >= 4096 B)
+            frames += framegen.random_frames(rng, 64, min_len=4096, max_len=9100)
+        else:                                   # large run with one frame at the jumbo bar
+            run = framegen.random_frames(rng, 64, min_len=4095, max_len=4095)
+            run[int(rng.integers(0, 64))] = framegen.random_frames(rng, 1, min_len=4096, max_len=4096)[0]
             frames += run
     return frames
 
@@ -93,11 +101,13 @@ def test_tx_fill_bursts_of_large_runs():
     compare(res, want_rec)
 
 
-def test_udp1500_descriptor_batch_without_hint_full_size():
+@pytest.mark.parametrize("name,n", [("udp1500", 1 << 20), ("udp6_jumbo", 1 << 17)])
+def test_descriptor_batch_without_hint_full_size(name, n):
     """bench.py's descriptor line (`descriptor.no_hint`): the 2^20-frame 1500-B
-    UDP batch as compact descriptors with no size hint — the mixed kernel,
-    every run large — against the oracle, planted corruptions included."""
-    w = lp.synth.make("udp1500", 1 << 20, seed=1000, corrupt_ppm=10000)
+    UDP batch (and the 9000-B jumbo batch) as compact descriptors with no size
+    hint — the mixed kernel, every run large — against the oracle, planted
+    corruptions included."""
+    w = lp.synth.make(name, n, seed=1000, corrupt_ppm=10000)
     offs = np.arange(w.n, dtype=np.uint64) * np.uint64(w.stride)
     lens = np.full(w.n, w.frame_len, np.uint32)
     rec = coracle.rx_batch(w.buf, w.n, offsets=offs, lengths=lens, nthreads=NTHREADS)

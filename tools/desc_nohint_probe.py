@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
-"""Kernel times of descriptor batches the mixed shape takes: the 1500-B UDP
-batch as compact descriptors without a size hint (bench.py's descriptor line),
-and the IMIX batch (full record and verify-only). Used with tools/abvar.sh
+"""Kernel times of descriptor batches the mixed shape takes: the 1500-B UDP and
+9000-B jumbo batches as compact descriptors without a size hint (bench.py's
+descriptor line) and with it, and the IMIX batch (full record and verify-only). Used with tools/abvar.sh
 (AB_SCRIPT) to compare library variants on one box.
 
   PNETGPU_LIB=.../libpnetgpu_V.so python tools/desc_nohint_probe.py
@@ -21,18 +21,19 @@ from bench import HBM_PEAK_GBS, Shard, descriptor_rate, time_launches  # noqa: E
 def main():
     dev = torch.device("cuda", 0)
     steps, warmup = 20, 3
-    sh = Shard("udp1500", 1 << 20, 1000, dev)
-    d = descriptor_rate(sh, steps, warmup, dev)
-    for k in ("no_hint", "with_hint"):
-        print(f"udp1500_desc {k:9s}: {d[k]['kernel_avg_ms'] * 1e3:7.1f} us  frac {d[k]['frac']:.4f}  {d[k]['kernel']}",
-              flush=True)
-    del sh
-    torch.cuda.empty_cache()
+    for name, n in (("udp1500", 1 << 20), ("udp6_jumbo", 1 << 17)):
+        sh = Shard(name, n, 1000, dev)
+        d = descriptor_rate(sh, steps, warmup, dev)
+        for k in ("no_hint", "with_hint"):
+            print(f"{name + '_desc':15s} {k:9s}: {d[k]['kernel_avg_ms'] * 1e3:7.1f} us  frac {d[k]['frac']:.4f}  "
+                  f"{d[k]['kernel']}", flush=True)
+        del sh
+        torch.cuda.empty_cache()
     for name in ("imix", "imix_verify"):
         sh = Shard(name, 1 << 22, 1000, dev)
         s = torch.cuda.Stream(dev)
         ms = time_launches(lambda st: sh.step(st), steps, warmup, s)
-        print(f"{name:12s}          : {ms * 1e3:7.1f} us  frac {sh.alg_bytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS:.4f}",
+        print(f"{name:15s}          : {ms * 1e3:7.1f} us  frac {sh.alg_bytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS:.4f}",
               flush=True)
         del sh
         torch.cuda.empty_cache()
