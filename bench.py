@@ -526,8 +526,10 @@ def tx_fill_rate(sh, steps, warmup, device):
 def descriptor_rate(sh, steps, warmup, device):
     """The same fixed-size frames handed over as a descriptor batch (compact
     descriptors, as the ring and the AF_PACKET path ship them): kernel time with
-    no size hint (the mixed shape) and with the hint pnetgpu_desc_size_hint
-    gives for their lengths (DESC_HINT_LARGE -> the MTU shape). Algorithmic
+    no size hint (the mixed shape, which streams runs of large or jumbo frames
+    in the MTU / jumbo order itself) and with the hint pnetgpu_desc_size_hint
+    gives for their lengths (DESC_HINT_LARGE -> the MTU shape, DESC_HINT_JUMBO
+    -> the jumbo shape). Algorithmic
     bytes = frames + 26-B record + 6-B descriptor per frame."""
     w = sh.w
     if not w.stride or w.buf is None:
@@ -928,9 +930,10 @@ def main():
                 if name in results and name != primary:
                     line["workloads"][name]["tx_fill"] = tx_fill_rate(results[name]["sh"], args.steps, args.warmup,
                                                                       device)
-            if "udp1500" in results:
-                line["workloads"]["udp1500"]["descriptor_mode"] = descriptor_rate(results["udp1500"]["sh"], args.steps,
-                                                                                 args.warmup, device)
+            for name in ("udp1500", "udp6_jumbo"):   # fixed-size frames as a descriptor batch, no hint / hint
+                if name in results:
+                    line["workloads"][name]["descriptor_mode"] = descriptor_rate(results[name]["sh"], args.steps,
+                                                                               args.warmup, device)
             if "tcp1500" in results:
                 line["workloads"]["tcp1500"]["ipv4_checksum_slices"] = slices_rate(results["tcp1500"]["sh"], args.steps,
                                                                                    args.warmup, device)
