@@ -143,7 +143,11 @@ extern "C" {
  * (profiles/r05/shape/), packed 1500-B frames 0.33 ms mixed -> 0.28 ms MTU,
  * 9000-B frames 0.205 -> 0.176 ms jumbo, 64-B/9000-B frames at 7:1 0.122 ->
  * 0.109 ms jumbo — but IMIX 0.34 ms mixed -> 0.58 ms MTU, 1.29 ms jumbo, so
- * the hint must describe the batch. Records are identical whatever the hint.
+ * the hint must describe the batch. Without a hint the mixed shape streams
+ * each run of 64 frames that are all 768 B - 4 KiB in the MTU order, and each
+ * run of frames all >= 4 KiB in the jumbo order (1500-B frames 0.283 ms,
+ * 9000-B 0.178 ms, profiles/r05/uni_runs/); the hint still saves the run
+ * checks. Records are identical whatever the hint.
  * pnetgpu_desc_size_hint computes it from host-side lengths. */
 #define PNETGPU_DESC_HINT_LARGE   0x200u  /* (nearly) every frame >= 768 B: the MTU shape       */
 #define PNETGPU_DESC_HINT_JUMBO   0x400u  /* most bytes in frames >= 4 KiB: the jumbo shape      */
