@@ -18,8 +18,27 @@ bench.load_library()
 from bench import HBM_PEAK_GBS, Shard, descriptor_rate, time_launches  # noqa: E402
 
 
+def nohint_only(name, n, dev, launches=5):
+    """Only the no-hint descriptor batch of one workload, a few launches (a
+    short program for rocprofv3 --pmc passes: tools/pmc_desc_nohint.sh)."""
+    sh = Shard(name, n, 1000, dev)
+    w = sh.w
+    offs = torch.from_numpy((np.arange(n, dtype=np.uint64) * np.uint64(w.stride)).astype(np.uint32).view(np.int32))
+    offs = offs.to(dev)
+    lens = torch.full((n,), w.frame_len, dtype=torch.int16, device=dev)
+    res = bench.lp.RxResult(n, dev, bench.lp.IPV4_COLUMNS, counters=False)
+    for _ in range(launches):
+        bench.lp.rx_process(sh.data, offsets=offs, lengths=lens, out=res, flags=bench.lp.DESC_COMPACT)
+    torch.cuda.synchronize()
+    print(f"{name}: {launches} no-hint launches, alg bytes per launch {sh.frame_bytes + n * 32}", flush=True)
+    return 0
+
+
 def main():
     dev = torch.device("cuda", 0)
+    if len(sys.argv) > 1 and sys.argv[1] == "--nohint-only":
+        name = sys.argv[2]
+        return nohint_only(name, {"udp1500": 1 << 20, "udp6_jumbo": 1 << 17}[name], dev)
     steps, warmup = 20, 3
     for name, n in (("udp1500", 1 << 20), ("udp6_jumbo", 1 << 17)):
         sh = Shard(name, n, 1000, dev)
