@@ -151,6 +151,14 @@ void launch_t(const RxArgs& args, int kind, int blocks, hipStream_t stream) {
 #ifndef PNET_SMALL_BLOCKS
 #define PNET_SMALL_BLOCKS 4
 #endif
+// The jumbo shape: 2 per CU (2 waves/SIMD, 9 KiB in flight per wave). With
+// more, a batch that fills them reads slower: 2^18 / 2^19 9000-B frames 0.81 /
+// 0.85 of 8 TB/s at 2 against 0.80 / 0.81 at 4 (bench.py --frames-scale 2 / 4,
+// same box, profiles/r05/jumbo_blocks/); the bench's 2^17 frames (2048 runs)
+// fill 2 per CU either way.
+#ifndef PNET_JUMBO_BLOCKS
+#define PNET_JUMBO_BLOCKS 2
+#endif
 
 int rx_blocks_per_cu(int kind, bool ext, int* numregs, int* lds) {
     const void* fn = ext ? pick_fn<true, false>(kind) : pick_fn<false, false>(kind);
@@ -160,7 +168,9 @@ int rx_blocks_per_cu(int kind, bool ext, int* numregs, int* lds) {
         if (lds) *lds = (int)fa.sharedSizeBytes;
     }
     const int nb = resident_blocks(fn, kBlock);
-    return kind == kKindSmall && nb > PNET_SMALL_BLOCKS ? PNET_SMALL_BLOCKS : nb;
+    if (kind == kKindSmall && nb > PNET_SMALL_BLOCKS) return PNET_SMALL_BLOCKS;
+    if (kind == kKindJumbo && nb > PNET_JUMBO_BLOCKS) return PNET_JUMBO_BLOCKS;
+    return nb;
 }
 
 // runs per block per pass (one per wave)
