@@ -193,8 +193,11 @@ __device__ __forceinline__ void tail_sums(const uint8_t* data, WaveLds<NW>& L, i
 #endif
 constexpr uint32_t kUniMin = 768;     // every frame of such a run at least this long (PNETGPU_DESC_HINT_LARGE's bar)
 constexpr uint32_t kJumboMin = 4096;  // and shorter than this; runs of frames all this long: the jumbo tail
+#ifndef PNET_JUMBO_LB
+#define PNET_JUMBO_LB 4   // the jumbo shape's (NT) launch bound (A/B: 2 lets it use 256 VGPRs)
+#endif
 template <int NW, int G, int U, bool NT, int PASS, bool DYN, bool EXT, bool TX>
-__global__ __launch_bounds__(kBlock, NW < 8 ? 5 : 4) void rx_kernel(RxArgs a) {
+__global__ __launch_bounds__(kBlock, NT ? PNET_JUMBO_LB : (NW < 8 ? 5 : 4)) void rx_kernel(RxArgs a) {
     // the window must hold every field the parse reads near (Ethernet + 2 VLAN
     // tags + the fixed IPv4 header / IPv6 addresses: 82 B) after a 15-B shift
     static_assert(NW >= 7 || NW == 6, "window granules");
