@@ -296,42 +296,103 @@ VERIFY_COLUMNS = ("status", "ip_csum", "l4_csum")
 
 def e2e_rate(sh, device, chunks=16, reps=3, columns=None):
     """PCIe-inclusive rate: pinned host frames -> H2D -> kernel -> D2H of the results,
-    double-buffered on two streams. Reported beside `value`, never as `value`."""
-    if not sh.w.stride:
-        return None
+    double-buffered on two streams. Fixed-stride batches ship the frames only;
+    descriptor batches (IMIX) ship each chunk's frame span plus its compact
+    descriptors (u32 offset rebased to the chunk + u16 length, 6 B/frame) with
+    the size hint the ring would give. Reported beside `value`, never as `value`.
+    `stages`: per-stage device time summed over the timed chunks (HIP events on
+    the two streams, so H2D of one chunk overlaps the kernel / D2H of the other)."""
     columns = columns or lp.IPV4_COLUMNS
-    n, stride = sh.n, sh.w.stride
-    host = torch.from_numpy(sh.w.buf[: n * stride]).pin_memory()
+    w = sh.w
+    n = sh.n
     per = n // chunks
     streams = [torch.cuda.Stream(device), torch.cuda.Stream(device)]
-    dbuf = [torch.empty(per * stride + 32, dtype=torch.uint8, device=device) for _ in range(2)]
     res = [lp.RxResult(per, device, columns, counters=False) for _ in range(2)]
     hout = [torch.empty(r.nbytes, dtype=torch.uint8).pin_memory() for r in res]
+    if w.stride:
+        stride = w.stride
+        host = torch.from_numpy(w.buf[: n * stride]).pin_memory()
+        spans = [(k * per * stride, (k + 1) * per * stride) for k in range(chunks)]
+        desc = None
+        up_desc = 0
+    else:
+        offs, lens = w.offsets[: per * chunks], w.lengths[: per * chunks]
+        if int(lens.max()) > 0xFFFF:
+            return None
+        spans = [(int(offs[k * per]), int(offs[(k + 1) * per - 1] + lens[(k + 1) * per - 1])) for k in range(chunks)]
+        if max(e - b for b, e in spans) > 0xFFFFFFFF:
+            return None
+        host = torch.from_numpy(w.buf[: spans[-1][1]]).pin_memory()
+        rebased = np.concatenate([(offs[k * per:(k + 1) * per] - np.uint64(spans[k][0])).astype(np.uint32)
+                                  for k in range(chunks)])
+        h_off = torch.from_numpy(rebased.view(np.int32)).pin_memory()
+        h_len = torch.from_numpy(lens.astype(np.uint16).view(np.int16)).pin_memory()
+        d_off = [torch.empty(per, dtype=torch.int32, device=device) for _ in range(2)]
+        d_len = [torch.empty(per, dtype=torch.int16, device=device) for _ in range(2)]
+        hints = [lp.desc_size_hint(lens[k * per:(k + 1) * per]) for k in range(chunks)]
+        desc = (h_off, h_len, d_off, d_len, hints)
+        up_desc = 6
+    span_max = max(e - b for b, e in spans)
+    dbuf = [torch.empty(span_max + 32, dtype=torch.uint8, device=device) for _ in range(2)]
+    for d in dbuf:
+        d.zero_()                                     # the granule tail past every span reads zeros
+    ev = {}
 
-    def chunk(k):
+    def chunk(k, timed):
         s, j = streams[k % 2], k % 2
+        b, e = spans[k]
         with torch.cuda.stream(s):
-            dbuf[j][: per * stride].copy_(host[k * per * stride:(k + 1) * per * stride], non_blocking=True)
-            lp.rx_process(dbuf[j], stride=stride, frame_len=stride, n_frames=per, out=res[j], stream=s)
+            if timed:
+                marks = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+                marks[0].record(s)
+            dbuf[j][: e - b].copy_(host[b:e], non_blocking=True)
+            if desc is None:
+                if timed:
+                    marks[1].record(s)
+                lp.rx_process(dbuf[j], stride=w.stride, frame_len=w.stride, n_frames=per, out=res[j], stream=s)
+            else:
+                h_off, h_len, d_off, d_len, hints = desc
+                d_off[j].copy_(h_off[k * per:(k + 1) * per], non_blocking=True)
+                d_len[j].copy_(h_len[k * per:(k + 1) * per], non_blocking=True)
+                if timed:
+                    marks[1].record(s)
+                lp.rx_process(dbuf[j], offsets=d_off[j], lengths=d_len[j], out=res[j], stream=s,
+                              flags=lp.DESC_COMPACT | hints[k])
+            if timed:
+                marks[2].record(s)
             res[j].to_host(hout[j], stream=s)             # every record column in one D2H
+            if timed:
+                marks[3].record(s)
+                ev.setdefault("marks", []).append(marks)
 
     # one untimed pass over the batch first: the first pass from a freshly
     # pinned buffer measured ~60 % of the later ones (profiles/r05/ring/)
     for k in range(chunks):
-        chunk(k)
+        chunk(k, False)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(reps):
         for k in range(chunks):
-            chunk(k)
+            chunk(k, True)
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     frames = reps * chunks * per
+    nbytes = reps * sum(e - b for b, e in spans)
+    st = {"h2d_s": 0.0, "kernel_s": 0.0, "d2h_s": 0.0}
+    for m in ev.get("marks", []):
+        st["h2d_s"] += m[0].elapsed_time(m[1]) / 1e3
+        st["kernel_s"] += m[1].elapsed_time(m[2]) / 1e3
+        st["d2h_s"] += m[2].elapsed_time(m[3]) / 1e3
     rb = lp.engine.column_bytes(columns)
-    return {"mpkts_s": round(frames / el / 1e6, 1), "gb_s": round(frames * stride / el / 1e9, 2),
-            **_link(frames, el, stride, res[0].nbytes / per),
+    return {"mpkts_s": round(frames / el / 1e6, 1), "gb_s": round(nbytes / el / 1e9, 2),
+            **_link(frames, el, nbytes / frames + up_desc, res[0].nbytes / per),
+            "stages": {"wall_s": round(el, 4), **{k: round(v, 4) for k, v in st.items()},
+                       "h2d_gb_s": round(nbytes / st["h2d_s"] / 1e9, 2) if st["h2d_s"] else None,
+                       "host_threads": 1},
             "note": "pinned host batch -> hipMemcpyAsync H2D -> rx kernel -> one D2H of the packed record "
-                    f"columns ({rb} B/frame: {', '.join(columns)}), {chunks} chunks double-buffered on 2 streams"}
+                    f"columns ({rb} B/frame: {', '.join(columns)}), {chunks} chunks double-buffered on 2 streams"
+                    + ("" if desc is None else "; descriptor batch: each chunk's frame span + compact descriptors "
+                                               "(6 B/frame) up, with the size hint pnetgpu_desc_size_hint gives")}
 
 
 def _ring_link(frames, nbytes, el, rb, nbatches):
@@ -341,12 +402,25 @@ def _ring_link(frames, nbytes, el, rb, nbatches):
     return _link(frames, el, nbytes / frames + 6, rb + 64 * nbatches / frames)
 
 
-def e2e_ring_rate(sh, seconds=3.0, columns=None, slots=None):
-    """Producer-inclusive rate: frames copied into the pinned ring
-    (pnetgpu_ring_push_many: the DataLinkReceiver::next() consumer), shipped,
-    verified and the record columns copied back (rotating slots: one filling,
-    one held by the consumer, the rest in flight)."""
-    columns = columns or lp.IPV4_COLUMNS
+def _ring_stages(ring, el):
+    """Where a ring line's wall time went (pnetgpu_ring_stats): host seconds in
+    push_many (descriptors + copies), submit (enqueueing) and wait (blocked on
+    the oldest batch), the rest of the host loop, and the device stage sums."""
+    st = ring.stats()
+    host = {k: st[k + "_ns"] / 1e9 for k in ("push", "submit", "wait")}
+    out = {"wall_s": round(el, 4), **{f"{k}_s": round(v, 4) for k, v in host.items()},
+           "other_host_s": round(el - sum(host.values()), 4),
+           "h2d_s": round(st["h2d_ms"] / 1e3, 4), "kernel_s": round(st["kernel_ms"] / 1e3, 4),
+           "d2h_s": round(st["d2h_ms"] / 1e3, 4), "batches": st["batches"], "timed_batches": st["timed_batches"],
+           "host_threads": st["host_threads"]}
+    if st["push_ns"]:
+        out["push_gb_s"] = round(st["bytes"] / (st["push_ns"] / 1e9) / 1e9, 2)
+    if st["h2d_ms"]:
+        out["h2d_gb_s"] = round(st["bytes"] / (st["h2d_ms"] / 1e3) / 1e9, 2)
+    return out
+
+
+def _ring_source(sh):
     w = sh.w
     n = min(sh.n, 1 << 22)
     if w.stride:
@@ -354,7 +428,19 @@ def e2e_ring_rate(sh, seconds=3.0, columns=None, slots=None):
         lens = np.full(n, w.frame_len, dtype=np.uint32)
     else:
         offs, lens = w.offsets[:n], w.lengths[:n]
-    ring = lp.Ring(batch_bytes=64 << 20, batch_frames=1 << 20, copy=False, columns=columns, slots=slots)
+    return offs, lens
+
+
+def e2e_ring_rate(sh, seconds=3.0, columns=None, slots=None):
+    """Producer-inclusive rate: frames copied into the pinned ring
+    (pnetgpu_ring_push_many: the DataLinkReceiver::next() consumer), shipped,
+    verified and the record columns copied back (rotating slots: one filling,
+    one held by the consumer, the rest in flight)."""
+    columns = columns or lp.IPV4_COLUMNS
+    w = sh.w
+    offs, lens = _ring_source(sh)
+    ring = lp.Ring(batch_bytes=64 << 20, batch_frames=1 << 20, copy=False, columns=columns, slots=slots,
+                   stage_times=True)
     nslots = ring.slots
     frames = nbytes = nb = 0
     t0 = time.perf_counter()
@@ -369,13 +455,15 @@ def e2e_ring_rate(sh, seconds=3.0, columns=None, slots=None):
         nbytes += b.counters["bytes"]          # the GPU counted them
         nb += 1
     el = time.perf_counter() - t0
+    stages = _ring_stages(ring, el)
     ring.close()
     rb = lp.engine.column_bytes(columns)
     return {"mpkts_s": round(frames / el / 1e6, 1), "gb_s": round(nbytes / el / 1e9, 2),
-            **_ring_link(frames, nbytes, el, rb, nb),
+            **_ring_link(frames, nbytes, el, rb, nb), "stages": stages,
             "note": "host frames pushed into the pinned ring with pnetgpu_ring_push_many (descriptors and "
-                    "source-adjacent frame copies split over up to 16 host threads), async H2D -> rx kernel -> D2H of "
-                    f"the record columns ({rb} B/frame: {', '.join(columns)}), {nslots} rotating slots of 1 Mi frames",
+                    f"non-temporal frame copies on a persistent pool of {stages['host_threads']} host threads), "
+                    f"async H2D -> rx kernel -> D2H of the record columns ({rb} B/frame: {', '.join(columns)}), "
+                    f"{nslots} rotating slots of 64 MiB / 1 Mi frames",
             "slots": nslots}
 
 
@@ -386,17 +474,12 @@ def e2e_zero_copy_rate(sh, seconds=3.0, columns=None, slots=None):
     record column copied back (rotating slots)."""
     columns = columns or lp.IPV4_COLUMNS
     w = sh.w
-    n = min(sh.n, 1 << 22)
-    if w.stride:
-        offs = np.arange(n, dtype=np.uint64) * np.uint64(w.stride)
-        lens = np.full(n, w.frame_len, dtype=np.uint32)
-        span = n * w.stride
-    else:
-        offs, lens = w.offsets[:n], w.lengths[:n]
-        span = int(offs[-1] + lens[-1])
+    offs, lens = _ring_source(sh)
+    span = int(offs[-1] + lens[-1])
     buf = w.buf[:span]
     reg = lp.HostRegistration(buf)
-    ring = lp.Ring(batch_bytes=64 << 20, batch_frames=1 << 20, copy=False, columns=columns, slots=slots)
+    ring = lp.Ring(batch_bytes=64 << 20, batch_frames=1 << 20, copy=False, columns=columns, slots=slots,
+                   stage_times=True)
     nslots = ring.slots
     frames = nbytes = nb = 0
     t0 = time.perf_counter()
@@ -412,15 +495,38 @@ def e2e_zero_copy_rate(sh, seconds=3.0, columns=None, slots=None):
             nbytes += b.counters["bytes"]          # the GPU counted them
             nb += 1
         el = time.perf_counter() - t0
+        stages = _ring_stages(ring, el)
     finally:
         ring.close()
         reg.close()
     rb = lp.engine.column_bytes(columns)
     return {"mpkts_s": round(frames / el / 1e6, 1), "gb_s": round(nbytes / el / 1e9, 2),
-            **_ring_link(frames, nbytes, el, rb, nb),
+            **_ring_link(frames, nbytes, el, rb, nb), "stages": stages,
             "note": "frames DMA'd straight from a registered host buffer (pnetgpu_ring_submit_region, no copy into "
                     f"the ring), rx kernel, D2H of the record columns ({rb} B/frame: {', '.join(columns)}; "
-                    f"pnetgpu_ring_set_columns), {nslots} rotating slots of 1 Mi frames", "slots": nslots}
+                    f"pnetgpu_ring_set_columns), {nslots} rotating slots of 64 MiB / 1 Mi frames", "slots": nslots}
+
+
+def pack_rate(sh, seconds=1.0):
+    """The ring producer's host ceiling on its own: pnetgpu_batch_pack of the same
+    frames into a 64-MiB pinned batch (the push_many pass, no GPU work)."""
+    offs, lens = _ring_source(sh)
+    dst = torch.empty(64 << 20, dtype=torch.uint8).pin_memory().numpy()
+    do = np.empty(len(offs), np.uint64)
+    dl = np.empty(len(offs), np.uint32)
+    frames = nbytes = 0
+    i = 0
+    lp.batch_pack(sh.w.buf, offs[:1 << 16], lens[:1 << 16], dst, do, dl)     # the pool starts
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        k, b = lp.batch_pack(sh.w.buf, offs[i:i + (1 << 20)], lens[i:i + (1 << 20)], dst, do, dl, check_bounds=False)
+        frames += k
+        nbytes += b
+        i = (i + k) % len(offs)
+    el = time.perf_counter() - t0
+    return {"gb_s": round(nbytes / el / 1e9, 2), "mpkts_s": round(frames / el / 1e6, 1),
+            "host_threads": lp.host_threads(),
+            "note": "pnetgpu_batch_pack into one 64-MiB pinned batch (descriptors + non-temporal copies), host only"}
 
 
 def time_launches(fn, steps, warmup, stream):
@@ -749,7 +855,10 @@ def launch_check(args, world, rank):
     bmin, bmax = shard_mod.all_reduce_min_max(float(lengths[lo:hi].sum()), "cpu")
     ok = int(ctr[0]) == n and int(ctr[1]) == int(lengths.sum()) and int(ctr[2]) == world * (world - 1) // 2
     if rank == 0:
+        coll = ({"backend": str(torch.distributed.get_backend()), "world_size": torch.distributed.get_world_size()}
+                if torch.distributed.is_initialized() else None)
         print(json.dumps({"metric": METRIC, "launch_check": True, "n_gpus": world, "world_size": world,
+                          "collective": coll,
                           "frames": int(ctr[0]), "bytes": int(ctr[1]), "wall_s": wall, "counters_ok": ok,
                           "shard_bytes_min": int(bmin), "shard_bytes_max": int(bmax)}),
               flush=True)
@@ -803,6 +912,12 @@ def main():
         torch.distributed.init_process_group(backend, timeout=datetime.timedelta(minutes=10))
         assert torch.distributed.get_world_size() == world
 
+    collective = None
+    if dist_on:
+        collective = {"backend": str(torch.distributed.get_backend()),
+                      "world_size": torch.distributed.get_world_size(),
+                      "library": "RCCL" if str(torch.distributed.get_backend()) == "nccl" and torch.version.hip
+                      else str(torch.distributed.get_backend())}
     names = [w for w in args.workloads.split(",") if w]
     results = {}
     primary = names[0]
@@ -903,6 +1018,9 @@ def main():
                 "alg_bytes_per_launch": sh.alg_bytes,
             },
             "counters_ok": p["counters_ok"],
+            # which collective library the reductions ran over, with how many
+            # ranks it reported (null at N = 1: no process group)
+            "collective": collective,
             "workloads": {},
         }
         for name, r in results.items():
@@ -957,12 +1075,21 @@ def main():
                 best["runs_link_gb_s"] = [x["link_gb_s"] for x in rs]
                 line[key] = best
             line["e2e_pcie_verify"] = e2e_rate(sh, device, columns=VERIFY_COLUMNS)
+            line["e2e_pack_only"] = pack_rate(sh)
             # the 1500-B batches over the same pipeline (the link's large-frame rate)
             for name in ("udp1500", "tcp1500"):
                 if name != primary and name in results and results[name]["sh"].w.buf is not None:
                     line["workloads"][name]["e2e_pcie"] = e2e_rate(results[name]["sh"], device)
                     if name == "udp1500":
                         line["workloads"][name]["e2e_zero_copy"] = e2e_zero_copy_rate(results[name]["sh"])
+            # configs[3] (IMIX, compact descriptors up) and configs[4] (9000-B
+            # jumbo frames, ~7,450 per 64-MiB ring batch) through all three producers
+            for name in ("imix", "udp6_jumbo"):
+                if name != primary and name in results and results[name]["sh"].w.buf is not None:
+                    wsh = results[name]["sh"]
+                    line["workloads"][name]["e2e_pcie"] = e2e_rate(wsh, device)
+                    line["workloads"][name]["e2e_zero_copy"] = e2e_zero_copy_rate(wsh, seconds=2.0)
+                    line["workloads"][name]["e2e_ring"] = e2e_ring_rate(wsh, seconds=2.0)
         print(json.dumps(line), flush=True)
     if dist_on:
         torch.distributed.barrier()

@@ -65,14 +65,56 @@ int  pnetgpu_ring_create_ex(pnetgpu_ctx* ctx, uint64_t batch_bytes, uint32_t bat
 uint32_t pnetgpu_ring_slots(const pnetgpu_ring* ring);
 void pnetgpu_ring_destroy(pnetgpu_ring* ring);
 
+/* Ring-only create flag (never passed to the kernel): time each batch's device
+ * stages with HIP events (H2D of frames + descriptors, receive kernel, D2H of
+ * the records), summed in pnetgpu_ring_stats. Costs four event records a batch. */
+#define PNETGPU_RING_STAGE_TIMES   0x10000u
+
+/* Where a ring's time went, summed since creation or the last reset. Host times
+ * are wall time on the calling thread inside the named calls; device times are
+ * per-batch stage durations on the slot streams (they overlap across slots). */
+typedef struct pnetgpu_ring_stats {
+    uint64_t batches;         /* batches shipped (submit / submit_region)                     */
+    uint64_t frames;          /* frames in them                                               */
+    uint64_t bytes;           /* bytes shipped host -> device (the frame spans)               */
+    uint64_t push_ns;         /* inside pnetgpu_ring_push_many: descriptors + copies          */
+    uint64_t submit_ns;       /* inside submit / submit_region: enqueueing H2D, kernel, D2H   */
+    uint64_t wait_ns;         /* inside pnetgpu_ring_wait, blocked on the oldest batch        */
+    uint64_t timed_batches;   /* batches whose device stages were timed                       */
+    double   h2d_ms;          /* PNETGPU_RING_STAGE_TIMES only: H2D of frames + descriptors   */
+    double   kernel_ms;       /*   the receive kernel                                         */
+    double   d2h_ms;          /*   D2H of counters + record columns                           */
+    uint32_t host_threads;    /* threads push_many's passes use (pnetgpu_host_threads)        */
+    uint32_t reserved;
+} pnetgpu_ring_stats;
+int pnetgpu_ring_stats_get(const pnetgpu_ring* ring, pnetgpu_ring_stats* out);
+/* Zero every sum (host_threads is kept). */
+int pnetgpu_ring_stats_reset(pnetgpu_ring* ring);
+
+/* Host threads the producers' parallel passes use, the caller included:
+ * PNETGPU_HOST_THREADS if set (1..64), else min(16, CPUs in the process's
+ * affinity mask, its cgroup CPU quota rounded down). The workers are created
+ * once per process, on the first large pass, and sleep between passes. */
+uint32_t pnetgpu_host_threads(void);
+
+/* Host batch builder without a ring (no HIP call): copies frames
+ * buf[offsets[i], +lengths[i]) back to back into dst (dst_cap bytes), writing
+ * dst_offsets[i] / dst_lengths[i], and stops at n frames or when the next frame
+ * does not fit: *packed frames, *packed_bytes bytes. PNETGPU_EFULL if the first
+ * frame alone exceeds dst_cap. The same pass as pnetgpu_ring_push_many, for a
+ * caller staging batches in its own pinned memory for pnetgpu_rx_process. */
+int pnetgpu_batch_pack(const uint8_t* buf, const uint64_t* offsets, const uint32_t* lengths, uint64_t n,
+                       uint8_t* dst, uint64_t dst_cap, uint64_t* dst_offsets, uint32_t* dst_lengths,
+                       uint64_t* packed, uint64_t* packed_bytes);
+
 /* Copy one frame into the filling batch: 0, PNETGPU_EFULL or PNETGPU_EBUSY. */
 int pnetgpu_ring_push(pnetgpu_ring* ring, const uint8_t* frame, uint32_t len);
 /* Copy n frames (frame i = buf[offsets[i], +lengths[i]) on the host) until the
  * batch is full; *pushed = how many were taken (may be < n: then submit).
  * Frames adjacent in buf are copied by one memcpy, and pushes of >= 2^16 frames
- * are split over up to 16 host threads (descriptors, the cut where the batch
- * fills and the copies); the batch holds the same frames in the same order as
- * n single pushes would. */
+ * are split over pnetgpu_host_threads() threads of a persistent pool
+ * (descriptors, the cut where the batch fills and the copies); the batch holds
+ * the same frames in the same order as n single pushes would. */
 int pnetgpu_ring_push_many(pnetgpu_ring* ring, const uint8_t* buf, const uint64_t* offsets,
                            const uint32_t* lengths, uint64_t n, uint64_t* pushed);
 /* Ship the filling batch (no-op returning 0 with *id = UINT64_MAX if empty). */

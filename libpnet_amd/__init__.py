@@ -7,7 +7,7 @@ include/pnetgpu.h); this package is its Python host binding.
 """
 from ._lib import DEFS, LIB_PATH, PnetGpuError, lib  # noqa: F401  (fails loudly if the .so is absent)
 from . import packet, synth  # noqa: F401  (packet: pnet_packet's function names)
-from .ring import HostRegistration, Ring, pcap_frames, pcap_index, pcap_info  # noqa: F401
+from .ring import HostRegistration, Ring, batch_pack, host_threads, pcap_frames, pcap_index, pcap_info  # noqa: F401
 from .afpacket import AfPacket, tpacket3_walk  # noqa: F401
 from .views import frame_view  # noqa: F401
 from .engine import (ALL_COLUMNS, COUNTER_NAMES, DESC_COMPACT, DESC_HINT_JUMBO, DESC_HINT_LARGE, desc_size_hint, FIELD_COLUMNS, IPV4_COLUMNS, RECORD_COLUMNS,  # noqa: F401

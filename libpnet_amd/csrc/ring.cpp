@@ -3,15 +3,16 @@
 // capture-file readers that feed it are in pcap.cpp).
 #include <hip/hip_runtime.h>
 
+#include <time.h>
+
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
 #include <deque>
 #include <new>
-#include <atomic>
-#include <thread>
 #include <vector>
 
+#include "host_pool.h"
 #include "pnetgpu.h"
 #include "pnetgpu_ring.h"
 #include "rx_internal.h"
@@ -29,6 +30,19 @@ constexpr uint32_t kColBytes[kNumCols] = {2, 2, 2, 2, 1, 1, 2, 2, 2, 2, 4, 4, 16
                                           8, 8, 1, 1, 1, 1, 2, 2, 1, 2, 1, 4, 2, 2, 4, 4, 1, 1, 1, 2, 2, 2};
 
 enum SlotState { kFree = 0, kFilling, kInFlight, kHeld };
+
+uint64_t now_ns() {
+    timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
+}
+
+// what one pack pass took: frames, bytes, and the size-hint statistics
+struct PackStats {
+    uint64_t frames = 0, bytes = 0;
+    uint32_t max_len = 0;
+    uint64_t n_large = 0, jumbo_bytes = 0;
+};
 
 struct Slot {
     uint8_t* h_frames = nullptr;
@@ -54,6 +68,10 @@ struct Slot {
     uint64_t rec_bytes = 0;
     hipStream_t stream = nullptr;
     hipEvent_t done = nullptr;
+    // PNETGPU_RING_STAGE_TIMES: timing events before the H2D, after it, after
+    // the kernel and after the D2H
+    hipEvent_t stage[4] = {};
+    bool timed = false;                      // this batch recorded them
     uint32_t n = 0;
     uint64_t bytes = 0;
     uint64_t id = 0;
@@ -93,6 +111,7 @@ struct pnetgpu_ring {
     int held = -1;
     std::deque<int> inflight;
     uint64_t next_id = 0;
+    pnetgpu_ring_stats stats{};
 };
 
 
@@ -108,6 +127,8 @@ static void free_slot(Slot& s) {
     if (s.d_rec) (void)hipFree(s.d_rec);
     if (s.h_rec) (void)hipHostFree(s.h_rec);
     if (s.done) (void)hipEventDestroy(s.done);
+    for (hipEvent_t e : s.stage)
+        if (e) (void)hipEventDestroy(e);
     if (s.stream) (void)hipStreamDestroy(s.stream);
     s = Slot{};
 }
@@ -163,7 +184,8 @@ int pnetgpu_ring_create_ex(pnetgpu_ctx* ctx, uint64_t batch_bytes, uint32_t batc
     pnetgpu::set_last_hip_error(0);
     if (!ctx || !out || batch_bytes == 0 || batch_frames == 0) return PNETGPU_EINVAL;
     if (nslots < PNETGPU_RING_MIN_SLOTS || nslots > (uint32_t)kMaxSlots) return PNETGPU_EINVAL;
-    if (flags & ~(PNETGPU_RX_VLAN | PNETGPU_RX_IPV6_EXT | PNETGPU_RX_L3)) return PNETGPU_EINVAL;
+    if (flags & ~(PNETGPU_RX_VLAN | PNETGPU_RX_IPV6_EXT | PNETGPU_RX_L3 | PNETGPU_RING_STAGE_TIMES))
+        return PNETGPU_EINVAL;
     *out = nullptr;
     auto* r = new (std::nothrow) pnetgpu_ring;
     if (!r) return PNETGPU_ENOMEM;
@@ -191,6 +213,8 @@ int pnetgpu_ring_create_ex(pnetgpu_ctx* ctx, uint64_t batch_bytes, uint32_t batc
              hipMalloc((void**)&s.d_len, 4ull * batch_frames) == hipSuccess &&
              hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking) == hipSuccess &&
              hipEventCreateWithFlags(&s.done, hipEventDisableTiming) == hipSuccess;
+        for (int e = 0; e < 4 && ok && (flags & PNETGPU_RING_STAGE_TIMES); ++e)
+            ok = hipEventCreate(&s.stage[e]) == hipSuccess;
         if (ok) ok = alloc_rec(s, rec_capacity(batch_frames, kDefaultCols));
         if (ok) std::memset(s.h_frames + batch_bytes, 0, 32);
     }
@@ -200,6 +224,7 @@ int pnetgpu_ring_create_ex(pnetgpu_ctx* ctx, uint64_t batch_bytes, uint32_t batc
         return PNETGPU_ENOMEM;
     }
     r->filling = take_free_slot(r);
+    r->stats.host_threads = pnetgpu::host_threads();
     *out = r;
     return PNETGPU_OK;
 }
@@ -240,150 +265,157 @@ int pnetgpu_ring_push(pnetgpu_ring* r, const uint8_t* frame, uint32_t len) {
     return PNETGPU_OK;
 }
 
+// Packs frames buf[offsets[i], +lengths[i]), i < m, back to back into dst from
+// byte `at` (at most room_b bytes), with their descriptors at index 0 of the
+// given arrays (off32 / len16 may be NULL): the longest prefix that fits, the
+// same cut as pushing one frame at a time. Returns the frames taken (0: the
+// first frame alone does not fit) and fills *st.
+//
+// Large packs run on the persistent host pool (host_pool.h), descriptors
+// included: one thread's copy into pinned memory tops out far below the PCIe
+// link the batch is headed for, and a serial descriptor pass capped 64-B frames
+// at ~330 Mframes/s end to end. Pass 1 sums each chunk's lengths; the caller
+// finds the cut (all m frames, or the first chunk whose frames overflow, scanned
+// to the exact frame); when the cut falls inside the push, pass 2 re-splits the
+// frames below it evenly (1500-B frames fill a 64-MiB slot within the first of
+// 16 chunks of a 2^20-frame push); the last pass writes every chunk's
+// descriptors and copies its frames at its prefix offset (runs of frames
+// adjacent in the source in one non-temporal copy).
+// a pack of fewer than 2^16 frames still copies in parallel from this many bytes
+constexpr uint64_t kParallelCopyMin = 4ull << 20;
+
+static uint64_t pack_frames(const uint8_t* buf, const uint64_t* offsets, const uint32_t* lengths, uint64_t m,
+                            uint64_t room_b, uint8_t* dst, uint64_t at, uint64_t* off64, uint32_t* len32,
+                            uint32_t* off32, uint16_t* len16, PackStats* st) {
+    *st = PackStats{};
+    auto fill_range = [&](uint64_t lo, uint64_t hi, uint64_t o) {
+        PackStats cs;
+        for (uint64_t i = lo; i < hi; ++i) {
+            const uint32_t len = lengths[i];
+            off64[i] = o;
+            len32[i] = len;
+            if (off32) off32[i] = (uint32_t)o;
+            if (len16) len16[i] = (uint16_t)len;
+            cs.max_len = std::max(cs.max_len, len);
+            cs.n_large += len >= pnetgpu::kHintLargeMin;
+            cs.jumbo_bytes += len >= pnetgpu::kHintJumboMin ? len : 0;
+            o += len;
+        }
+        uint64_t i = lo;
+        while (i < hi) {
+            uint64_t j = i + 1;
+            while (j < hi && offsets[j] == offsets[j - 1] + lengths[j - 1]) ++j;
+            const uint64_t run = off64[j - 1] + lengths[j - 1] - off64[i];
+            if (run) pnetgpu::stage_copy(dst + off64[i], buf + offsets[i], run);
+            i = j;
+        }
+        return cs;
+    };
+    const unsigned threads = pnetgpu::host_threads();
+    uint64_t k = 0, bytes = 0, span = 0;   // the cut, its bytes, the frame range the chunks split
+    unsigned nt = threads;
+    std::vector<uint64_t> csum;
+    if (m < (1u << 16) || threads <= 1) {
+        // few frames: the cut in one serial scan of the lengths; the copies
+        // still go parallel when they are large (7,456 jumbo frames fill a
+        // 64-MiB slot, one thread's copy of which trails the link)
+        while (k < m && lengths[k] <= room_b - bytes) bytes += lengths[k++];
+        if (k == 0) return 0;
+        nt = bytes >= kParallelCopyMin ? (unsigned)std::min<uint64_t>(threads, (k + 15) / 16) : 1u;
+        if (nt <= 1) {
+            *st = fill_range(0, k, at);
+            st->frames = k;
+            st->bytes = bytes;
+            return k;
+        }
+        span = k;
+        csum.assign(nt, 0);
+        for (unsigned t = 0; t < nt; ++t)
+            for (uint64_t i = k * t / nt, hi = k * (t + 1) / nt; i < hi; ++i) csum[t] += lengths[i];
+    } else {
+        csum.assign(nt, 0);
+        pnetgpu::parallel_run(nt, [&](unsigned t) {
+            uint64_t sum = 0;
+            for (uint64_t i = m * t / nt, hi = m * (t + 1) / nt; i < hi; ++i) sum += lengths[i];
+            csum[t] = sum;
+        });
+        unsigned c = 0;
+        while (c < nt && bytes + csum[c] <= room_b) bytes += csum[c++];
+        k = m;
+        if (c < nt) {                                  // chunk c overflows: its exact cut
+            k = m * c / nt;
+            while (lengths[k] <= room_b - bytes) bytes += lengths[k++];
+        }
+        if (k == 0) return 0;
+        span = m;
+        if (k < m && k >= (uint64_t)nt * 64) {         // re-split [0, k) evenly
+            span = k;
+            pnetgpu::parallel_run(nt, [&](unsigned t) {
+                uint64_t sum = 0;
+                for (uint64_t i = k * t / nt, hi = k * (t + 1) / nt; i < hi; ++i) sum += lengths[i];
+                csum[t] = sum;
+            });
+        }
+    }
+    std::vector<PackStats> cst(nt);
+    pnetgpu::parallel_run(nt, [&](unsigned t) {
+        const uint64_t lo = span * t / nt, hi = std::min(span * (t + 1) / nt, k);
+        if (lo >= hi) return;
+        uint64_t o = at;
+        for (unsigned u = 0; u < t; ++u) o += csum[u];
+        cst[t] = fill_range(lo, hi, o);
+    });
+    for (unsigned u = 0; u < nt; ++u) {
+        st->max_len = std::max(st->max_len, cst[u].max_len);
+        st->n_large += cst[u].n_large;
+        st->jumbo_bytes += cst[u].jumbo_bytes;
+    }
+    st->frames = k;
+    st->bytes = bytes;
+    return k;
+}
+
 int pnetgpu_ring_push_many(pnetgpu_ring* r, const uint8_t* buf, const uint64_t* offsets, const uint32_t* lengths,
                            uint64_t n, uint64_t* pushed) {
     if (!r || !pushed || (n && (!buf || !offsets || !lengths))) return PNETGPU_EINVAL;
     *pushed = 0;
     if (n == 0) return PNETGPU_OK;
     if (r->filling < 0 && (r->filling = take_free_slot(r)) < 0) return PNETGPU_EBUSY;
+    const uint64_t t0 = now_ns();
     Slot& s = r->slots[r->filling];
-    // descriptors of the frames that fit, in order (the same cut as pushing one by one)
-    const uint64_t room_f = r->cap_frames - s.n;
-    const uint64_t room_b = r->cap_bytes - s.bytes;
-    const uint64_t m = std::min(n, room_f);
-    uint8_t* dst = s.h_frames;
-    // frames [lo, hi) with their slot byte offsets starting at `at`: descriptors,
-    // then the bytes (runs of frames adjacent in the source go in one memcpy);
-    // returns the chunk's largest length and its size-hint counts
-    struct Stats {
-        uint32_t mx = 0;
-        uint64_t large = 0, jumbo = 0;
-    };
-    auto fill_range = [&](uint64_t lo, uint64_t hi, uint64_t at) {
-        Stats st;
-        uint64_t o = at;
-        for (uint64_t i = lo; i < hi; ++i) {
-            const uint32_t len = lengths[i];
-            s.h_off[s.n + i] = o;
-            s.h_len[s.n + i] = len;
-            s.h_off32[s.n + i] = (uint32_t)o;
-            s.h_len16[s.n + i] = (uint16_t)len;
-            st.mx = std::max(st.mx, len);
-            st.large += len >= pnetgpu::kHintLargeMin;
-            st.jumbo += len >= pnetgpu::kHintJumboMin ? len : 0;
-            o += len;
-        }
-        const uint64_t* doff = s.h_off + s.n;
-        uint64_t i = lo;
-        while (i < hi) {
-            uint64_t j = i + 1;
-            while (j < hi && offsets[j] == offsets[j - 1] + lengths[j - 1]) ++j;
-            const uint64_t run = doff[j - 1] + lengths[j - 1] - doff[i];
-            if (run) std::memcpy(dst + doff[i], buf + offsets[i], run);
-            i = j;
-        }
-        return st;
-    };
-    // Large pushes are split over host threads, descriptors included: one
-    // thread's memcpy into pinned memory tops out far below the PCIe link the
-    // batch is headed for, and a serial descriptor pass capped 64-B frames at
-    // ~330 Mframes/s end to end. Pass 1 sums each chunk's lengths; the last
-    // thread to finish finds the cut (all m frames, or the first chunk whose
-    // frames overflow the slot, scanned to the exact frame: the same cut as
-    // single pushes), and pass 2 fills every chunk's frames below the cut at
-    // its prefix offset.
-    uint64_t k = 0, bytes = 0;
-    unsigned nt = 1;
-    if (m >= (1u << 16)) nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-    bool done = false;
-    if (nt > 1) {
-        std::vector<uint64_t> csum(nt, 0);
-        std::vector<Stats> cst(nt);
-        std::atomic<unsigned> arrived{0};
-        uint64_t kcut = 0, bcut = 0;       // written by the decider before the release below
-        std::atomic<int> start{0};   // 0: wait, 1: go, 2: abandoned (a thread could not be created)
-        // barrier 1 (the cut) and, when the push overflows the slot, barrier 2
-        // (the frames below the cut re-split evenly: otherwise one chunk would
-        // hold all of them — 1500-B frames fill a 64-MiB slot within the first
-        // of 16 chunks of a 2^20-frame push)
-        std::atomic<unsigned> arrived2{0};
-        bool rechunk = false;
-        auto work = [&](unsigned t) {
-            while (start.load(std::memory_order_acquire) == 0) std::this_thread::yield();
-            if (start.load(std::memory_order_acquire) == 2) return;
-            uint64_t lo = m * t / nt, hi = m * (t + 1) / nt;
-            uint64_t sum = 0;
-            for (uint64_t i = lo; i < hi; ++i) sum += lengths[i];
-            csum[t] = sum;
-            if (arrived.fetch_add(1) + 1 == nt) {   // the last to arrive decides
-                uint64_t cum = 0;
-                unsigned c = 0;
-                while (c < nt && cum + csum[c] <= room_b) cum += csum[c++];
-                uint64_t kk = m;
-                if (c < nt) {                       // chunk c overflows: its exact cut
-                    kk = m * c / nt;
-                    while (lengths[kk] <= room_b - cum) cum += lengths[kk++];
-                }
-                kcut = kk;
-                bcut = cum;
-                rechunk = kk < m && kk >= (uint64_t)nt * 64;
-                arrived.fetch_add(1, std::memory_order_release);   // == nt + 1: released
-            }
-            while (arrived.load(std::memory_order_acquire) <= nt) std::this_thread::yield();
-            if (rechunk) {                          // [0, kcut) in nt even chunks, their sums again
-                lo = kcut * t / nt;
-                hi = kcut * (t + 1) / nt;
-                sum = 0;
-                for (uint64_t i = lo; i < hi; ++i) sum += lengths[i];
-                csum[t] = sum;
-                arrived2.fetch_add(1, std::memory_order_acq_rel);
-                while (arrived2.load(std::memory_order_acquire) < nt) std::this_thread::yield();
-            }
-            if (lo >= kcut) return;
-            uint64_t at = s.bytes;
-            for (unsigned c = 0; c < t; ++c) at += csum[c];
-            cst[t] = fill_range(lo, std::min(hi, kcut), at);
-        };
-        // no exception may cross the C-ABI: a thread that cannot be created
-        // (process/thread limits) releases the ones already started, which
-        // return at once, and the push falls back to the serial pass below
-        std::vector<std::thread> th;
-        bool started = true;
-        try {
-            th.reserve(nt - 1);
-            for (unsigned t = 1; t < nt; ++t) th.emplace_back(work, t);
-        } catch (...) {
-            started = false;
-        }
-        start.store(started ? 1 : 2, std::memory_order_release);
-        if (started) work(0);
-        for (auto& t : th) t.join();
-        if (started) {
-            if (kcut == 0) return PNETGPU_EFULL;
-            k = kcut;
-            bytes = bcut;
-            for (unsigned c = 0; c < nt; ++c) {
-                s.max_len = std::max(s.max_len, cst[c].mx);
-                s.n_large += cst[c].large;
-                s.jumbo_bytes += cst[c].jumbo;
-            }
-            done = true;
-        }
-    }
-    if (!done) {
-        while (k < m && lengths[k] <= room_b - bytes) bytes += lengths[k++];
-        if (k == 0) return PNETGPU_EFULL;
-        const Stats st = fill_range(0, k, s.bytes);
-        s.max_len = std::max(s.max_len, st.mx);
-        s.n_large += st.large;
-        s.jumbo_bytes += st.jumbo;
-    }
+    PackStats st;
+    const uint64_t k = pack_frames(buf, offsets, lengths, std::min<uint64_t>(n, r->cap_frames - s.n),
+                                   r->cap_bytes - s.bytes, s.h_frames, s.bytes, s.h_off + s.n, s.h_len + s.n,
+                                   s.h_off32 + s.n, s.h_len16 + s.n, &st);
+    r->stats.push_ns += now_ns() - t0;
+    if (k == 0) return PNETGPU_EFULL;
+    s.max_len = std::max(s.max_len, st.max_len);
+    s.n_large += st.n_large;
+    s.jumbo_bytes += st.jumbo_bytes;
     s.n += k;
-    s.bytes += bytes;
-    s.frame_bytes += bytes;
+    s.bytes += st.bytes;
+    s.frame_bytes += st.bytes;
     *pushed = k;
     return PNETGPU_OK;
 }
+
+int pnetgpu_batch_pack(const uint8_t* buf, const uint64_t* offsets, const uint32_t* lengths, uint64_t n, uint8_t* dst,
+                       uint64_t dst_cap, uint64_t* dst_offsets, uint32_t* dst_lengths, uint64_t* packed,
+                       uint64_t* packed_bytes) {
+    if (!packed || !packed_bytes || (n && (!buf || !offsets || !lengths || !dst || !dst_offsets || !dst_lengths)))
+        return PNETGPU_EINVAL;
+    *packed = *packed_bytes = 0;
+    if (n == 0) return PNETGPU_OK;
+    PackStats st;
+    const uint64_t k = pack_frames(buf, offsets, lengths, n, dst_cap, dst, 0, dst_offsets, dst_lengths, nullptr,
+                                   nullptr, &st);
+    if (k == 0) return PNETGPU_EFULL;
+    *packed = k;
+    *packed_bytes = st.bytes;
+    return PNETGPU_OK;
+}
+
+uint32_t pnetgpu_host_threads(void) { return pnetgpu::host_threads(); }
 
 // Ship slot s: H2D of the frames from `src` (the slot's pinned batch, or a
 // caller region for submit_region) and of the descriptors, receive kernel, D2H
@@ -393,19 +425,18 @@ static int ship_slot(pnetgpu_ring* r, Slot& s, const uint8_t* src, uint64_t* id)
     const hipStream_t st = s.stream;
     // compact descriptors (6 B/frame over PCIe instead of 12) whenever they can
     // describe the batch; the full ones stay on the host for the waited batch view
-#ifdef PNETGPU_RING_FULL_DESC   // A/B build only (tools/): always the u64/u32 form
-    const bool compact = false;
-#else
     const bool compact = s.bytes <= UINT32_MAX && s.max_len <= UINT16_MAX;
-#endif
     const void* h_off = compact ? (const void*)s.h_off32 : (const void*)s.h_off;
     const void* h_len = compact ? (const void*)s.h_len16 : (const void*)s.h_len;
+    s.timed = (r->flags & PNETGPU_RING_STAGE_TIMES) != 0;
+    if (s.timed && hipEventRecord(s.stage[0], st) != hipSuccess) return pnetgpu::hip_fail(hipGetLastError());
     // granule rule: the tail past the last frame is readable (32 zero bytes)
     if (hipMemcpyAsync(s.d_frames, src, s.bytes, hipMemcpyHostToDevice, st) != hipSuccess ||
         (src != s.h_frames && hipMemsetAsync(s.d_frames + s.bytes, 0, 32, st) != hipSuccess) ||
         hipMemcpyAsync(s.d_off, h_off, (compact ? 4ull : 8ull) * s.n, hipMemcpyHostToDevice, st) != hipSuccess ||
         hipMemcpyAsync(s.d_len, h_len, (compact ? 2ull : 4ull) * s.n, hipMemcpyHostToDevice, st) != hipSuccess ||
-        hipMemsetAsync(s.d_rec, 0, 8ull * PNETGPU_NCOUNTERS, st) != hipSuccess)
+        hipMemsetAsync(s.d_rec, 0, 8ull * PNETGPU_NCOUNTERS, st) != hipSuccess ||
+        (s.timed && hipEventRecord(s.stage[1], st) != hipSuccess))
         return pnetgpu::hip_fail(hipGetLastError());
     pnetgpu_batch b{};
     b.data = s.d_frames;
@@ -415,7 +446,7 @@ static int ship_slot(pnetgpu_ring* r, Slot& s, const uint8_t* src, uint64_t* id)
     b.lengths = s.d_len;
     // the batch's size mix picks the kernel's tail shape (frames of >= 768 B:
     // MTU; mostly jumbo bytes: jumbo; else mixed); records are the same
-    b.flags = r->flags | (compact ? PNETGPU_DESC_COMPACT : 0u) |
+    b.flags = (r->flags & ~PNETGPU_RING_STAGE_TIMES) | (compact ? PNETGPU_DESC_COMPACT : 0u) |
               pnetgpu::desc_size_hint(s.n, s.frame_bytes, s.n_large, s.jumbo_bytes);
     pnetgpu_rx_columns c{};
     uint64_t at = 8ull * PNETGPU_NCOUNTERS;          // the counters lead the record block
@@ -431,9 +462,13 @@ static int ship_slot(pnetgpu_ring* r, Slot& s, const uint8_t* src, uint64_t* id)
     int rc = pnetgpu_rx_process(r->ctx, &b, &c, st);
     if (rc) return rc;
     s.col_mask = r->col_mask;
-    if (hipMemcpyAsync(s.h_rec, s.d_rec, at, hipMemcpyDeviceToHost, st) != hipSuccess ||   // counters + records
-        hipEventRecord(s.done, st) != hipSuccess)
+    if ((s.timed && hipEventRecord(s.stage[2], st) != hipSuccess) ||
+        hipMemcpyAsync(s.h_rec, s.d_rec, at, hipMemcpyDeviceToHost, st) != hipSuccess ||   // counters + records
+        (s.timed && hipEventRecord(s.stage[3], st) != hipSuccess) || hipEventRecord(s.done, st) != hipSuccess)
         return pnetgpu::hip_fail(hipGetLastError());
+    r->stats.batches += 1;
+    r->stats.frames += s.n;
+    r->stats.bytes += s.bytes;
     s.state = kInFlight;
     s.id = r->next_id++;
     if (id) *id = s.id;
@@ -450,7 +485,10 @@ int pnetgpu_ring_submit(pnetgpu_ring* r, uint64_t* id) {
     Slot& s = r->slots[r->filling];
     if (s.n == 0) return PNETGPU_OK;
     s.frames_view = s.h_frames;
-    return ship_slot(r, s, s.h_frames, id);
+    const uint64_t t0 = now_ns();
+    const int rc = ship_slot(r, s, s.h_frames, id);
+    r->stats.submit_ns += now_ns() - t0;
+    return rc;
 }
 
 int pnetgpu_ring_submit_region(pnetgpu_ring* r, const uint8_t* base, const uint64_t* offsets, const uint32_t* lengths,
@@ -490,7 +528,9 @@ int pnetgpu_ring_submit_region(pnetgpu_ring* r, const uint8_t* base, const uint6
     s.n_large = large;
     s.jumbo_bytes = jumbo;
     s.frames_view = base + o0;
+    const uint64_t t0 = now_ns();
     const int rc = ship_slot(r, s, base + o0, id);
+    r->stats.submit_ns += now_ns() - t0;
     if (rc) {   // nothing shipped: the slot is empty again (its pinned batch never held these frames)
         s.n = 0;
         s.bytes = s.frame_bytes = s.n_large = s.jumbo_bytes = 0;
@@ -522,7 +562,22 @@ int pnetgpu_ring_wait(pnetgpu_ring* r, pnetgpu_ring_batch* out) {
     const int i = r->inflight.front();
     Slot& s = r->slots[i];
     // a failed wait leaves the batch in flight (the next wait tries it again)
-    if (const hipError_t e = hipEventSynchronize(s.done)) return pnetgpu::hip_fail(e);
+    const uint64_t t0 = now_ns();
+    const hipError_t e = hipEventSynchronize(s.done);
+    r->stats.wait_ns += now_ns() - t0;
+    if (e) return pnetgpu::hip_fail(e);
+    if (s.timed) {
+        float ms[3] = {0, 0, 0};
+        bool ok = true;
+        for (int k = 0; k < 3 && ok; ++k) ok = hipEventElapsedTime(&ms[k], s.stage[k], s.stage[k + 1]) == hipSuccess;
+        if (ok) {
+            r->stats.h2d_ms += ms[0];
+            r->stats.kernel_ms += ms[1];
+            r->stats.d2h_ms += ms[2];
+            r->stats.timed_batches += 1;
+        }
+        s.timed = false;
+    }
     r->inflight.pop_front();
     s.state = kHeld;
     r->held = i;
@@ -554,6 +609,20 @@ int pnetgpu_ring_set_columns(pnetgpu_ring* r, uint64_t column_mask) {
             if (s->rec_cap < need && !alloc_rec(*s, need)) return PNETGPU_ENOMEM;
     }
     r->col_mask = column_mask;
+    return PNETGPU_OK;
+}
+
+int pnetgpu_ring_stats_get(const pnetgpu_ring* r, pnetgpu_ring_stats* out) {
+    if (!r || !out) return PNETGPU_EINVAL;
+    *out = r->stats;
+    return PNETGPU_OK;
+}
+
+int pnetgpu_ring_stats_reset(pnetgpu_ring* r) {
+    if (!r) return PNETGPU_EINVAL;
+    const uint32_t threads = r->stats.host_threads;
+    r->stats = pnetgpu_ring_stats{};
+    r->stats.host_threads = threads;
     return PNETGPU_OK;
 }
 

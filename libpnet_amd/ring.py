@@ -16,9 +16,23 @@ from .engine import COLUMNS, COUNTER_NAMES, context
 EFULL, EBUSY, EEMPTY = DEFS["PNETGPU_EFULL"], DEFS["PNETGPU_EBUSY"], DEFS["PNETGPU_EEMPTY"]
 
 
+STAGE_TIMES = DEFS["PNETGPU_RING_STAGE_TIMES"]
+
+
 class RingBatch(ctypes.Structure):
     _fields_ = [("id", ctypes.c_uint64), ("n_frames", ctypes.c_uint64), ("frames", ctypes.c_void_p),
                 ("offsets", ctypes.c_void_p), ("lengths", ctypes.c_void_p), ("cols", RxColumns)]
+
+
+class RingStats(ctypes.Structure):
+    """pnetgpu_ring_stats (include/pnetgpu_ring.h)."""
+    _fields_ = [("batches", ctypes.c_uint64), ("frames", ctypes.c_uint64), ("bytes", ctypes.c_uint64),
+                ("push_ns", ctypes.c_uint64), ("submit_ns", ctypes.c_uint64), ("wait_ns", ctypes.c_uint64),
+                ("timed_batches", ctypes.c_uint64), ("h2d_ms", ctypes.c_double), ("kernel_ms", ctypes.c_double),
+                ("d2h_ms", ctypes.c_double), ("host_threads", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
+
+    def as_dict(self):
+        return {name: getattr(self, name) for name, _ in self._fields_ if name != "reserved"}
 
 
 def _setup():
@@ -59,6 +73,14 @@ def _setup():
     lib.pnetgpu_pcap_scan.argtypes = [vp, u64, ctypes.POINTER(u64), vp, vp, u64, ctypes.POINTER(u64)]
     lib.pnetgpu_pcap_info.restype = i32
     lib.pnetgpu_pcap_info.argtypes = [vp, u64, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)]
+    lib.pnetgpu_ring_stats_get.restype = i32
+    lib.pnetgpu_ring_stats_get.argtypes = [vp, ctypes.POINTER(RingStats)]
+    lib.pnetgpu_ring_stats_reset.restype = i32
+    lib.pnetgpu_ring_stats_reset.argtypes = [vp]
+    lib.pnetgpu_host_threads.restype = u32
+    lib.pnetgpu_host_threads.argtypes = []
+    lib.pnetgpu_batch_pack.restype = i32
+    lib.pnetgpu_batch_pack.argtypes = [vp, vp, vp, u64, vp, u64, vp, vp, ctypes.POINTER(u64), ctypes.POINTER(u64)]
 
 
 _setup()
@@ -132,14 +154,46 @@ class Batch:
         return self._cache["records"]
 
 
+def host_threads():
+    """Threads the producers' parallel passes use, the caller included (pnetgpu_host_threads)."""
+    return int(lib.pnetgpu_host_threads())
+
+
+def batch_pack(buf, offsets, lengths, dst, dst_offsets, dst_lengths, check_bounds=True):
+    """pnetgpu_batch_pack: frames buf[offsets[i], +lengths[i]) back to back into dst
+    (host arrays, no GPU), descriptors into dst_offsets / dst_lengths; returns
+    (frames packed, bytes packed). Raises on PNETGPU_EFULL (first frame > dst).
+    check_bounds=False skips the O(n) numpy check that every frame lies inside
+    buf (for callers whose descriptors come from a scan of buf itself)."""
+    buf = np.ascontiguousarray(buf, np.uint8)
+    offsets = np.ascontiguousarray(offsets, np.uint64)
+    lengths = np.ascontiguousarray(lengths, np.uint32)
+    n = len(offsets)
+    for a, dt in ((dst, np.uint8), (dst_offsets, np.uint64), (dst_lengths, np.uint32)):
+        if a.dtype != dt or not a.flags.c_contiguous:
+            raise TypeError("dst arrays must be contiguous uint8 / uint64 / uint32")
+    if len(lengths) != n or len(dst_offsets) < n or len(dst_lengths) < n:
+        raise ValueError("offsets, lengths and the descriptor outputs must cover n frames")
+    if check_bounds and n and int((offsets + lengths).max()) > buf.size:
+        raise ValueError("a frame extends past buf")
+    k, b = ctypes.c_uint64(), ctypes.c_uint64()
+    check(lib.pnetgpu_batch_pack(ctypes.c_void_p(buf.ctypes.data), ctypes.c_void_p(offsets.ctypes.data),
+                                 ctypes.c_void_p(lengths.ctypes.data), n, ctypes.c_void_p(dst.ctypes.data), dst.size,
+                                 ctypes.c_void_p(dst_offsets.ctypes.data), ctypes.c_void_p(dst_lengths.ctypes.data),
+                                 ctypes.byref(k), ctypes.byref(b)), "pnetgpu_batch_pack")
+    return int(k.value), int(b.value)
+
+
 class Ring:
     """Pinned host batches -> asynchronous GPU verification (rotating slots: one
     filling, one held by the consumer, the rest in flight)."""
 
     def __init__(self, batch_bytes=64 << 20, batch_frames=1 << 18, device=0, copy=True, flags=0, columns=None,
-                 slots=None):
+                 slots=None, stage_times=False):
         """columns: names of the record columns to compute and copy back (default all);
-        slots: slot count (default PNETGPU_RING_DEFAULT_SLOTS)."""
+        slots: slot count (default PNETGPU_RING_DEFAULT_SLOTS); stage_times: time each
+        batch's H2D / kernel / D2H on the GPU (PNETGPU_RING_STAGE_TIMES, see stats())."""
+        flags |= STAGE_TIMES if stage_times else 0
         self.ctx = context(device)
         self.copy = copy
         h = ctypes.c_void_p()
@@ -165,6 +219,16 @@ class Ring:
             self.close()
         except Exception:
             pass
+
+    def stats(self):
+        """pnetgpu_ring_stats as a dict: host seconds inside push_many / submit /
+        wait, device stage sums (stage_times rings), batches, frames, bytes."""
+        st = RingStats()
+        check(lib.pnetgpu_ring_stats_get(self.h, ctypes.byref(st)), "pnetgpu_ring_stats_get")
+        return st.as_dict()
+
+    def reset_stats(self):
+        check(lib.pnetgpu_ring_stats_reset(self.h), "pnetgpu_ring_stats_reset")
 
     def _wait(self):
         rb = RingBatch()

@@ -118,12 +118,20 @@ def test_tuning_entry_points_without_gpu():
 
 def test_environment_read_only_at_context_creation():
     """The product path reads no environment variable per call: the only
-    getenv in the C++ sources is tuning_from_env (called by pnetgpu_ctx_create)."""
+    getenv calls in the C++ sources are tuning_from_env (called by
+    pnetgpu_ctx_create) and the host pool's size (compute_threads, whose result
+    host_threads() caches for the process)."""
     import re
     src_dir = os.path.join(ROOT, "libpnet_amd", "csrc")
     for f in sorted(os.listdir(src_dir)):
         text = open(os.path.join(src_dir, f)).read()
         hits = [m.start() for m in re.finditer(r"\bgetenv\s*\(", text)]
+        if f == "host_pool.cpp":
+            assert len(hits) == 1
+            fn = text.rfind("\nunsigned compute_threads(", 0, hits[0])
+            assert fn >= 0 and text.find("\n}\n", fn) > hits[0]
+            assert text.count("g_threads = compute_threads()") == 2
+            continue
         if f != "abi.cpp":
             assert not hits, f
             continue

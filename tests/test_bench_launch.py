@@ -34,6 +34,11 @@ def test_bench_gpus_n_starts_n_ranks(n):
     assert len(lines) == 1, p.stdout          # rank 0 only
     line = lines[0]
     assert line["n_gpus"] == n and line["world_size"] == n
+    # the line names the collective backend and the world size its process group reported
+    if n == 1:
+        assert line["collective"] is None
+    else:
+        assert line["collective"] == {"backend": "gloo", "world_size": n}
     assert line["counters_ok"] is True
     assert line["frames"] == 100003
     # byte-balanced: no rank's shard is more than one 1500-B frame off the mean

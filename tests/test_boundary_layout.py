@@ -18,8 +18,9 @@ from libpnet_amd import _lib, ring
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 STRUCTS = {"pnetgpu_batch": _lib.Batch, "pnetgpu_rx_columns": _lib.RxColumns,
-           "pnetgpu_ring_batch": ring.RingBatch, "pnetgpu_slice_desc": _lib.SliceDesc}
-RUST_SIZES = {"u8": 1, "u16": 2, "u32": 4, "u64": 8, "c_int": 4}
+           "pnetgpu_ring_batch": ring.RingBatch, "pnetgpu_slice_desc": _lib.SliceDesc,
+           "pnetgpu_ring_stats": ring.RingStats}
+RUST_SIZES = {"u8": 1, "u16": 2, "u32": 4, "u64": 8, "c_int": 4, "f64": 8}
 
 
 def test_ctypes_offsets_match_the_c_header(tmp_path):

@@ -97,6 +97,7 @@ def test_bench_two_ranks_one_gpu():
     assert len(lines) == 1, p.stdout
     line = lines[0]
     assert line["n_gpus"] == 2 and line["counters_ok"] is True
+    assert line["collective"] == {"backend": "gloo", "world_size": 2, "library": "gloo"}
     assert line["workloads"]["imix"]["counters_ok"] is True
     assert line["config"]["frames_scale"] == 0.01
     # one global batch, sharded: the two ranks' frames add up to it
@@ -125,6 +126,7 @@ def test_bench_four_ranks_one_gpu():
     assert len(lines) == 1, p.stdout
     line = lines[0]
     assert line["n_gpus"] == 4 and line["counters_ok"] is True
+    assert line["collective"] == {"backend": "gloo", "world_size": 4, "library": "gloo"}
     assert line["config"]["global_batch_frames"] == 4 * int((1 << 24) * 0.002)
     im = line["workloads"]["imix"]
     assert im["counters_ok"] is True

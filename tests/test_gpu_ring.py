@@ -244,3 +244,42 @@ def test_ring_zero_copy_pcapng_image(tmp_path, big):
         out = list(ring.feed_region(img, offs, lens)) + list(ring.drain())
     check_batches(out, frames)
     assert list(lp.pcap_frames(p)) == frames
+
+
+@pytest.mark.parametrize("producer", ["push_many", "zero_copy"])
+def test_ring_jumbo_batches_and_stage_stats(producer):
+    """configs[4]'s 9000-B IPv6/UDP frames through the bench's ring geometry
+    (64-MiB slots: 7,456 jumbo frames a batch, past the reference producer's
+    4096-B default read buffer, pnet_datalink/src/lib.rs:164-178): every batch
+    equals the source frames and the oracle's records, the planted corruptions
+    are all counted, and the ring's stage statistics account for every batch
+    (PNETGPU_RING_STAGE_TIMES: H2D, kernel and D2H timed on the device)."""
+    n = 20000
+    w = lp.synth.make("udp6_jumbo", n, seed=12, corrupt_ppm=20000)
+    offs = np.arange(n, dtype=np.uint64) * np.uint64(w.stride)
+    lens = np.full(n, w.frame_len, np.uint32)
+    ring = lp.Ring(batch_bytes=64 << 20, batch_frames=1 << 20, copy=True, stage_times=True)
+    reg = lp.HostRegistration(w.buf) if producer == "zero_copy" else None
+    try:
+        feed = ring.feed_region if producer == "zero_copy" else ring.feed_many
+        out = sorted(list(feed(w.buf, offs, lens)) + list(ring.drain()), key=lambda b: b.id)
+        st = ring.stats()
+    finally:
+        ring.close()
+        if reg:
+            reg.close()
+    assert [b.n for b in out] == [7456, 7456, n - 2 * 7456]
+    i = 0
+    for b in out:
+        got = np.asarray(b.frames[:int(b.offsets[-1] + b.lengths[-1])])
+        assert np.array_equal(got, w.buf[i * 9000:(i + b.n) * 9000]), b.id
+        rec = coracle.rx_batch(b.frames, b.n, offsets=b.offsets, lengths=b.lengths)
+        for c, v in b.records.items():
+            assert np.array_equal(v, rec[c]), (b.id, c)
+        i += b.n
+    assert sum(b.counters["l4_csum_bad"] for b in out) == w.expect["l4_bad"] > 0
+    assert sum(b.counters["bytes"] for b in out) == n * 9000
+    assert st["batches"] == st["timed_batches"] == 3 and st["frames"] == n and st["bytes"] == n * 9000
+    assert st["h2d_ms"] > 0 and st["kernel_ms"] > 0 and st["d2h_ms"] > 0
+    assert st["wait_ns"] > 0 and st["submit_ns"] > 0 and st["host_threads"] >= 1
+    assert (st["push_ns"] > 0) == (producer == "push_many")
