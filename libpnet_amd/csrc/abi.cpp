@@ -82,12 +82,8 @@ int slice_grid(pnetgpu_ctx* ctx, int which, int pseudo, bool extra, uint64_t wan
     return (int)std::max<uint64_t>(1, std::min<uint64_t>(want, cap));
 }
 constexpr int kRunFrames = 64;      // frames per wave-run
-#ifndef PNET_STATIC_PCT
-#define PNET_STATIC_PCT 88   // share of a batch's runs assigned statically (100: no claims)
-#endif
-#ifndef PNET_CLAIM_COUNTERS
-#define PNET_CLAIM_COUNTERS 64
-#endif
+// PNET_STATIC_PCT: share of a batch's runs assigned statically (100: no claims);
+// PNET_CLAIM_COUNTERS: claim counters per launch (rx_config.h)
 
 // Run scheduling of a persistent-grid launch (RunSched): a static grid-stride
 // share, then claimed units, so that waves whose share ran slow (the younger

@@ -107,14 +107,6 @@ __device__ __forceinline__ void rotate_prio(uint32_t step) {
     default: __builtin_amdgcn_s_setprio(3);
     }
 }
-#ifdef PNET_PRIO_ROTATE   // A/B: every kernel rotates per run
-#define PNET_PRIO(k) rotate_prio(k)
-#else
-#define PNET_PRIO(k)
-#endif
-#ifndef PNET_ROTATE_MTU
-#define PNET_ROTATE_MTU 1   // the MTU shape rotates per run (0: A/B without)
-#endif
 
 // The runs one wave processes (RxArgs::sched): its grid-stride share of
 // [0, nstatic), then runs claimed from one of the launch's nctr counters (the
@@ -163,9 +155,6 @@ struct RunQueue {
     __device__ void claim() {
         if (__lane_id() == 0) kraw = (uint32_t)atomicAdd(ctr, 1ull);
         inflight = true;
-#ifdef PNET_CLAIM_EAGER   // A/B: the round-3 claim, waited for where it is made
-        resolve();
-#endif
     }
     // the in-flight claim's run (waits for the atomic's return)
     __device__ void resolve() {
@@ -500,47 +489,6 @@ __device__ __forceinline__ void tx_write(uint8_t* frame, const Parsed& P, uint32
     }
 }
 
-// TX through the frame's LDS window (rx_kernel): the window copy is patched,
-// then each aligned 16-B granule holding a checksum field is stored whole
-// (one dwordx4 store) when it lies inside the frame and the window; a field
-// outside that (short frames, fields straddling a granule, fields past the
-// window) gets byte stores. A granule inside the frame holds only this frame's
-// bytes (frames of a TX batch do not overlap), unchanged since the window was
-// loaded except for the patched field. `fb` is the frame's aligned base
-// (granule 0 of the window), `sh` the frame's offset in it.
-#ifndef PNET_TX_GRANULES
-#define PNET_TX_GRANULES 0   // A/B: 1 = granule stores from the window, 0 = byte stores (tx_write)
-#endif
-__device__ __forceinline__ void tx_write_window(uint8_t* fb, uint8_t* slot, int sh, uint32_t len, int kwin,
-                                                const Parsed& P, uint32_t ipc, uint32_t l4c) {
-    int pos[2];
-    uint32_t val[2];
-    int nf = 0;
-    if (P.is_v4) { pos[nf] = sh + (int)P.l3 + 10; val[nf++] = ipc; }
-    if (P.st & PNET_ST_L4_CSUM_DONE) { pos[nf] = sh + P.l4csum_at; val[nf++] = l4c; }
-    for (int k = 0; k < nf; ++k) {
-        if (pos[k] + 2 <= kwin) {
-            slot[pos[k]] = (uint8_t)(val[k] >> 8);
-            slot[pos[k] + 1] = (uint8_t)val[k];
-        }
-    }
-    int stored = -1;
-    for (int k = 0; k < nf; ++k) {
-        const int p = pos[k], g = p >> 4;
-        const bool whole = ((p + 1) >> 4) == g && 16 * g >= sh && 16 * g + 16 <= sh + (int)len && 16 * g + 16 <= kwin;
-        if (whole) {
-            if (g != stored) {
-                const uint32_t* s32 = reinterpret_cast<const uint32_t*>(slot + 16 * g);
-                *reinterpret_cast<uint4*>(fb + 16 * g) = make_uint4(s32[0], s32[1], s32[2], s32[3]);
-                stored = g;
-            }
-        } else {
-            fb[p] = (uint8_t)(val[k] >> 8);
-            fb[p + 1] = (uint8_t)val[k];
-        }
-    }
-}
-
 // Per-wave counters (ballots: wave-uniform) and coalesced column stores.
 struct Counters {
     uint32_t frames = 0, v4 = 0, v6 = 0, ipbad = 0, l4bad = 0, malf = 0, unk = 0;
@@ -604,11 +552,7 @@ struct Counters {
 // Column element store (streaming: written once, never re-read by the kernel)
 template <class T>
 __device__ __forceinline__ void put(T* col, uint64_t i, T v) {
-#ifdef PNET_PLAIN_STORES
-    col[i] = v;
-#else
     __builtin_nontemporal_store(v, col + i);
-#endif
 }
 
 // Column stores for the frames of one run: the base is wave-uniform (SGPR) and
@@ -618,9 +562,7 @@ __device__ __forceinline__ void put(T* col, uint64_t i, T v) {
 // per column for the whole kernel (16 columns: 32 VGPRs, spills in the flat
 // kernel); with it each store recomputes its address (one VALU op).
 __device__ __forceinline__ uint64_t opaque_index(uint64_t i) {
-#ifndef PNET_HOIST_COLUMNS   // A/B: let the compiler hoist the column addresses
     asm volatile("" : "+v"(i));
-#endif
     return i;
 }
 
@@ -656,7 +598,7 @@ __device__ __forceinline__ void store_columns(const pnetgpu_rx_columns& C, uint6
 }
 
 // A frame's record packed in 8 dwords, for stores deferred past later runs
-// (rx_kernel, PNET_DEFER): every column of store_columns except the IPv6
+// (rx_kernel, kDeferRuns): every column of store_columns except the IPv6
 // address columns (read from the LDS slot at store time).
 struct Rec {
     uint32_t w[8];

@@ -17,9 +17,6 @@ namespace {
 // ============================================================================
 // rx_kernel: generic (descriptor mode, any alignment, any length).
 // ============================================================================
-#ifndef PNET_MTU_ALT
-#define PNET_MTU_ALT 1   // the MTU shape streams odd frames backward (below; A/B: 0)
-#endif
 template <int NW>
 struct WaveLds {
     static constexpr int kSlot = NW * 16 + 4;   // +4 B pad: conflict-free parse reads
@@ -63,7 +60,7 @@ __device__ __forceinline__ uint32_t lane_range_sum(const uint8_t* fb, int lo, in
 // LDS counter instead of a fixed stride of the list, and the list holds the
 // frames needing more than one round first, so mixed sizes balance across the
 // groups (the caller sets L.qhead = kWave / G).
-// ALT (the unified MTU shape, PNET_MTU_ALT): odd frames are streamed from
+// ALT (the unified MTU shape): odd frames are streamed from
 // their last granule backward, so the line a frame's end shares with the next
 // frame's start is read by both groups in the same round (even frame: its
 // last round; odd frame: its last round, which then covers its start), instead
@@ -167,37 +164,10 @@ __device__ __forceinline__ void tail_sums(const uint8_t* data, WaveLds<NW>& L, i
 // EXT: batch flags may be non-zero (VLAN / IPv6 extension dispatch) or
 // header-field columns may be requested; the plain instantiation compiles the
 // parse without those branches (half the code, SGPR spills 118 -> 14, IMIX -2 %).
-#ifndef PNET_SHORT_NT
-#define PNET_SHORT_NT 1   // non-temporal granule loads in 4-granule short runs (A/B: 0)
-#endif
-#ifndef PNET_SHORT_RUNS
-#define PNET_SHORT_RUNS 1   // A/B: short-run fast path in the mixed shape
-#endif
-#ifndef PNET_TX_DEFER
-#define PNET_TX_DEFER 3   // runs whose in-place TX writes the unified (MTU) shape holds back (A/B: 0)
-#endif
-#ifndef PNET_DEFER
-#define PNET_DEFER 3   // runs whose records the unified (MTU) shape holds back (A/B: 0 = store each run's at once)
-#endif
-#ifndef PNET_MIXED_UNI
-#define PNET_MIXED_UNI 1   // the mixed shape streams runs of large frames in the unified order (A/B: 0)
-#endif
-#ifndef PNET_UNI_ROTATE
-#define PNET_UNI_ROTATE 1   // A/B: 0 = those runs keep the wave's issue priority
-#endif
-#ifndef PNET_MIXED_JUMBO
-#define PNET_MIXED_JUMBO 1   // ... and runs of jumbo frames with the jumbo shape's tail (A/B: 0)
-#endif
-#ifndef PNET_MIXED_JUMBO_U
-#define PNET_MIXED_JUMBO_U 9   // its loads in flight per lane, as the jumbo shape (8 in the TX + EXT one: no spill)
-#endif
 constexpr uint32_t kUniMin = 768;     // every frame of such a run at least this long (PNETGPU_DESC_HINT_LARGE's bar)
 constexpr uint32_t kJumboMin = 4096;  // and shorter than this; runs of frames all this long: the jumbo tail
-#ifndef PNET_JUMBO_LB
-#define PNET_JUMBO_LB 4   // the jumbo shape's (NT) launch bound (A/B: 2 lets it use 256 VGPRs)
-#endif
 template <int NW, int G, int U, bool NT, int PASS, bool DYN, bool EXT, bool TX>
-__global__ __launch_bounds__(kBlock, NT ? PNET_JUMBO_LB : (NW < 8 ? 5 : 4)) void rx_kernel(RxArgs a) {
+__global__ __launch_bounds__(kBlock, NT ? kJumboWaves : (NW < 8 ? 5 : 4)) void rx_kernel(RxArgs a) {
     // the window must hold every field the parse reads near (Ethernet + 2 VLAN
     // tags + the fixed IPv4 header / IPv6 addresses: 82 B) after a 15-B shift
     static_assert(NW >= 7 || NW == 6, "window granules");
@@ -207,7 +177,7 @@ __global__ __launch_bounds__(kBlock, NT ? PNET_JUMBO_LB : (NW < 8 ? 5 : 4)) void
     // runs of short aligned frames take the small kernel's fast path (the
     // mixed shape's plain instantiation: no dispatch flags, header-field
     // columns or TX)
-    constexpr bool kShortRuns = PNET_SHORT_RUNS && PASS == 0 && DYN && !EXT && !TX;
+    constexpr bool kShortRuns = PASS == 0 && DYN && !EXT && !TX;
     // the short-run realignment reads slot dwords up to byte sh + 67 (sh <= 15)
     static_assert(!kShortRuns || kSlot >= 15 + 68, "short runs need a slot of at least 83 B");
 
@@ -240,7 +210,7 @@ __global__ __launch_bounds__(kBlock, NT ? PNET_JUMBO_LB : (NW < 8 ? 5 : 4)) void
     PNET_WT_BEGIN;
     uint32_t run_count = 0;
     (void)run_count;
-    // Deferred record stores (PNET_DEFER): a small write stream inside a read
+    // Deferred record stores (kDeferRuns): a small write stream inside a read
     // stream costs out of proportion to its bytes; the unified shape
     // keeps the last kDefer runs' records in registers (8 dwords per run) and
     // stores a run's record only when a newer one needs its place, or at the
@@ -248,17 +218,17 @@ __global__ __launch_bounds__(kBlock, NT ? PNET_JUMBO_LB : (NW < 8 ? 5 : 4)) void
     // the record stores of a launch then go out together at its end instead
     // of between reads. 1500-B batches -1.6 % at 3 runs (128 VGPRs, still 4
     // waves/SIMD); 1 or 2 runs measured even (profiles/r05/defer/).
-    constexpr int kDefer = (PNET_DEFER > 0 && PASS == 1 && !EXT && !TX) ? PNET_DEFER : 0;
+    constexpr int kDefer = (PASS == 1 && !EXT && !TX) ? kDeferRuns : 0;
     constexpr int kDq = kDefer > 0 ? kDefer : 1;
     const bool defer = kDefer > 0 && !a.cols.src_ipv6 && !a.cols.dst_ipv6;
     Rec dq[kDq];
     uint64_t dqf[kDq];
     int dqn = 0;
-    // TX (PNET_TX_DEFER): the in-place checksum writes of the last kTxDefer
+    // TX (kTxDeferRuns): the in-place checksum writes of the last kTxDefer
     // runs held back the same way (frame offset, field positions, values: 4
     // dwords per run): 1500-B TX fill -1 % at 3 runs, same box, three
     // interleaved rounds (profiles/r05/defer/ab_tx_defer.txt)
-    constexpr int kTxDefer = (PNET_TX_DEFER > 0 && PASS == 1 && TX) ? PNET_TX_DEFER : 0;
+    constexpr int kTxDefer = (PASS == 1 && TX) ? kTxDeferRuns : 0;
     constexpr int kTq = kTxDefer > 0 ? kTxDefer : 1;
     uint64_t tqo[kTq];
     uint32_t tqp[kTq], tqv[kTq];
@@ -280,12 +250,11 @@ __global__ __launch_bounds__(kBlock, NT ? PNET_JUMBO_LB : (NW < 8 ? 5 : 4)) void
     fetch_desc(run);
     while (run < a.nruns) {
         PNET_WT_RUN;
-        PNET_PRIO(run_count++);
         // the MTU shape (4 runs per wave at 2^20 frames: too few to balance by
         // claims) rotates its issue priority per run: 1500-B batches -1.5 %,
         // same box, four interleaved rounds (profiles/r03/claims/ab_rotate.txt);
         // jumbo frames rotated per frame measured even, not done
-        if (PNET_ROTATE_MTU && PASS == 1) rotate_prio(run_count++);
+        if (PASS == 1) rotate_prio(run_count++);
         const uint64_t nrun = q.take();   // the next run (its claim went out a run ago)
         // ---- 1. descriptor -------------------------------------------------
         const uint64_t f0 = run * kWave;
@@ -331,15 +300,15 @@ __global__ __launch_bounds__(kBlock, NT ? PNET_JUMBO_LB : (NW < 8 ? 5 : 4)) void
         // MTU-size traffic without PNETGPU_DESC_HINT_LARGE, or a burst of it
         // inside a mix): each frame streamed once in the MTU shape's unified
         // order instead of window first, then tail
-        constexpr bool kUniRuns = PNET_MIXED_UNI && PASS == 0 && DYN;
+        constexpr bool kUniRuns = PASS == 0 && DYN;
         const bool uni = kUniRuns && __ballot(in_batch && (desc_bad || len < kUniMin || len >= kJumboMin)) == 0ull;
         // and a run of jumbo frames (every frame >= 4 KiB): the jumbo shape's
         // tail, one frame per wave round
-        const bool jrun = kUniRuns && PNET_MIXED_JUMBO && !uni &&
+        const bool jrun = kUniRuns && !uni &&
                           __ballot(in_batch && (desc_bad || len < kJumboMin)) == 0ull;
         // such runs rotate their issue priority as the MTU shape does: no-hint
         // 1500-B batches -2.6 %, IMIX even (profiles/r05/uni_runs/ab_rotate.txt)
-        if (PNET_UNI_ROTATE && kUniRuns && uni) rotate_prio(run_count++);
+        if (kUniRuns && uni) rotate_prio(run_count++);
 
         // ---- 2. window: NW*64 granule loads, all in flight before any store --
         if (kShortRuns && four) {   // wave-uniform: 4 granules per frame
@@ -350,7 +319,7 @@ __global__ __launch_bounds__(kBlock, NT ? PNET_JUMBO_LB : (NW < 8 ? 5 : 4)) void
                 const int fl = q >> 2, c = q & 3;
                 g[i] = make_uint4(0, 0, 0, 0);
                 if ((uint32_t)c < L.end[fl])
-                    g[i] = PNET_SHORT_NT ? load16_nt(a.data + L.base[fl] + 16u * c) : load16(a.data + L.base[fl] + 16u * c);
+                    g[i] = load16_nt(a.data + L.base[fl] + 16u * c);
             }
             fetch_desc(nrun);
 #pragma unroll
@@ -402,12 +371,12 @@ __global__ __launch_bounds__(kBlock, NT ? PNET_JUMBO_LB : (NW < 8 ? 5 : 4)) void
             if (DYN && lane == 0) L.qhead = kWave / G;
             wave_sync();
             if (kUniRuns && uni)   // the MTU shape's tail configuration (PNET_MTU_CFG)
-                tail_sums<NW, 8, 4, false, true, false, PNET_MTU_ALT>(a.data, L, lane, __popcll(tmask) PNET_TAIL_STAT);
-            else if (kUniRuns && PNET_MIXED_JUMBO && jrun)   // the jumbo shape's (PNET_JUMBO_CFG)
-                tail_sums<NW, 64, (TX && EXT ? 8 : PNET_MIXED_JUMBO_U), true, false, false>(
+                tail_sums<NW, 8, 4, false, true, false, true>(a.data, L, lane, __popcll(tmask) PNET_TAIL_STAT);
+            else if (kUniRuns && jrun)   // the jumbo shape's (PNET_JUMBO_CFG)
+                tail_sums<NW, 64, (TX && EXT ? 8 : kMixedJumboU), true, false, false>(
                     a.data, L, lane, __popcll(tmask) PNET_TAIL_STAT);
             else
-                tail_sums<NW, G, U, NT, (PASS != 0), DYN, (PNET_MTU_ALT && PASS == 1 && !DYN)>(
+                tail_sums<NW, G, U, NT, (PASS != 0), DYN, (PASS == 1 && !DYN)>(
                     a.data, L, lane, __popcll(tmask) PNET_TAIL_STAT);
         }
         wave_sync();
@@ -469,10 +438,7 @@ __global__ __launch_bounds__(kBlock, NT ? PNET_JUMBO_LB : (NW < 8 ? 5 : 4)) void
             tqv[0] = val;
             tqn = tqn < kTxDefer ? tqn + 1 : kTxDefer;
         } else if (TX && in_batch && !desc_bad) {
-            if (PNET_TX_GRANULES)
-                tx_write_window(const_cast<uint8_t*>(a.data) + base, slot, sh, len, kWin, P, ipc, l4c);
-            else
-                tx_write(const_cast<uint8_t*>(a.data) + off, P, ipc, l4c);
+            tx_write(const_cast<uint8_t*>(a.data) + off, P, ipc, l4c);
         }
         if (kDefer > 0 && defer) {
             const Rec cur = pack_rec(P, ipc, l4c);
@@ -488,10 +454,8 @@ __global__ __launch_bounds__(kBlock, NT ? PNET_JUMBO_LB : (NW < 8 ? 5 : 4)) void
         } else {
             store_columns(a.cols, f0, lane, in_batch, P, ipc, l4c, slot, sh);
         }
-#ifndef PNET_NO_FIELD_COLUMNS   // A/B: the header-field stores compiled out
         if (EXT && a.field_cols && in_batch)   // header-field columns: EXT instantiations only
             store_field_columns(a.cols, f0 + lane, P, FrameBytes{slot + sh, a.data + off, kWin - sh}, EXT && a.l3mode);
-#endif
         if (a.cols.counters) K.add(in_batch && !desc_bad, len, P.st);
         wave_sync();   // slots and lists are rewritten by the next run
         PNET_PH(3);   // probe: stores, counters

@@ -4,6 +4,7 @@
 #include <stdint.h>
 
 #include "pnetgpu.h"
+#include "rx_config.h"
 
 namespace pnetgpu {
 
@@ -28,9 +29,6 @@ namespace pnetgpu {
 // us) but do not end the launch sooner - its last few blocks set the end
 // either way - and measured even to 1 % slower over 8 interleaved rounds
 // (profiles/r05/wave_ends/), so 32 stays.
-#ifndef PNET_CLAIM_CHUNK
-#define PNET_CLAIM_CHUNK 32
-#endif
 constexpr uint32_t kClaimChunk = PNET_CLAIM_CHUNK;
 
 struct RunSched {

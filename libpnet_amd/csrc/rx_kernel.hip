@@ -94,25 +94,11 @@ static int resident_blocks(const void* fn, int block_threads) {
 // and deep loads; MTU frames 8-lane groups streaming each whole frame once
 // (unified: -6 % time); jumbo frames the whole wave on one frame, 9 KiB in
 // flight per round (one round per 9000-B frame), non-temporal.
-#ifndef PNET_MIXED_CFG
-#define PNET_MIXED_CFG 4, 8, false, 0, true
-#endif
-#ifndef PNET_MTU_CFG
-#define PNET_MTU_CFG 8, 4, false, 1, false
-#endif
-#ifndef PNET_JUMBO_CFG
-#define PNET_JUMBO_CFG 64, 9, true, 0, false
-#endif
-// window granules of the mixed shape (6: 96-B window, 5 blocks/CU by LDS)
-#ifndef PNET_MIXED_NW
-#define PNET_MIXED_NW 8
-#endif
+// (PNET_MIXED_CFG / _MTU_CFG / _JUMBO_CFG, rx_config.h).
+// Window granules of the mixed shape: PNET_MIXED_NW (6: 96-B window, 5 blocks/CU by LDS).
 #define PNET_MIXED_FN(EXT, TX) rx_kernel<PNET_MIXED_NW, PNET_MIXED_CFG, EXT, TX>
 // window granules of the MTU shape's plain instantiations (the EXT ones, with
-// the VLAN / extension-header / field-column code, keep 8: at 6 they spill)
-#ifndef PNET_MTU_NW
-#define PNET_MTU_NW 8
-#endif
+// the VLAN / extension-header / field-column code, keep 8: at 6 they spill): PNET_MTU_NW
 #define PNET_MTU_FN(EXT, TX) rx_kernel<((EXT) ? 8 : PNET_MTU_NW), PNET_MTU_CFG, EXT, TX>
 #define PNET_JUMBO_FN(EXT, TX) rx_kernel<8, PNET_JUMBO_CFG, EXT, TX>
 
@@ -147,18 +133,12 @@ void launch_t(const RxArgs& args, int kind, int blocks, hipStream_t stream) {
 
 // Resident blocks of the small kernel: 4 per CU (4 waves/SIMD) measured best
 // from 3 to 8 in one process (udp64 274 us at 4 vs 285-303 us at 5-8; its 75
-// VGPRs would allow 6), tools/kbench.py --env PNETGPU_BLOCKS_PER_CU.
-#ifndef PNET_SMALL_BLOCKS
-#define PNET_SMALL_BLOCKS 4
-#endif
+// VGPRs would allow 6), tools/kbench.py --env PNETGPU_BLOCKS_PER_CU: PNET_SMALL_BLOCKS.
 // The jumbo shape: 2 per CU (2 waves/SIMD, 9 KiB in flight per wave). With
 // more, a batch that fills them reads slower: 2^18 / 2^19 9000-B frames 0.81 /
 // 0.85 of 8 TB/s at 2 against 0.80 / 0.81 at 4 (bench.py --frames-scale 2 / 4,
 // same box, profiles/r05/jumbo_blocks/); the bench's 2^17 frames (2048 runs)
-// fill 2 per CU either way.
-#ifndef PNET_JUMBO_BLOCKS
-#define PNET_JUMBO_BLOCKS 2
-#endif
+// fill 2 per CU either way: PNET_JUMBO_BLOCKS.
 
 int rx_blocks_per_cu(int kind, bool ext, int* numregs, int* lds) {
     const void* fn = ext ? pick_fn<true, false>(kind) : pick_fn<false, false>(kind);

@@ -18,9 +18,6 @@ namespace {
 // One group of 16 lanes per slice (4 slices per wave per step): coalesced
 // 16-B granules, masked sums, shuffle reduce, lane 0 of the group finalizes.
 
-#ifndef PNET_SLICE_U
-#define PNET_SLICE_U 4   // loads in flight per lane in the slice kernels
-#endif
 // Sum of bytes [b, 16) of granule g: the dword holding b in part, the ones
 // after it whole (b = 16: none). Granules by value, picked with selects: an
 // indexed pick (or one through an array reference) becomes a scratch array.
@@ -201,13 +198,13 @@ __global__ __launch_bounds__(kBlock, EXTRA ? 7 : 8) void slice_kernel(SliceArgs 
         const bool lng = (uint64_t)len + elen > kExactMax;
         uint32_t acc, tacc = 0, te = 0, tte = 0;
         if (lng) acc = group_range_sum_t<G, 1>(a.data, off, len, j, &tacc);   // group-uniform, rare
-        else acc = group_range_sum<G, PNET_SLICE_U>(a.data, off, len, j);
+        else acc = group_range_sum<G, kSliceU>(a.data, off, len, j);
         if (EXTRA) {
             // sum_be_words(extra, extra.len() / 2): every whole word, never the odd
             // trailing byte (util.rs:114; the quirk documented at udp.rs:42-44); the
             // extra slice starts its own word alignment
             if (lng) te = group_range_sum_t<G, 1>(a.data, eoff, elen & ~1u, j, &tte);
-            else te = group_range_sum<G, PNET_SLICE_U>(a.data, eoff, elen & ~1u, j);
+            else te = group_range_sum<G, kSliceU>(a.data, eoff, elen & ~1u, j);
         }
         if (j == 0) {
             // skipped word: bytes [2*skip, 2*skip+2) of the slice that exist (util.rs:166-178)
@@ -353,7 +350,7 @@ __device__ __forceinline__ uint32_t run_range_sum(const SliceArgs& a, uint64_t r
     if (m8) listed_sums<2, 4>(m8, lane, list, gsum, a.data, off, len);
     if (m16) listed_sums<4, 4>(m16, lane, list, gsum, a.data, off, len);
     if (m32) listed_sums<8, 4>(m32, lane, list, gsum, a.data, off, len);
-    if (lmask) listed_sums<16, PNET_SLICE_U>(lmask, lane, list, gsum, a.data, off, len);
+    if (lmask) listed_sums<16, kSliceU>(lmask, lane, list, gsum, a.data, off, len);
     // slices of sums past kExactMax: with their plain byte sums (rare)
     if (const uint64_t xmask = __ballot(in && exact))
         listed_sums<16, 1, true>(xmask, lane, list, gsum, a.data, off, len, gtsum);
@@ -456,15 +453,12 @@ __device__ __forceinline__ void run_finish(const SliceArgs& a, uint64_t run, int
 // (the last as in slice_kernel), and one coalesced 2-B store per lane.
 // slice_kernel gave 16 lanes to every slice: a 20-B slice left 14 of them idle
 // and the results went out as 2-B stores scattered 32 B apart.
-#ifndef PNET_RUN_MINWAVES
-#define PNET_RUN_MINWAVES 1   // A/B: waves per SIMD the register allocation must allow
-#endif
 // EXTRA: the *_checksum_adv form (util.rs:109-114): the extra slice summed
 // by the same machinery as a second range (whole words only, its own word
 // alignment), where slice_kernel gave 16 lanes to every slice (80-B slices
 // 10 % of 8 TB/s).
 template <int PSEUDO, bool EXTRA>
-__global__ __launch_bounds__(kBlock, PNET_RUN_MINWAVES) void slice_run_kernel(SliceArgs a) {
+__global__ __launch_bounds__(kBlock, 1) void slice_run_kernel(SliceArgs a) {
     __shared__ uint4 dstage[kWavesPerBlock][kRunDense];
     __shared__ uint32_t gsum[kWavesPerBlock][kWave];
     __shared__ uint32_t gtsum[kWavesPerBlock][kWave];   // plain byte sums of long slices (kExactMax)
@@ -619,21 +613,13 @@ __device__ __forceinline__ void tiny_finish(const SliceArgs& a, const TinyStage&
     const int e = sh + (int)s.len;
     const uint32_t nneed = s.len ? (uint32_t)((e + 15) >> 4) : 0u;
     const bool small = nneed <= (uint32_t)kTinyGranules;
-#ifdef PNET_TINY_AB_NOCHUNK   // A/B: whole granules only (wrong sums: the VALU cost of the edges)
-    uint32_t acc = granule_sum(s.v[1], granule_sum(s.v[0], 0u));
-#else
     uint32_t acc = chunk_sum(s.v[0], s.v[1], s.v[2], make_uint4(0, 0, 0, 0), 0, sh, e, nneed,
                              __ballot(nneed > 2u) == 0ull);
-#endif
     // skipped word: its bytes [2 skip, 2 skip + 2) that lie in the slice
     // (util.rs:166-178), from the granules (a small slice's lie in them)
     const uint64_t q = 2ull * s.skip;
     const bool s0 = q < s.len, s1 = q + 1 < s.len;
-#ifdef PNET_TINY_AB_NOWINDOW   // A/B: no skipped-word extraction (wrong sums)
-    uint32_t pair = s.v[0].x;
-#else
     uint32_t pair = window_bytes(s.v[0], s.v[1], s.v[2], small && s0 ? (uint32_t)sh + (uint32_t)q : 0u);
-#endif
     uint32_t tsum = 0;        // a long slice's plain byte sum (kExactMax)
     bool any_long = false;    // wave-uniform: the run holds one
     if (__ballot(!small)) {   // wave-uniform: a run with longer slices
@@ -684,11 +670,8 @@ __device__ __forceinline__ uint64_t uniform64(uint64_t x) {
            (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)x);
 }
 
-#ifndef PNET_TINY_MINWAVES
-#define PNET_TINY_MINWAVES 1   // A/B: waves per SIMD the register allocation must allow
-#endif
 template <bool COMPACT>
-__global__ __launch_bounds__(kBlock, PNET_TINY_MINWAVES) void slice_tiny_kernel(SliceArgs a) {
+__global__ __launch_bounds__(kBlock, 1) void slice_tiny_kernel(SliceArgs a) {
     const int lane = threadIdx.x & (kWave - 1);
     const int wv = threadIdx.x / kWave;
     const uint64_t nruns = (a.n + kWave - 1) / kWave;
@@ -802,10 +785,6 @@ __global__ __launch_bounds__(kBlock) void slice_strided_kernel(SliceArgs a) {
         }
         wave_sync();
         const int pb = (int)(a.first + a.delta + cur.i0 * s - cur.g0);   // stage byte of the block's slice 0
-#ifdef PNET_STRIDED_NOCOMP   // A/B: one result per block from the stage, no slice sums
-        if (lane == 0 && st[lane * 17] == 0x12345u) a.out[cur.i0] = 1;
-        if (false)
-#endif
 #pragma unroll 1
         for (uint32_t r = 0; r < R; ++r) {
             const uint32_t k = 64u * r + lane;
@@ -866,11 +845,7 @@ __global__ __launch_bounds__(kBlock) void slice_strided_kernel(SliceArgs a) {
                 if (!(p & 1)) f = bswap16(f);
                 res = (~f) & 0xFFFFu;                           // util.rs:76-82 (non-empty)
             }
-#ifdef PNET_STRIDED_NOSTORE   // A/B: results stored only if they hit a magic value
-            if (k < cur.nsl && res == 0x12345u) a.out[cur.i0 + k] = (uint16_t)res;
-#else
             if (k < cur.nsl) a.out[cur.i0 + k] = (uint16_t)res;
-#endif
         }
         wave_sync();   // the stage is rewritten by the next block
         cur = nxt;

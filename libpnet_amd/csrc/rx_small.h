@@ -16,7 +16,6 @@ namespace {
 // ============================================================================
 // rx_small_kernel: fixed stride, frames 16-B aligned, span <= 64 B.
 // ============================================================================
-#ifndef PNET_SMALL_LINEAR   // A/B: the round-2 linear 80-B slots
 // 64-B slots with granule c of frame f at slot granule (c + f/4) & 3: the
 // transpose's ds_write_b128 (4 frames x 4 granules per 16-lane pass) and its
 // ds_read_b128 (16 frames, one granule each) both hit 16 distinct 4-bank groups
@@ -28,10 +27,6 @@ namespace {
 // the verify-only record 221-225 vs 222-232 us; bit-exact.
 constexpr int kSmallSlot = 64;
 __device__ __forceinline__ int small_gpos(int f, int c) { return f * kSmallSlot + 16 * ((c + (f >> 2)) & 3); }
-#else
-constexpr int kSmallSlot = 80;   // 16-B aligned slots; ds_read_b128 conflict-free (20l mod 64 distinct per 16 lanes)
-__device__ __forceinline__ int small_gpos(int f, int c) { return f * kSmallSlot + 16 * c; }
-#endif
 
 struct SmallRun {
     uint4 g[4];
@@ -162,9 +157,6 @@ __device__ __forceinline__ bool small_fast(const uint32_t (&w)[16], uint32_t len
     return slow;
 }
 
-#ifndef PNET_SMALL_WAVES
-#define PNET_SMALL_WAVES 4   // waves/SIMD the small kernel is register-bounded for
-#endif
 // FIELDS: the header-field columns may be requested (a separate instantiation:
 // their code in the loop cost the plain record 3-10 % on MI355X)
 template <bool TX, bool FIELDS>
@@ -178,14 +170,11 @@ __global__ __launch_bounds__(kBlock, PNET_SMALL_WAVES) void rx_small_kernel(RxAr
 
     const uint64_t wave_stride = (uint64_t)gridDim.x * kWavesPerBlock;
     PNET_WT_BEGIN;
-    uint32_t run_count = 0;
-    (void)run_count;
     RunQueue q(a.sched, a.nruns, (uint64_t)blockIdx.x * kWavesPerBlock + wv, wave_stride);
     uint64_t run = q.take();
     SmallRun cur = run < a.nruns ? small_load(a, run, lane) : SmallRun{};
     while (run < a.nruns) {
         PNET_WT_RUN;
-        PNET_PRIO(run_count++);
         // software pipelining: the next run's loads are in flight while this one is processed
         // (two runs ahead measured no faster: the wave is not short of loads in flight)
         const uint64_t nrun = q.take();
@@ -214,20 +203,13 @@ __global__ __launch_bounds__(kBlock, PNET_SMALL_WAVES) void rx_small_kernel(RxAr
         const bool slow = in_batch && small_fast(wv16, len, P, ipc, l4c);
         // ---- generic path through LDS for the lanes the fast path did not take ----
         const bool need_v6 = a.cols.src_ipv6 || a.cols.dst_ipv6;
-#ifndef PNET_SMALL_LINEAR
         // the slot as frame bytes (wave-uniform): each lane rewrites its own slot
         // linearly from its registers (no other lane reads it before the next sync)
         if (TX || (FIELDS && a.field_cols) || need_v6 || __ballot(slow)) {
 #pragma unroll
             for (int c = 0; c < 4; ++c) *reinterpret_cast<uint4*>(slot + 16 * c) = cur.g[c];
         }
-#endif
-#ifdef PNET_SMALL_NOSLOW
-        if (slow) P.st = 0xFFFFu;
-        if (false) {
-#else
         if (__ballot(slow) || need_v6) {
-#endif
             if (slow) {
                 // flags are 0 here and the frame (<= 64 B) is entirely in its slot
                 P = parse_frame(FrameBytes{slot, slot, 64}, len, 0u);
@@ -242,25 +224,13 @@ __global__ __launch_bounds__(kBlock, PNET_SMALL_WAVES) void rx_small_kernel(RxAr
             // lines instead of four scattered byte stores per frame, which left
             // every line of the batch partially dirty (0.63 ms -> see DESIGN.md)
             if (in_batch) tx_write(slot, P, ipc, l4c);
-#ifdef PNET_SMALL_TX_PARTIAL
-            // A/B: write back only the granules holding a patched field
-            // (granule 1: the IPv4 checksum; the L4 field's granule)
-            __shared__ uint8_t txm[kWavesPerBlock][kWave];
-            txm[wv][lane] = (uint8_t)((P.is_v4 ? 1u << ((P.l3 + 10) >> 4) | 1u << ((P.l3 + 11) >> 4) : 0u) |
-                                      ((P.st & PNET_ST_L4_CSUM_DONE) ? 1u << (P.l4csum_at >> 4) |
-                                                                      1u << ((P.l4csum_at + 1) >> 4) : 0u));
-#endif
             wave_sync();
             const uint32_t span = (a.frame_len + 15u) >> 4;
             const uint32_t c = (uint32_t)(lane & 3);
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 const uint64_t f = f0 + 16 * i + (lane >> 2);
-#ifdef PNET_SMALL_TX_PARTIAL
-                if (f < a.n && c < span && ((txm[wv][16 * i + (lane >> 2)] >> c) & 1u)) {
-#else
                 if (f < a.n && c < span) {
-#endif
                     const uint4 v = *reinterpret_cast<const uint4*>(lds_slots[wv] + (16 * i + (lane >> 2)) * kSmallSlot +
                                                                     16 * c);
                     __builtin_nontemporal_store(u32x4_t{v.x, v.y, v.z, v.w},
@@ -271,10 +241,8 @@ __global__ __launch_bounds__(kBlock, PNET_SMALL_WAVES) void rx_small_kernel(RxAr
         }
         PNET_PH(2);   // probe: fast path / parse
         store_columns(a.cols, f0, lane, in_batch, P, ipc, l4c, slot, 0);
-#ifndef PNET_NO_FIELD_COLUMNS   // A/B: the header-field stores compiled out
         if (FIELDS && a.field_cols && in_batch)
             store_field_columns(a.cols, f0 + lane, P, FrameBytes{slot, slot, 64}, false);
-#endif
         if (a.cols.counters) K.add(in_batch, len, P.st);
         wave_sync();
         PNET_PH(3);   // probe: stores, counters

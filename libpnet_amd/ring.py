@@ -111,7 +111,7 @@ class Batch:
     yielding it, so views must not outlive the consumer's loop iteration.
     The views are made on first use (offsets, lengths, frames, records): a
     consumer that reads only the counters costs one small view per batch, which
-    keeps the ring at the link's rate (tools/ring_probe.py)."""
+    keeps the ring at the link's rate (tools/probes/ring_probe.py)."""
 
     def __init__(self, rb, copy=True):
         n = int(rb.n_frames)

@@ -1,6 +1,6 @@
 """GPU parity of the MTU shape with several runs per wave: the record stores and
 the TX fill's in-place writes of the last three runs are held back in
-registers (rx_generic.h, PNET_DEFER / PNET_TX_DEFER) and stored when a newer run
+registers (rx_generic.h; kDeferRuns / kTxDeferRuns in rx_config.h) and stored when a newer run
 needs the place or at the wave's end. The full-size tests run 4 runs per wave;
 here the grid is cut to one block per CU (the blocks_per_cu tuning) so waves
 hold 4, 8 (the claimed-run schedule then joins in) or a ragged number of runs,

@@ -1,4 +1,4 @@
-"""GPU parity of the mixed shape's large-frame runs (rx_generic.h, PNET_MIXED_UNI):
+"""GPU parity of the mixed shape's large-frame runs (rx_generic.h, kUniRuns):
 a run of 64 frames whose every frame is at least 768 B (and under 4 KiB) is
 streamed in the MTU shape's unified order inside the mixed kernel, and a run of
 frames all at least 4 KiB with the jumbo shape's tail (descriptor batches

@@ -1,7 +1,8 @@
 #!/bin/bash
 # A/B over library variants, interleaved over rounds ("default" = shipped .so).
 # usage: tools/abvar.sh "<workloads>" rounds V1 V2 ...   (KB_ARGS: extra kbench.py arguments, e.g. --tx;
-#        AB_SCRIPT: a probe script to run per variant instead of kbench.py, e.g. tools/desc_nohint_probe.py)
+#        AB_SCRIPT: a probe script to run per variant instead of kbench.py, e.g. tools/probes/desc_nohint_probe.py, or
+#        "bench.py --workloads udp6_jumbo --no-extra --no-cpu --no-e2e" for a bench line per variant)
 # Even rounds run the variants in reverse order (ABBA), so an order effect
 # (the first process of a round is ~1 % slower on some boxes) cancels.
 W=$1; R=$2; shift 2

@@ -4,7 +4,7 @@ The same IMIX frames timed packed (as generated) and re-packed at 128-B aligned
 offsets (no line holds two frames; algorithmic bytes unchanged), both in
 descriptor mode through the mixed kernel.
 
-  python tools/align_probe.py [--n 4194304] [--reps 20]
+  python tools/probes/align_probe.py [--n 4194304] [--reps 20]
 """
 import argparse
 import os
@@ -13,7 +13,7 @@ import sys
 import numpy as np
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 import libpnet_amd as lp  # noqa: E402
 from libpnet_amd.engine import IPV4_COLUMNS  # noqa: E402
 

@@ -4,7 +4,7 @@ descriptors vs PNETGPU_DESC_COMPACT u32/u16 ones: kernel time per launch
 (HIP events around back-to-back launches on one stream), interleaved rounds,
 records compared.
 
-  python tools/compact_probe.py [--n 4194304] [--reps 20]
+  python tools/probes/compact_probe.py [--n 4194304] [--reps 20]
 """
 import argparse
 import os
@@ -13,7 +13,7 @@ import sys
 import numpy as np
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 import libpnet_amd as lp  # noqa: E402
 from libpnet_amd.engine import IPV4_COLUMNS  # noqa: E402
 

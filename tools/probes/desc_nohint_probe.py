@@ -4,7 +4,7 @@
 descriptor line) and with it, and the IMIX batch (full record and verify-only). Used with tools/abvar.sh
 (AB_SCRIPT) to compare library variants on one box.
 
-  PNETGPU_LIB=.../libpnetgpu_V.so python tools/desc_nohint_probe.py
+  PNETGPU_LIB=.../libpnetgpu_V.so python tools/probes/desc_nohint_probe.py
 """
 import os
 import sys
@@ -12,7 +12,7 @@ import sys
 import numpy as np
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 import bench  # noqa: E402
 bench.load_library()
 from bench import HBM_PEAK_GBS, Shard, descriptor_rate, time_launches  # noqa: E402

@@ -12,7 +12,7 @@ cutL: the first L bytes of udp1500 frames packed (L = 768 ... 1280: where the
 shapes cross); jumbo9000: 9000-B IPv6 frames packed; jmix: 64-B and 9000-B
 frames at 7:1.
 
-  python tools/desc_shape_probe.py [--rounds 3] [--reps 10]
+  python tools/probes/desc_shape_probe.py [--rounds 3] [--reps 10]
 """
 import argparse
 import os
@@ -21,7 +21,7 @@ import sys
 import numpy as np
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 import libpnet_amd as lp  # noqa: E402
 
 KINDS = {"mixed": 0, "mtu": 2, "jumbo": 3}

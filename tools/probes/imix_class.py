@@ -17,7 +17,7 @@ launches, so every timed launch is preceded by a 1-GiB read of an unrelated
 tensor (cache flush) and timed by its own event pair (the same ~few-us event
 overhead in every row). Output: one line per variant, median/min over rounds.
 
-  python tools/imix_class.py [--rounds 5] [--reps 6]
+  python tools/probes/imix_class.py [--rounds 5] [--reps 6]
 """
 import argparse
 import json
@@ -27,7 +27,7 @@ import sys
 import numpy as np
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 import libpnet_amd as lp  # noqa: E402
 
 HBM = 8000.0

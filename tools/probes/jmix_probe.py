@@ -6,7 +6,7 @@ same batch through the library PNETGPU_LIB names (run once per variant, e.g.
 tools/abvar-style: default vs libpnetgpu_nosplit.so) and checks the records
 against the oracle.
 
-  PNETGPU_LIB=... python tools/jmix_probe.py [--n 1048576]
+  PNETGPU_LIB=... python tools/probes/jmix_probe.py [--n 1048576]
 """
 import argparse
 import os
@@ -15,7 +15,7 @@ import sys
 import numpy as np
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 import libpnet_amd as lp  # noqa: E402
 from oracle import coracle  # noqa: E402
 

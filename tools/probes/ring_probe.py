@@ -5,7 +5,7 @@ Ring.feed_region (a Batch object with numpy views per waited batch, as the
 bench does) and (b) through the C-ABI directly from a ctypes loop
 (submit_region / wait / release, no per-batch Python objects), interleaved.
 
-  python tools/ring_probe.py [--slots 4] [--rounds 2] [--seconds 3]
+  python tools/probes/ring_probe.py [--slots 4] [--rounds 2] [--seconds 3]
 """
 import argparse
 import ctypes
@@ -16,7 +16,7 @@ import time
 import numpy as np
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 import bench  # noqa: E402
 
 

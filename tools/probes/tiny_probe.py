@@ -5,7 +5,7 @@ slice_run_kernel and slice_tiny_kernel (tuning slice_kernel run / tiny), full
 median kernel time per launch; also the tiny kernel with every run static
 (static_pct 100). Every timed result is checked against the first kernel's.
 
-  python tools/tiny_probe.py [--sizes 8,12,16,20,24,32,48,64] [--rounds 3] [--variants run,tiny]
+  python tools/probes/tiny_probe.py [--sizes 8,12,16,20,24,32,48,64] [--rounds 3] [--variants run,tiny]
   tools/tiny_ab.sh TAG SIZES V...   the tiny kernel of library variants (PNETGPU_LIB), interleaved
 """
 import argparse
@@ -15,7 +15,7 @@ import sys
 import numpy as np
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 import libpnet_amd as lp  # noqa: E402
 
 PEAK = 8000.0

@@ -3,7 +3,7 @@
 //   read      : stream 1 GiB with coalesced dwordx4 loads, fold into one word/wave
 //   read+cols : the same reads + 26 B/frame of SoA column stores (64-B frames)
 //   copy      : float4 copy 1 GiB -> 1 GiB (the guide's 6.29 TB/s reference point)
-// Build: hipcc --offload-arch=gfx950 -O3 -o tools/sol tools/sol.hip
+// Build: hipcc --offload-arch=gfx950 -O3 -o tools/sol/sol tools/sol/sol.hip
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdint>

@@ -5,7 +5,7 @@
 //                    counted vmcnt, lane l reads frame l back (source-swizzled, conflict-free)
 //   glds+cols <S>  : the same + 26 B/frame of non-temporal SoA column stores
 //   reg+cols       : register-staged 4 KiB per run, one run prefetched (today's shape)
-// Build: hipcc --offload-arch=gfx950 -O3 -o tools/sol2 tools/sol2.hip
+// Build: hipcc --offload-arch=gfx950 -O3 -o tools/sol/sol2 tools/sol/sol2.hip
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdint>

@@ -3,7 +3,7 @@
 //   grp8     : 8 lanes per frame, 8 frames x 128 B per wave instruction (the MTU kernel's shape),
 //              loaded by glds into an S-deep ring of 1-KiB slots, or into registers (U in flight)
 // Every lane reads back only the granule it loaded (sum of words), so LDS is conflict-free.
-// Build: hipcc --offload-arch=gfx950 -O3 -o tools/sol3 tools/sol3.hip
+// Build: hipcc --offload-arch=gfx950 -O3 -o tools/sol/sol3 tools/sol/sol3.hip
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdint>

@@ -3,7 +3,7 @@
 // (saddr form, per-lane source offsets permuted inside 64-B pieces), per-wave
 // contiguous ranges, LDS padded to the stream kernel's footprint; the consumer
 // reads its 64-B piece and sums it, plus W dependent VALU ops of fake work per step.
-// Build: hipcc --offload-arch=gfx950 -O3 -o tools/sol4 tools/sol4.hip
+// Build: hipcc --offload-arch=gfx950 -O3 -o tools/sol/sol4 tools/sol/sol4.hip
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdint>

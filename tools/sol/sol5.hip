@@ -4,7 +4,7 @@
 //   wN   : pure writes, each lane stores N bytes (one instruction = 64 N bytes)
 //   r+wN : glds read stream (4-KiB steps, 3-step ring) + the same writes, per step
 //          64 N bytes x K instructions so that writes / reads = 26 / 64
-// Build: hipcc --offload-arch=gfx950 -O3 -o tools/sol5 tools/sol5.hip
+// Build: hipcc --offload-arch=gfx950 -O3 -o tools/sol/sol5 tools/sol/sol5.hip
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdint>

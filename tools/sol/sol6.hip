@@ -7,7 +7,7 @@
 //   read+cols runs streamed + the 12 record columns (26 B/frame, nt stores)
 //   +scan     each 1-KiB chunk also does the per-chunk prefix bookkeeping a real
 //             kernel needs (wave scan of the granule sums + 2 ds_bpermute reads)
-// Build: hipcc --offload-arch=gfx950 -O3 -o tools/sol6 tools/sol6.hip
+// Build: hipcc --offload-arch=gfx950 -O3 -o tools/sol/sol6 tools/sol/sol6.hip
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdint>

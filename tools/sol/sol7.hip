@@ -6,7 +6,7 @@
 // bookkeeping a real kernel needs (lane-local prefix of its 4 granules, one wave
 // scan, the 64 prefixes written to an LDS table); a run's 12 record columns
 // (26 B/frame, nt stores) go out when the stream passes the run's last byte.
-// Build: hipcc --offload-arch=gfx950 -O3 -o tools/sol7 tools/sol7.hip
+// Build: hipcc --offload-arch=gfx950 -O3 -o tools/sol/sol7 tools/sol/sol7.hip
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdint>
