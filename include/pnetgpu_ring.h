@@ -195,9 +195,10 @@ void pnetgpu_pcap_close(pnetgpu_pcap* p);
  * (img_bytes at the end; for pcapng a block boundary). pcapng's section state
  * at *pos comes from the blocks before it: a call that continues the calling
  * thread's previous scan (same img and img_bytes, *pos where that call
- * stopped) resumes with the state it stopped with, any other call re-reads the
- * block headers before *pos — so an image must not be rewritten in place
- * between the calls of one scan. PNETGPU_EFORMAT for a bad
+ * stopped, and the same first 28 bytes and block header at *pos) resumes with
+ * the state it stopped with, any other call re-reads the block headers before
+ * *pos — so an image must not be rewritten in place between the calls of one
+ * scan except from its first bytes on. PNETGPU_EFORMAT for a bad
  * header, an unsupported link type, a truncated record or block, or (pcapng)
  * a block whose two length fields differ or a packet naming an undescribed
  * interface. Link types: Ethernet (1) and raw IP (101, 228, 229) — check

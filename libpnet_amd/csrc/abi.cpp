@@ -4,6 +4,7 @@
 // and launches the HIP kernels of rx_kernel.hip. No compute happens on the
 // host: there is no CPU fallback path in this library.
 #include <hip/hip_runtime.h>
+#include <time.h>
 
 #include <algorithm>
 #include <atomic>
@@ -41,6 +42,7 @@ struct pnetgpu_ctx {
     // gave that launch.
     unsigned long long* d_sched = nullptr;
     uint32_t* done_host = nullptr;
+    uint32_t* done_dev = nullptr;      // the device alias of done_host (hipHostGetDevicePointer): what kernels write
     uint32_t seq[kSchedBlocks] = {};
     uint32_t next_seq = 0;
     uint32_t next_block = 0;
@@ -139,7 +141,7 @@ int plan_sched(pnetgpu_ctx* ctx, uint64_t nunits, uint64_t nwaves, void* stream,
     s->nstatic = (nunits * (uint64_t)static_pct / 100) / nwaves * nwaves;
     s->ctr = ctr;
     s->groups_done = ctr + (size_t)kMaxCtrs * kCtrStride;
-    s->done_host = ctx->done_host + b;
+    s->done_host = ctx->done_dev + b;
     s->seq = ctx->seq[b];
     const int64_t tn = tuning(ctx, PNETGPU_TUNE_CLAIM_COUNTERS);
     const uint64_t nctr = tn > 0 ? (uint64_t)tn : PNET_CLAIM_COUNTERS;
@@ -263,6 +265,10 @@ int pnetgpu_ctx_create(int device, pnetgpu_ctx** out) {
         pnetgpu_ctx_destroy(c);
         return PNETGPU_ENOMEM;
     }
+    if (hipHostGetDevicePointer((void**)&c->done_dev, c->done_host, 0) != hipSuccess || !c->done_dev) {
+        pnetgpu_ctx_destroy(c);
+        return PNETGPU_EHIP;
+    }
     for (uint32_t i = 0; i < kSchedBlocks; ++i) c->done_host[i] = 0;   // == seq[i]: every block free
     if (hipMemset(c->d_sched, 0, kSchedBytes) != hipSuccess) {
         pnetgpu_ctx_destroy(c);
@@ -307,9 +313,24 @@ int pnetgpu_ctx_sched_stats(const pnetgpu_ctx* ctx, uint64_t stats[PNETGPU_NSCHE
 void pnetgpu_ctx_destroy(pnetgpu_ctx* ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
-    // launches still in flight write their counter block and host word: let
-    // them finish before the pool goes away
-    if (ctx->d_sched) (void)hipDeviceSynchronize();
+    // launches still in flight write their counter block and host word: wait
+    // for exactly those (each held block's word reaching its sequence number),
+    // not for every stream of the device; static and graph-captured launches
+    // never touch the pool. A block not handed back within 30 s (a faulted
+    // device) falls back to a device-wide synchronize, which reports the fault.
+    if (ctx->d_sched && ctx->done_host) {
+        bool held = true;
+        for (int spin = 0; held && spin < 600000; ++spin) {
+            held = false;
+            for (uint32_t i = 0; i < kSchedBlocks && !held; ++i)
+                held = __atomic_load_n(&ctx->done_host[i], __ATOMIC_ACQUIRE) != ctx->seq[i];
+            if (held) {
+                const timespec ts{0, 50000};
+                nanosleep(&ts, nullptr);
+            }
+        }
+        if (held) (void)hipDeviceSynchronize();
+    }
     if (ctx->d_sched) (void)hipFree(ctx->d_sched);
     if (ctx->done_host) (void)hipHostFree(ctx->done_host);
     delete ctx;

@@ -162,10 +162,30 @@ int ng_walk(const uint8_t* img, uint64_t img_bytes, uint64_t from, uint64_t cap,
 // instead of walking the block headers from byte 0 again (which made a scan of
 // n packets in batches of k cost n^2 / k block reads). Per thread: a scan's
 // calls come from one thread; any other call walks from byte 0 as before.
+// A resumed call must be the same image, not another one of the same size that
+// the allocator placed at the same address: the image's first 28 bytes (its
+// SHB header) and the 12 bytes of the block at pos are matched too.
 struct NgResume {
     const uint8_t* img = nullptr;
     uint64_t img_bytes = 0, pos = 0;
+    uint8_t head[28] = {}, at[12] = {};
     NgState st;
+    static size_t head_len(uint64_t img_bytes) { return (size_t)std::min<uint64_t>(28, img_bytes); }
+    static size_t at_len(uint64_t img_bytes, uint64_t pos) {
+        return pos < img_bytes ? (size_t)std::min<uint64_t>(12, img_bytes - pos) : 0;
+    }
+    bool matches(const uint8_t* i, uint64_t n, uint64_t p) const {
+        return p && img == i && img_bytes == n && pos == p && std::memcmp(head, i, head_len(n)) == 0 &&
+               std::memcmp(at, i + p, at_len(n, p)) == 0;
+    }
+    void keep(const uint8_t* i, uint64_t n, uint64_t p, const NgState& s) {
+        img = i;
+        img_bytes = n;
+        pos = p;
+        st = s;
+        std::memcpy(head, i, head_len(n));
+        std::memcpy(at, i + p, at_len(n, p));
+    }
 };
 thread_local NgResume g_resume;
 
@@ -302,7 +322,7 @@ int pnetgpu_pcap_scan(const uint8_t* img, uint64_t img_bytes, uint64_t* pos, uin
         // headers only until then)
         NgState st;
         uint64_t start = 0;
-        if (*pos && g_resume.img == img && g_resume.img_bytes == img_bytes && g_resume.pos == *pos) {
+        if (g_resume.matches(img, img_bytes, *pos)) {
             st = g_resume.st;     // *pos is a block boundary this thread's last scan of the image stopped at
             start = *pos;
         }
@@ -315,10 +335,7 @@ int pnetgpu_pcap_scan(const uint8_t* img, uint64_t img_bytes, uint64_t* pos, uin
         g_resume.img = nullptr;
         if (rc) return rc;
         if (k && linktype_flags(st.linktype, &flags)) return PNETGPU_EFORMAT;
-        g_resume.img = img;
-        g_resume.img_bytes = img_bytes;
-        g_resume.pos = next;
-        g_resume.st = st;
+        g_resume.keep(img, img_bytes, next, st);
         *n = k;
         *pos = next;
         return PNETGPU_OK;

@@ -130,7 +130,8 @@ def test_counter_blocks_reused_across_many_launches(tune):
 def test_more_launches_in_flight_than_blocks(tune):
     """Four streams held behind a spin kernel: the first 64 launches take the
     pool's 64 blocks, the other 36 find every block held and run the static
-    schedule. Every record equals the oracle's, and once the launches are done
+    schedule (exactly so when the gate still held after the last enqueue; a
+    host slower than the gate sees blocks come back, and only the totals hold). Every record equals the oracle's, and once the launches are done
     every block is back."""
     n = 8 * 1024 * 64                         # 8 runs x 256 CUs x 4 waves x 64 frames
     w = lp.synth.make("udp64", n, seed=17, corrupt_ppm=10000)
@@ -151,8 +152,11 @@ def test_more_launches_in_flight_than_blocks(tune):
     assert s0["blocks_held"] == 0 and s0["blocks"] == 64
     results = [dv.run(n, stream=streams[i % 4], out=outs[i]) for i in range(100)]
     d = _delta(s0, _stats())
+    gate_held = not gate.query()              # no launch can have finished and handed a block back
     torch.cuda.synchronize()
-    assert d == {"claimed": 64, "static_busy": 36, "static_captured": 0}, d
+    assert d["claimed"] + d["static_busy"] == 100 and d["claimed"] >= 64 and d["static_captured"] == 0, d
+    if gate_held:                             # a slow host can outlast the gate: then the split is not fixed
+        assert d == {"claimed": 64, "static_busy": 36, "static_captured": 0}, d
     compare(results[0], rec)
     for i, r in enumerate(results):
         for c, col in r.columns.items():

@@ -187,3 +187,34 @@ def test_pcapng_scan_resumes_and_restarts():
     for s in stops[::-1][:6]:
         _, r = _scan(a, s, 10 ** 6)
         assert r == [x for x in want_a if x[0] >= s]
+
+
+def test_pcapng_scan_resume_checks_the_image_not_only_its_address():
+    """A batched pcapng scan resumes with the section state its previous call
+    stopped with only when the image is the same one: a different image of the
+    same size rewritten into the same buffer (as allocator reuse would place
+    it) is walked from its own headers again, so its records come out right."""
+    import ctypes
+    from libpnet_amd._lib import lib
+    from tests.pcaputil import pcapng_bytes
+    rng = np.random.default_rng(4)
+    lens = rng.integers(60, 200, 40)
+    fa = [bytes(rng.integers(0, 256, n, dtype=np.uint8)) for n in lens]
+    fb = [bytes(rng.integers(0, 256, n, dtype=np.uint8)) for n in lens]
+    a, b = pcapng_bytes(fa), pcapng_bytes(fb, big_endian=True)
+    assert len(a) == len(b)
+    buf = np.frombuffer(a, np.uint8).copy()
+    offs = np.zeros(64, np.uint64)
+    lns = np.zeros(64, np.uint32)
+    pos, n = ctypes.c_uint64(0), ctypes.c_uint64()
+
+    def scan(cap):
+        rc = lib.pnetgpu_pcap_scan(ctypes.c_void_p(buf.ctypes.data), buf.size, ctypes.byref(pos),
+                                   ctypes.c_void_p(offs.ctypes.data), ctypes.c_void_p(lns.ctypes.data), cap,
+                                   ctypes.byref(n))
+        assert rc == 0
+        return [bytes(buf[int(o):int(o) + int(ln)]) for o, ln in zip(offs[:n.value], lns[:n.value])]
+
+    assert scan(5) == fa[:5]
+    buf[:] = np.frombuffer(b, np.uint8)        # another image, same size, same address
+    assert scan(64) == fb[5:]
