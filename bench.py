@@ -294,14 +294,16 @@ def _link(frames, el, up, down):
 VERIFY_COLUMNS = ("status", "ip_csum", "l4_csum")
 
 
-def e2e_rate(sh, device, chunks=16, reps=3, columns=None):
+def e2e_rate(sh, device, chunks=16, reps=3, columns=None, verify=None):
     """PCIe-inclusive rate: pinned host frames -> H2D -> kernel -> D2H of the results,
     double-buffered on two streams. Fixed-stride batches ship the frames only;
     descriptor batches (IMIX) ship each chunk's frame span plus its compact
     descriptors (u32 offset rebased to the chunk + u16 length, 6 B/frame) with
     the size hint the ring would give. Reported beside `value`, never as `value`.
     `stages`: per-stage device time summed over the timed chunks (HIP events on
-    the two streams, so H2D of one chunk overlaps the kernel / D2H of the other)."""
+    the two streams, so H2D of one chunk overlaps the kernel / D2H of the other).
+    verify(first_frame, n, result): called (tests) for the last two chunks after
+    the timed region, with the device result they left in the two buffers."""
     columns = columns or lp.IPV4_COLUMNS
     w = sh.w
     n = sh.n
@@ -376,6 +378,9 @@ def e2e_rate(sh, device, chunks=16, reps=3, columns=None):
             chunk(k, True)
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
+    if verify:
+        for k in (chunks - 2, chunks - 1):
+            verify(k * per, per, res[k % 2])
     frames = reps * chunks * per
     nbytes = reps * sum(e - b for b, e in spans)
     st = {"h2d_s": 0.0, "kernel_s": 0.0, "d2h_s": 0.0}
