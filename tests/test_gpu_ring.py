@@ -283,3 +283,50 @@ def test_ring_jumbo_batches_and_stage_stats(producer):
     assert st["h2d_ms"] > 0 and st["kernel_ms"] > 0 and st["d2h_ms"] > 0
     assert st["wait_ns"] > 0 and st["submit_ns"] > 0 and st["host_threads"] >= 1
     assert (st["push_ns"] > 0) == (producer == "push_many")
+
+
+_AFFINITY_CHILD = r"""
+import json, os, sys
+os.sched_setaffinity(0, {cpus})
+sys.path.insert(0, {root!r})
+import numpy as np
+import libpnet_amd as lp
+from oracle import coracle
+tasks = lambda: set(os.listdir("/proc/self/task"))
+w = lp.synth.make("imix", 150000, seed=21)
+ring = lp.Ring(batch_bytes=8 << 20, batch_frames=1 << 17, copy=True)
+before = tasks()
+out = sorted(list(ring.feed_many(w.buf, w.offsets, w.lengths)) + list(ring.drain()), key=lambda b: b.id)
+st = ring.stats()
+ring.close()
+ok = sum(b.n for b in out) == 150000
+i = 0
+for b in out:
+    rec = coracle.rx_batch(b.frames, b.n, offsets=b.offsets, lengths=b.lengths)
+    ok = ok and all(np.array_equal(v, rec[c]) for c, v in b.records.items())
+    ok = ok and np.array_equal(b.lengths, w.lengths[i:i + b.n])
+    i += b.n
+print(json.dumps({{"threads": lp.host_threads(), "stats_threads": st["host_threads"], "ok": bool(ok),
+                   "batches": len(out), "push_ns": st["push_ns"]}}))
+"""
+
+
+def test_ring_push_many_two_cpus():
+    """pnetgpu_ring_push_many in a process limited to two CPUs: its pool has
+    two threads (the caller and one worker), every batch equals the oracle,
+    and the ring's statistics report the pool size."""
+    import json
+    import os
+    import subprocess
+    import sys
+    cpus = set(sorted(os.sched_getaffinity(0))[:2])
+    if len(cpus) < 2:
+        pytest.skip("needs 2 CPUs")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k != "PNETGPU_HOST_THREADS"}
+    p = subprocess.run([sys.executable, "-c", _AFFINITY_CHILD.format(cpus=cpus, root=root)], cwd=root, env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stderr[-3000:]
+    r = json.loads(p.stdout.strip().splitlines()[-1])
+    assert r["threads"] == 2 and r["stats_threads"] == 2
+    assert r["ok"] and r["batches"] > 3 and r["push_ns"] > 0
