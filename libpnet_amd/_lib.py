@@ -17,7 +17,7 @@ ROOT = os.path.dirname(PKG_DIR)
 # PNETGPU_LIB selects an alternative build of the same library (tuning A/B runs)
 LIB_PATH = os.environ.get("PNETGPU_LIB") or os.path.join(PKG_DIR, "libpnetgpu.so")
 HEADERS = [os.path.join(ROOT, "include", h)
-           for h in ("pnetgpu.h", "pnetgpu_synth.h", "pnetgpu_ring.h", "pnetgpu_afpacket.h")]
+           for h in ("pnetgpu.h", "pnetgpu_synth.h", "pnetgpu_ring.h", "pnetgpu_afpacket.h", "pnetgpu_util.h")]
 
 
 class PnetGpuError(RuntimeError):

@@ -51,10 +51,38 @@ struct pnetgpu_ctx {
     uint64_t captured_static = 0;      // launches captured into a graph: static schedule
     // PNETGPU_TUNE_* (-1: default), from the environment at creation only
     int64_t tune[PNETGPU_NTUNE];
+    // host-memory entry points (pnetgpu_util.h): device scratch they stage
+    // through and the stream they run on, both created on first use
+    uint8_t* util_scratch = nullptr;
+    size_t util_cap = 0;
+    hipStream_t util_stream = nullptr;
 };
 
 namespace pnetgpu {
 int ctx_device(const pnetgpu_ctx* ctx) { return ctx->device; }
+
+int ctx_util_scratch(pnetgpu_ctx* ctx, size_t bytes, uint8_t** d, hipStream_t* stream) {
+    if (hipSetDevice(ctx->device) != hipSuccess) return hip_fail(hipGetLastError());
+    if (!ctx->util_stream && hipStreamCreateWithFlags(&ctx->util_stream, hipStreamNonBlocking) != hipSuccess) {
+        ctx->util_stream = nullptr;
+        return hip_fail(hipGetLastError());
+    }
+    if (bytes > ctx->util_cap) {
+        size_t cap = 1u << 16;
+        while (cap < bytes) cap *= 2;
+        uint8_t* p = nullptr;
+        if (hipMalloc((void**)&p, cap) != hipSuccess) {
+            (void)hipGetLastError();
+            return PNETGPU_ENOMEM;
+        }
+        if (ctx->util_scratch) (void)hipFree(ctx->util_scratch);   // no staged call is in flight: each one syncs
+        ctx->util_scratch = p;
+        ctx->util_cap = cap;
+    }
+    *d = ctx->util_scratch;
+    *stream = ctx->util_stream;
+    return PNETGPU_OK;
+}
 static thread_local int g_last_hip_error = 0;
 int last_hip_error() { return g_last_hip_error; }
 void set_last_hip_error(int e) { g_last_hip_error = e; }
@@ -331,6 +359,9 @@ void pnetgpu_ctx_destroy(pnetgpu_ctx* ctx) {
         }
         if (held) (void)hipDeviceSynchronize();
     }
+    if (ctx->util_stream) (void)hipStreamSynchronize(ctx->util_stream);
+    if (ctx->util_scratch) (void)hipFree(ctx->util_scratch);
+    if (ctx->util_stream) (void)hipStreamDestroy(ctx->util_stream);
     if (ctx->d_sched) (void)hipFree(ctx->d_sched);
     if (ctx->done_host) (void)hipHostFree(ctx->done_host);
     delete ctx;

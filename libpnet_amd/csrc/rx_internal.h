@@ -122,6 +122,9 @@ constexpr uint32_t kHintJumboMin = 4096;    // bytes: a frame of the jumbo shape
 
 // device index a context is bound to (abi.cpp)
 int ctx_device(const pnetgpu_ctx* ctx);
+// the context's device scratch of at least `bytes` (grown on demand) and its
+// own stream, for the host-memory entry points (util_host.cpp); sets the device
+int ctx_util_scratch(pnetgpu_ctx* ctx, size_t bytes, uint8_t** d, hipStream_t* stream);
 
 int rx_blocks_per_cu(int kind, bool ext, int* numregs, int* lds);
 int rx_waves_per_block(int kind);

@@ -197,3 +197,77 @@ class icmpv6:
     def checksum(packet, source, destination):
         """icmpv6::checksum: util::ipv6_checksum(packet, 1, &[], src, dst, Icmpv6) (icmpv6.rs:80-85)."""
         return util.ipv6_checksum(packet, 1, b"", source, destination, 58)
+
+
+def _host_setup():
+    import ctypes
+    from ._lib import lib
+    vp, u64, u8 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint8
+    lib.pnetgpu_util_checksum.restype = ctypes.c_int
+    lib.pnetgpu_util_checksum.argtypes = [vp, vp, u64, u64, ctypes.POINTER(ctypes.c_uint16)]
+    for fn in (lib.pnetgpu_util_ipv4_checksum, lib.pnetgpu_util_ipv6_checksum):
+        fn.restype = ctypes.c_int
+        fn.argtypes = [vp, vp, u64, u64, vp, u64, vp, vp, u8, ctypes.POINTER(ctypes.c_uint16)]
+    lib.pnetgpu_checksum_slices_host.restype = ctypes.c_int
+    lib.pnetgpu_checksum_slices_host.argtypes = [vp, vp, u64, u64, vp, vp, vp, vp]
+    return ctypes, lib
+
+
+class util_host:
+    """pnet_packet::util's three functions through the host-memory C-ABI
+    (include/pnetgpu_util.h: the entry points a Rust or C caller replacing one
+    `util::checksum(&[u8], usize)` call binds): host bytes in, the word out, one
+    synchronous staged launch on the context's own stream."""
+
+    @staticmethod
+    def _buf(b):
+        b = bytes(b)
+        return b, (len(b) and b) or None
+
+    @staticmethod
+    def checksum(data, skipword):
+        ctypes, lib = _host_setup()
+        from ._lib import check
+        data, p = util_host._buf(data)
+        out = ctypes.c_uint16()
+        check(lib.pnetgpu_util_checksum(engine.context(_DEVICE[0]).handle, p, len(data), int(skipword),
+                                        ctypes.byref(out)), "pnetgpu_util_checksum")
+        return int(out.value)
+
+    @staticmethod
+    def _pseudo(version, data, skipword, extra_data, source, destination, next_level_protocol):
+        ctypes, lib = _host_setup()
+        from ._lib import check
+        alen = 4 if version == 4 else 16
+        data, p = util_host._buf(data)
+        extra, e = util_host._buf(extra_data or b"")
+        s, d = _addr(source, alen), _addr(destination, alen)
+        fn = lib.pnetgpu_util_ipv4_checksum if version == 4 else lib.pnetgpu_util_ipv6_checksum
+        out = ctypes.c_uint16()
+        check(fn(engine.context(_DEVICE[0]).handle, p, len(data), int(skipword), e, len(extra), s, d,
+                 int(next_level_protocol) & 0xFF, ctypes.byref(out)), f"pnetgpu_util_ipv{version}_checksum")
+        return int(out.value)
+
+    @staticmethod
+    def ipv4_checksum(data, skipword, extra_data, source, destination, next_level_protocol):
+        return util_host._pseudo(4, data, skipword, extra_data, source, destination, next_level_protocol)
+
+    @staticmethod
+    def ipv6_checksum(data, skipword, extra_data, source, destination, next_level_protocol):
+        return util_host._pseudo(6, data, skipword, extra_data, source, destination, next_level_protocol)
+
+    @staticmethod
+    def checksum_slices(buf, offsets, lengths, skipwords):
+        """pnetgpu_checksum_slices_host over host numpy arrays; returns uint16 words."""
+        ctypes, lib = _host_setup()
+        from ._lib import check
+        buf = np.ascontiguousarray(buf, np.uint8)
+        offsets = np.ascontiguousarray(offsets, np.uint64)
+        lengths = np.ascontiguousarray(lengths, np.uint32)
+        skipwords = np.ascontiguousarray(skipwords, np.uint32)
+        n = len(offsets)
+        out = np.zeros(n, np.uint16)
+        check(lib.pnetgpu_checksum_slices_host(engine.context(_DEVICE[0]).handle, buf.ctypes.data, buf.size, n,
+                                               offsets.ctypes.data, lengths.ctypes.data, skipwords.ctypes.data,
+                                               out.ctypes.data), "pnetgpu_checksum_slices_host")
+        return out

@@ -72,7 +72,7 @@ def test_argument_validation_without_gpu():
 
 
 def test_include_headers_compile_as_c():
-    for h in ("pnetgpu.h", "pnetgpu_synth.h", "pnetgpu_ring.h", "pnetgpu_afpacket.h"):
+    for h in ("pnetgpu.h", "pnetgpu_synth.h", "pnetgpu_ring.h", "pnetgpu_afpacket.h", "pnetgpu_util.h"):
         subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-fsyntax-only", "-x", "c",
                         os.path.join(ROOT, "include", h)], check=True)
 

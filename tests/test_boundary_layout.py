@@ -78,7 +78,7 @@ def test_rust_mirror_matches_the_c_header(cname):
 def test_rust_extern_block_declares_every_entry_point():
     text = open(os.path.join(ROOT, "INTEGRATION.md")).read()
     declared = set(re.findall(r"pub fn (\w+)\(", text))
-    for h in ("pnetgpu.h", "pnetgpu_ring.h", "pnetgpu_afpacket.h"):
+    for h in ("pnetgpu.h", "pnetgpu_ring.h", "pnetgpu_afpacket.h", "pnetgpu_util.h"):
         src = re.sub(r"/\*.*?\*/", "", open(os.path.join(ROOT, "include", h)).read(), flags=re.S)
         for fn in re.findall(r"^\s*(?:int|void|const char\*|uint\w+)\s+\**(pnetgpu_\w+)\s*\(", src, re.M):
             assert fn in declared, f"{h}: {fn} missing from the INTEGRATION.md Rust binding"

@@ -12,10 +12,11 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 EXE = os.path.join(ROOT, "libpnet_amd", "build", "rx_verify")
 SENDER = os.path.join(ROOT, "libpnet_amd", "build", "rs_sender")
+UTIL = os.path.join(ROOT, "libpnet_amd", "build", "util_checksum")
 
 
 def test_example_built_and_linked():
-    for exe in (EXE, SENDER):
+    for exe in (EXE, SENDER, UTIL):
         assert os.access(exe, os.X_OK), "run `make -C libpnet_amd` (build())"
         out = subprocess.run(["ldd", exe], capture_output=True, text=True, check=True).stdout
         assert "libpnetgpu.so" in out and "not found" not in out
@@ -52,3 +53,23 @@ def test_rs_sender_fills_what_the_oracle_computes(tmp_path):
                               frame_len=64)
     assert np.array_equal(buf, want[: n * 64])
 
+
+
+@pytest.mark.gpu
+def test_util_checksum_example_reference_kats():
+    """examples/util_checksum.c (pnetgpu_util.h from plain C, host bytes in,
+    the word out) on the reference's own KATs: icmp.rs:82-108's checksums,
+    udp.rs:58-100 (0x9178) and tcp.rs:288-357."""
+    from tests import kats
+
+    def run(*args):
+        r = subprocess.run([UTIL, *args], capture_output=True, text=True, timeout=60)
+        assert r.returncode == 0, r.stderr
+        return int(r.stdout.strip(), 16)
+
+    for v in kats.by_kind("checksum"):
+        assert run(bytes(v["data"]).hex(), str(v["skipword"])) == v["expected"], v["name"]
+    v4 = {v["name"]: v for v in kats.by_kind("ipv4_checksum")}
+    assert run("-4", bytes(v4["udp_ipv4_checksum"]["data"]).hex(), "3", "c0a80001", "c0a800c7", "17") == 0x9178
+    assert run("-4", bytes(v4["tcp_ipv4_checksum"]["data"]).hex(), "8", "c0a80201", "c0a86f33", "6") == \
+        v4["tcp_ipv4_checksum"]["expected"]
