@@ -1,5 +1,6 @@
 // host_asan_test.cpp — AddressSanitizer/UBSan run of the library's HOST code
-// (no GPU needed): the synthetic-frame producer, the classic-pcap and pcapng
+// (no GPU needed): the synthetic-frame producer, the batch producer's parallel
+// pack (fuzzed, on the host pool's threads), the classic-pcap and pcapng
 // readers and in-memory indexers (fuzzed), the TPACKET_V3 block walk (fuzzed: it parses memory the
 // OS kernel writes) and the C-ABI's argument validation. Linked from objects built with
 // -fsanitize=address,undefined (libpnet_amd/Makefile target `asan-test`), so
@@ -16,8 +17,10 @@
 #include "pnetgpu_afpacket.h"
 #include "pnetgpu_ring.h"
 #include "pnetgpu_synth.h"
+#include "pnetgpu_util.h"
 
 static int failures = 0;
+static uint32_t rnd();
 #define CHECK(c)                                                              \
     do {                                                                      \
         if (!(c)) {                                                           \
@@ -150,6 +153,53 @@ static void test_abi_validation() {
     pnetgpu_ctx_destroy(nullptr);
     pnetgpu_ring_destroy(nullptr);
     pnetgpu_pcap_close(nullptr);
+    // host-memory util entry points (pnetgpu_util.h): argument checks before any HIP call
+    uint8_t a4[4] = {};
+    CHECK(pnetgpu_util_checksum(nullptr, data, 16, 0, out) == PNETGPU_EINVAL);
+    CHECK(pnetgpu_util_ipv4_checksum(nullptr, data, 16, 0, nullptr, 0, a4, a4, 17, out) == PNETGPU_EINVAL);
+    CHECK(pnetgpu_util_ipv6_checksum(nullptr, data, 16, 0, nullptr, 0, a4, a4, 17, out) == PNETGPU_EINVAL);
+    CHECK(pnetgpu_checksum_slices_host(nullptr, data, 16, 4, off, len, skip, out) == PNETGPU_EINVAL);
+    CHECK(pnetgpu_batch_pack(nullptr, off, len, 4, data, 16, off, len, nullptr, nullptr) == PNETGPU_EINVAL);
+}
+
+// pnetgpu_batch_pack (the pnetgpu_ring_push_many pass on the persistent host
+// pool) over random frame layouts and capacities: the frames taken are the
+// longest prefix that fits, copied byte for byte to their packed offsets, and
+// nothing is written past the destination (ASan guards its end).
+static void test_pack_fuzz() {
+    CHECK(pnetgpu_host_threads() >= 1);
+    for (int round = 0; round < 40; ++round) {
+        const uint64_t n = round % 4 == 0 ? 70000 + rnd() % 40000 : 1 + rnd() % 3000;
+        std::vector<uint64_t> offs(n), doff(n, ~0ull);
+        std::vector<uint32_t> lens(n), dlen(n, ~0u);
+        uint64_t at = 0, total = 0;
+        for (uint64_t i = 0; i < n; ++i) {
+            const uint32_t r = rnd() % 100;
+            lens[i] = r < 60 ? 64 : r < 90 ? 576 : r < 98 ? 1500 : 9000;
+            at += (rnd() % 4 == 0) ? rnd() % 40 : 0;     // gaps: copies break inside chunks
+            offs[i] = at;
+            at += lens[i];
+            total += lens[i];
+        }
+        std::vector<uint8_t> src(at);
+        for (auto& b : src) b = (uint8_t)rnd();
+        const uint64_t cap = round % 3 == 0 ? total : 1 + rnd() % (total + 1);
+        std::vector<uint8_t> dst(cap);
+        uint64_t k = 0, bytes = 0;
+        const int rc = pnetgpu_batch_pack(src.data(), offs.data(), lens.data(), n, dst.data(), cap, doff.data(),
+                                          dlen.data(), &k, &bytes);
+        uint64_t want = 0, wb = 0;
+        while (want < n && lens[want] <= cap - wb) wb += lens[want++];
+        CHECK(want == 0 ? rc == PNETGPU_EFULL : rc == PNETGPU_OK);
+        CHECK(k == want && bytes == wb);
+        uint64_t o = 0;
+        for (uint64_t i = 0; i < k; ++i) {
+            CHECK(doff[i] == o && dlen[i] == lens[i]);
+            CHECK(std::memcmp(dst.data() + o, src.data() + offs[i], lens[i]) == 0);
+            o += lens[i];
+        }
+        CHECK(k == n || doff[k] == ~0ull);              // nothing past the cut
+    }
 }
 
 // Random mutations of valid TPACKET_V3 blocks and pcap images: every call
@@ -336,6 +386,7 @@ int main() {
     test_synth();
     test_pcap();
     test_abi_validation();
+    test_pack_fuzz();
     test_walk_fuzz();
     test_scan_fuzz();
     test_pcapng_fuzz();
