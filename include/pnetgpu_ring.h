@@ -77,7 +77,7 @@ typedef struct pnetgpu_ring_stats {
     uint64_t batches;         /* batches shipped (submit / submit_region)                     */
     uint64_t frames;          /* frames in them                                               */
     uint64_t bytes;           /* bytes shipped host -> device (the frame spans)               */
-    uint64_t push_ns;         /* inside pnetgpu_ring_push_many: descriptors + copies          */
+    uint64_t push_ns;         /* push_many: descriptors + copies; submit_region: descriptors */
     uint64_t submit_ns;       /* inside submit / submit_region: enqueueing H2D, kernel, D2H   */
     uint64_t wait_ns;         /* inside pnetgpu_ring_wait, blocked on the oldest batch        */
     uint64_t timed_batches;   /* batches whose device stages were timed                       */

@@ -502,24 +502,85 @@ int pnetgpu_ring_submit_region(pnetgpu_ring* r, const uint8_t* base, const uint6
     Slot& s = r->slots[r->filling];
     if (s.n) return PNETGPU_EFULL;               // pushed frames are waiting: submit them first
     // the longest prefix of frames, ascending and non-overlapping, whose span fits the slot
+    const uint64_t t_desc = now_ns();
     const uint64_t o0 = offsets[0];
+    const uint64_t limit = std::min<uint64_t>(n, r->cap_frames);
     uint64_t k = 0, end = o0, fbytes = 0, large = 0, jumbo = 0;
     uint32_t mx = 0;
-    while (k < n && k < r->cap_frames) {
-        if (offsets[k] < end) return PNETGPU_EINVAL;   // frames must ascend without overlap
-        const uint64_t fe = offsets[k] + lengths[k];
-        if (fe - o0 > r->cap_bytes) break;
-        s.h_off[k] = offsets[k] - o0;
-        s.h_len[k] = lengths[k];
-        s.h_off32[k] = (uint32_t)(offsets[k] - o0);
-        s.h_len16[k] = (uint16_t)lengths[k];
-        mx = std::max(mx, lengths[k]);
-        fbytes += lengths[k];
-        large += lengths[k] >= pnetgpu::kHintLargeMin;
-        jumbo += lengths[k] >= pnetgpu::kHintJumboMin ? lengths[k] : 0;
-        end = fe;
-        ++k;
+    auto desc_range = [&](uint64_t lo, uint64_t hi) {   // descriptors + size statistics of [lo, hi)
+        PackStats st;
+        for (uint64_t i = lo; i < hi; ++i) {
+            const uint32_t len = lengths[i];
+            s.h_off[i] = offsets[i] - o0;
+            s.h_len[i] = len;
+            s.h_off32[i] = (uint32_t)(offsets[i] - o0);
+            s.h_len16[i] = (uint16_t)len;
+            st.max_len = std::max(st.max_len, len);
+            st.bytes += len;
+            st.n_large += len >= pnetgpu::kHintLargeMin;
+            st.jumbo_bytes += len >= pnetgpu::kHintJumboMin ? len : 0;
+        }
+        return st;
+    };
+    bool done = false;
+    const unsigned nt = limit >= (1u << 16) ? pnetgpu::host_threads() : 1u;
+    if (nt > 1) {
+        // Parallel form (a 64-B batch of 2^20 frames took ~1.4 ms on one thread,
+        // the zero-copy producer's whole budget per batch): ascending frames have
+        // ascending ends, so the cut is a binary search over the ends; then every
+        // chunk of [0, cut] checks the order and the fit (the cut frame: order
+        // only) while it writes its descriptors. Any anomaly (an overlap or a
+        // descending frame) reruns the serial pass below, whose result is the
+        // contract.
+        auto fits = [&](uint64_t i) { return offsets[i] >= o0 && offsets[i] + lengths[i] - o0 <= r->cap_bytes; };
+        uint64_t lo = 0, hi = limit;                     // largest prefix whose last frame fits
+        while (lo < hi) {
+            const uint64_t mid = lo + (hi - lo + 1) / 2;
+            if (fits(mid - 1)) lo = mid;
+            else hi = mid - 1;
+        }
+        const uint64_t kk = lo, checked = std::min(kk + 1, limit);
+        if (kk > 0) {
+            std::vector<PackStats> cst(nt);
+            std::vector<uint8_t> bad(nt, 0);
+            pnetgpu::parallel_run(nt, [&](unsigned t) {
+                const uint64_t a = checked * t / nt, b = checked * (t + 1) / nt;
+                for (uint64_t i = std::max<uint64_t>(a, 1); i < b; ++i)
+                    if (offsets[i] < offsets[i - 1] + lengths[i - 1]) bad[t] = 1;
+                for (uint64_t i = a; i < std::min(b, kk); ++i)
+                    if (!fits(i)) bad[t] = 1;
+                cst[t] = desc_range(a, std::min(b, kk));
+            });
+            bool ok = true;
+            for (unsigned t = 0; t < nt; ++t) ok = ok && !bad[t];
+            if (ok) {
+                k = kk;
+                end = offsets[k - 1] + lengths[k - 1];
+                for (const PackStats& c : cst) {
+                    mx = std::max(mx, c.max_len);
+                    fbytes += c.bytes;
+                    large += c.n_large;
+                    jumbo += c.jumbo_bytes;
+                }
+                done = true;
+            }
+        }
     }
+    if (!done) {
+        while (k < limit) {
+            if (offsets[k] < end) return PNETGPU_EINVAL;   // frames must ascend without overlap
+            const uint64_t fe = offsets[k] + lengths[k];
+            if (fe - o0 > r->cap_bytes) break;
+            end = fe;
+            ++k;
+        }
+        const PackStats st = desc_range(0, k);
+        mx = st.max_len;
+        fbytes = st.bytes;
+        large = st.n_large;
+        jumbo = st.jumbo_bytes;
+    }
+    r->stats.push_ns += now_ns() - t_desc;       // the descriptor pass (no frame copies here)
     if (k == 0) return PNETGPU_EFULL;            // the first frame alone exceeds batch_bytes
     s.n = (uint32_t)k;
     s.bytes = end - o0;                          // the span shipped (gaps included)

@@ -330,3 +330,52 @@ def test_ring_push_many_two_cpus():
     r = json.loads(p.stdout.strip().splitlines()[-1])
     assert r["threads"] == 2 and r["stats_threads"] == 2
     assert r["ok"] and r["batches"] > 3 and r["push_ns"] > 0
+
+
+@pytest.mark.parametrize("batch_bytes", [64 << 20, 6 << 20])
+def test_ring_zero_copy_large_regions(batch_bytes):
+    """submit_region over pushes of >= 2^16 frames (the parallel descriptor pass:
+    binary-searched cut, chunked order and fit checks): IMIX frames with gaps,
+    cut by the slot's frame count (64 MiB) or its bytes (6 MiB); every batch
+    equals the oracle and the frames are the caller's bytes."""
+    w = lp.synth.make("imix", 200000, seed=23, corrupt_ppm=20000)
+    rng = np.random.default_rng(23)
+    gaps = rng.integers(0, 2, w.offsets.size) * rng.integers(0, 24, w.offsets.size)
+    offs = (w.offsets + np.cumsum(gaps)).astype(np.uint64)
+    buf = np.zeros(int(offs[-1] + w.lengths[-1]) + 64, np.uint8)
+    for o, no, n in zip(w.offsets.tolist(), offs.tolist(), w.lengths.tolist()):
+        buf[no:no + n] = w.buf[o:o + n]
+    ring = lp.Ring(batch_bytes=batch_bytes, batch_frames=1 << 17, copy=True)
+    out = sorted(list(ring.feed_region(buf, offs, w.lengths)) + list(ring.drain()), key=lambda b: b.id)
+    ring.close()
+    assert sum(b.n for b in out) == offs.size and len(out) >= 2
+    i = 0
+    for b in out:
+        assert np.array_equal(b.lengths, w.lengths[i:i + b.n])
+        assert np.array_equal(b.offsets.astype(np.uint64) + offs[i], offs[i:i + b.n])
+        rec = coracle.rx_batch(b.frames, b.n, offsets=b.offsets, lengths=b.lengths)
+        for c, v in b.records.items():
+            assert np.array_equal(v, rec[c]), (b.id, c)
+        i += b.n
+    assert sum(b.counters["l4_csum_bad"] for b in out) == w.expect["l4_bad"]
+
+
+def test_ring_zero_copy_large_region_overlap_rejected():
+    """An overlap deep inside a push of 2^17 frames (inside the first batch,
+    then past it) is rejected exactly where the serial contract rejects it:
+    PNETGPU_EINVAL for the batch that contains it, the batches before it shipped."""
+    n = 1 << 17
+    lens = np.full(n, 64, np.uint32)
+    offs = np.arange(n, dtype=np.uint64) * np.uint64(64)
+    buf = np.zeros(n * 64 + 64, np.uint8)
+    for at in (5000, 100000):
+        bad = offs.copy()
+        bad[at] = bad[at - 1] + np.uint64(10)               # overlaps the frame before it
+        ring = lp.Ring(batch_bytes=64 << 20, batch_frames=1 << 16, copy=True)
+        got = []
+        with pytest.raises(PnetGpuError):
+            for b in ring.feed_region(buf, bad, lens):
+                got.append(b.n)
+        # the batches of frames before the overlap that completed before the error
+        assert sum(got) <= (at // (1 << 16)) * (1 << 16)
+        ring.close()
