@@ -282,7 +282,7 @@ def test_ring_jumbo_batches_and_stage_stats(producer):
     assert st["batches"] == st["timed_batches"] == 3 and st["frames"] == n and st["bytes"] == n * 9000
     assert st["h2d_ms"] > 0 and st["kernel_ms"] > 0 and st["d2h_ms"] > 0
     assert st["wait_ns"] > 0 and st["submit_ns"] > 0 and st["host_threads"] >= 1
-    assert (st["push_ns"] > 0) == (producer == "push_many")
+    assert st["push_ns"] > 0                       # push_many: copies + descriptors; zero-copy: descriptors
 
 
 _AFFINITY_CHILD = r"""
