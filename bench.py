@@ -294,7 +294,7 @@ def _link(frames, el, up, down):
 VERIFY_COLUMNS = ("status", "ip_csum", "l4_csum")
 
 
-def e2e_rate(sh, device, chunks=16, reps=3, columns=None, verify=None):
+def e2e_rate(sh, device, chunks=16, reps=3, columns=None, verify=None, seconds=1.5):
     """PCIe-inclusive rate: pinned host frames -> H2D -> kernel -> D2H of the results,
     double-buffered on two streams. Fixed-stride batches ship the frames only;
     descriptor batches (IMIX) ship each chunk's frame span plus its compact
@@ -368,10 +368,17 @@ def e2e_rate(sh, device, chunks=16, reps=3, columns=None, verify=None):
                 ev.setdefault("marks", []).append(marks)
 
     # one untimed pass over the batch first: the first pass from a freshly
-    # pinned buffer measured ~60 % of the later ones (profiles/r05/ring/)
+    # pinned buffer measured ~60 % of the later ones (profiles/r05/ring/); a
+    # second one sizes the timed region to about `seconds` (at least `reps`
+    # passes), comparable with the ring lines' few seconds
     for k in range(chunks):
         chunk(k, False)
     torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    for k in range(chunks):
+        chunk(k, False)
+    torch.cuda.synchronize()
+    reps = max(reps, int(seconds / max(time.perf_counter() - t1, 1e-4)))
     t0 = time.perf_counter()
     for _ in range(reps):
         for k in range(chunks):
