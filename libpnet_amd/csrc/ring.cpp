@@ -288,10 +288,20 @@ static uint64_t pack_frames(const uint8_t* buf, const uint64_t* offsets, const u
                             uint64_t room_b, uint8_t* dst, uint64_t at, uint64_t* off64, uint32_t* len32,
                             uint32_t* off32, uint16_t* len16, PackStats* st) {
     *st = PackStats{};
+    // one pass per chunk: descriptors, size statistics, and the copies of runs
+    // of source-adjacent frames, each issued when the run ends
     auto fill_range = [&](uint64_t lo, uint64_t hi, uint64_t o) {
         PackStats cs;
+        uint64_t run_src = lo < hi ? offsets[lo] : 0, run_dst = o, src_end = run_src;
         for (uint64_t i = lo; i < hi; ++i) {
             const uint32_t len = lengths[i];
+            const uint64_t so = offsets[i];
+            if (so != src_end) {                       // not adjacent to the previous frame: copy that run
+                if (o > run_dst) pnetgpu::stage_copy(dst + run_dst, buf + run_src, o - run_dst);
+                run_src = so;
+                run_dst = o;
+            }
+            src_end = so + len;
             off64[i] = o;
             len32[i] = len;
             if (off32) off32[i] = (uint32_t)o;
@@ -301,14 +311,7 @@ static uint64_t pack_frames(const uint8_t* buf, const uint64_t* offsets, const u
             cs.jumbo_bytes += len >= pnetgpu::kHintJumboMin ? len : 0;
             o += len;
         }
-        uint64_t i = lo;
-        while (i < hi) {
-            uint64_t j = i + 1;
-            while (j < hi && offsets[j] == offsets[j - 1] + lengths[j - 1]) ++j;
-            const uint64_t run = off64[j - 1] + lengths[j - 1] - off64[i];
-            if (run) pnetgpu::stage_copy(dst + off64[i], buf + offsets[i], run);
-            i = j;
-        }
+        if (o > run_dst) pnetgpu::stage_copy(dst + run_dst, buf + run_src, o - run_dst);
         return cs;
     };
     const unsigned threads = pnetgpu::host_threads();
