@@ -3,6 +3,7 @@
 // capture-file readers that feed it are in pcap.cpp).
 #include <hip/hip_runtime.h>
 
+#include <immintrin.h>
 #include <time.h>
 
 #include <algorithm>
@@ -302,9 +303,11 @@ static uint64_t pack_frames(const uint8_t* buf, const uint64_t* offsets, const u
                 run_dst = o;
             }
             src_end = so + len;
-            off64[i] = o;
-            len32[i] = len;
-            if (off32) off32[i] = (uint32_t)o;
+            // non-temporal: the arrays are written once, in order, and read
+            // next by the DMA engine or the consumer (no read-for-ownership)
+            _mm_stream_si64(reinterpret_cast<long long*>(off64 + i), (long long)o);
+            _mm_stream_si32(reinterpret_cast<int*>(len32 + i), (int)len);
+            if (off32) _mm_stream_si32(reinterpret_cast<int*>(off32 + i), (int)(uint32_t)o);
             if (len16) len16[i] = (uint16_t)len;
             cs.max_len = std::max(cs.max_len, len);
             cs.n_large += len >= pnetgpu::kHintLargeMin;
@@ -312,6 +315,7 @@ static uint64_t pack_frames(const uint8_t* buf, const uint64_t* offsets, const u
             o += len;
         }
         if (o > run_dst) pnetgpu::stage_copy(dst + run_dst, buf + run_src, o - run_dst);
+        _mm_sfence();                                  // the streamed descriptors before the hand-over
         return cs;
     };
     const unsigned threads = pnetgpu::host_threads();
