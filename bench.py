@@ -296,7 +296,11 @@ VERIFY_COLUMNS = ("status", "ip_csum", "l4_csum")
 
 def e2e_rate(sh, device, chunks=16, reps=3, columns=None, verify=None, seconds=1.5):
     """PCIe-inclusive rate: pinned host frames -> H2D -> kernel -> D2H of the results,
-    double-buffered on two streams. Fixed-stride batches ship the frames only;
+    double-buffered on two streams, paced as a producer is: a buffer pair is
+    reused once its previous chunk is back (at most two chunks in flight; the
+    two streams then stay out of phase, one's H2D beside the other's D2H, which
+    moved 77-79 GB/s of link traffic where enqueueing every chunk up front moved
+    53-57 on the same box: tools/ring_factor_probe.py). Fixed-stride batches ship the frames only;
     descriptor batches (IMIX) ship each chunk's frame span plus its compact
     descriptors (u32 offset rebased to the chunk + u16 length, 6 B/frame) with
     the size hint the ring would give. Reported beside `value`, never as `value`.
@@ -340,9 +344,13 @@ def e2e_rate(sh, device, chunks=16, reps=3, columns=None, verify=None, seconds=1
         d.zero_()                                     # the granule tail past every span reads zeros
     ev = {}
 
+    done = [None, None]
+
     def chunk(k, timed):
         s, j = streams[k % 2], k % 2
         b, e = spans[k]
+        if done[j] is not None:
+            done[j].synchronize()        # a producer reuses a buffer pair once its last chunk is back
         with torch.cuda.stream(s):
             if timed:
                 marks = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
@@ -366,6 +374,8 @@ def e2e_rate(sh, device, chunks=16, reps=3, columns=None, verify=None, seconds=1
             if timed:
                 marks[3].record(s)
                 ev.setdefault("marks", []).append(marks)
+            done[j] = torch.cuda.Event()
+            done[j].record(s)
 
     # one untimed pass over the batch first: the first pass from a freshly
     # pinned buffer measured ~60 % of the later ones (profiles/r05/ring/); a
@@ -402,7 +412,8 @@ def e2e_rate(sh, device, chunks=16, reps=3, columns=None, verify=None, seconds=1
                        "h2d_gb_s": round(nbytes / st["h2d_s"] / 1e9, 2) if st["h2d_s"] else None,
                        "host_threads": 1},
             "note": "pinned host batch -> hipMemcpyAsync H2D -> rx kernel -> one D2H of the packed record "
-                    f"columns ({rb} B/frame: {', '.join(columns)}), {chunks} chunks double-buffered on 2 streams"
+                    f"columns ({rb} B/frame: {', '.join(columns)}), {chunks} chunks double-buffered on 2 streams, "
+                    "at most 2 in flight"
                     + ("" if desc is None else "; descriptor batch: each chunk's frame span + compact descriptors "
                                                "(6 B/frame) up, with the size hint pnetgpu_desc_size_hint gives")}
 
@@ -443,7 +454,7 @@ def _ring_source(sh):
     return offs, lens
 
 
-def e2e_ring_rate(sh, seconds=3.0, columns=None, slots=None):
+def e2e_ring_rate(sh, seconds=3.0, columns=None, slots=None, stage_times=True):
     """Producer-inclusive rate: frames copied into the pinned ring
     (pnetgpu_ring_push_many: the DataLinkReceiver::next() consumer), shipped,
     verified and the record columns copied back (rotating slots: one filling,
@@ -452,7 +463,7 @@ def e2e_ring_rate(sh, seconds=3.0, columns=None, slots=None):
     w = sh.w
     offs, lens = _ring_source(sh)
     ring = lp.Ring(batch_bytes=64 << 20, batch_frames=1 << 20, copy=False, columns=columns, slots=slots,
-                   stage_times=True)
+                   stage_times=stage_times)
     nslots = ring.slots
     frames = nbytes = nb = 0
     t0 = time.perf_counter()
@@ -475,11 +486,11 @@ def e2e_ring_rate(sh, seconds=3.0, columns=None, slots=None):
             "note": "host frames pushed into the pinned ring with pnetgpu_ring_push_many (descriptors and "
                     f"non-temporal frame copies on a persistent pool of {stages['host_threads']} host threads), "
                     f"async H2D -> rx kernel -> D2H of the record columns ({rb} B/frame: {', '.join(columns)}), "
-                    f"{nslots} rotating slots of 64 MiB / 1 Mi frames",
+                    f"{nslots} rotating slots of 64 MiB / 1 Mi frames on 2 alternating streams",
             "slots": nslots}
 
 
-def e2e_zero_copy_rate(sh, seconds=3.0, columns=None, slots=None):
+def e2e_zero_copy_rate(sh, seconds=3.0, columns=None, slots=None, stage_times=True):
     """Zero-copy producer: the host frames stay where they are (a registered
     buffer, as an mmap'd pcap file or AF_PACKET ring would be) and each batch is
     one DMA of their span (pnetgpu_ring_submit_region), verified, and every
@@ -491,7 +502,7 @@ def e2e_zero_copy_rate(sh, seconds=3.0, columns=None, slots=None):
     buf = w.buf[:span]
     reg = lp.HostRegistration(buf)
     ring = lp.Ring(batch_bytes=64 << 20, batch_frames=1 << 20, copy=False, columns=columns, slots=slots,
-                   stage_times=True)
+                   stage_times=stage_times)
     nslots = ring.slots
     frames = nbytes = nb = 0
     t0 = time.perf_counter()
@@ -516,7 +527,8 @@ def e2e_zero_copy_rate(sh, seconds=3.0, columns=None, slots=None):
             **_ring_link(frames, nbytes, el, rb, nb), "stages": stages,
             "note": "frames DMA'd straight from a registered host buffer (pnetgpu_ring_submit_region, no copy into "
                     f"the ring), rx kernel, D2H of the record columns ({rb} B/frame: {', '.join(columns)}; "
-                    f"pnetgpu_ring_set_columns), {nslots} rotating slots of 64 MiB / 1 Mi frames", "slots": nslots}
+                    f"pnetgpu_ring_set_columns), {nslots} rotating slots of 64 MiB / 1 Mi frames on 2 alternating streams",
+            "slots": nslots}
 
 
 def pack_rate(sh, seconds=1.0):

@@ -8,10 +8,11 @@
  * pnetgpu_ring_push() copies each frame into a pinned host batch (descriptor
  * mode: offsets + lengths), pnetgpu_ring_submit() ships a full batch
  * asynchronously (hipMemcpyAsync H2D -> pnetgpu_rx_process -> D2H of every
- * result column) on the slot's own stream, and pnetgpu_ring_wait() hands back the
+ * result column) on one of the ring's two streams (alternating by submission),
+ * and pnetgpu_ring_wait() hands back the
  * oldest finished batch's records in pinned host memory. Slots rotate (default
  * PNETGPU_RING_DEFAULT_SLOTS: one filling, one held by the application, the
- * rest in flight, each on its own stream), so the H2D of one batch overlaps the
+ * rest in flight on alternating streams), so the H2D of one batch overlaps the
  * kernel and D2H of the previous ones and the application's host work.
  *
  * Validity: a waited batch (its frames and records) stays valid until the next

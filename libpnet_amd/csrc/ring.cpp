@@ -21,7 +21,8 @@
 namespace {
 
 // slots per ring: one filling, one held by the application, the rest in flight
-// (each on its own stream, so H2D of batch k+1 overlaps the kernel and D2H of k)
+// (on two streams alternating by submission, so H2D of batch k+1 overlaps the
+// kernel and D2H of k)
 constexpr int kDefaultSlots = PNETGPU_RING_DEFAULT_SLOTS;
 constexpr int kMaxSlots = PNETGPU_RING_MAX_SLOTS;
 constexpr int kNumCols = 38;       // the 16 record columns, then the 22 header-field columns (ABI v3)
@@ -67,7 +68,6 @@ struct Slot {
     uint8_t* h_rec = nullptr;
     uint64_t col_off[kNumCols] = {};
     uint64_t rec_bytes = 0;
-    hipStream_t stream = nullptr;
     hipEvent_t done = nullptr;
     // PNETGPU_RING_STAGE_TIMES: timing events before the H2D, after it, after
     // the kernel and after the D2H
@@ -113,6 +113,16 @@ struct pnetgpu_ring {
     std::deque<int> inflight;
     uint64_t next_id = 0;
     pnetgpu_ring_stats stats{};
+    // Batches alternate between two streams by submission order (batch id % 2),
+    // whatever slot they fill: consecutive batches overlap (one's H2D with the
+    // other's kernel and D2H) and no two in flight share a stream. Per-slot
+    // streams (round 5) put up to four copies on the link at once and left
+    // batch pairs on one stream whenever the free slots came back out of
+    // order; two alternating streams moved 75 GB/s of link traffic where
+    // three or four moved 60-69 on the same box (tools/ring_factor_probe.py,
+    // profiles/r06/e2e/).
+    static constexpr int kStreams = 2;
+    hipStream_t streams[kStreams] = {};
 };
 
 
@@ -130,7 +140,6 @@ static void free_slot(Slot& s) {
     if (s.done) (void)hipEventDestroy(s.done);
     for (hipEvent_t e : s.stage)
         if (e) (void)hipEventDestroy(e);
-    if (s.stream) (void)hipStreamDestroy(s.stream);
     s = Slot{};
 }
 
@@ -201,6 +210,7 @@ int pnetgpu_ring_create_ex(pnetgpu_ctx* ctx, uint64_t batch_bytes, uint32_t batc
         return pnetgpu::hip_fail(hipGetLastError());
     }
     bool ok = true;
+    for (auto& st : r->streams) ok = ok && hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess;
     for (int i = 0; i < r->nslots && ok; ++i) {
         Slot& s = r->slots[i];
         const size_t fb = batch_bytes + 32;    // granule tail
@@ -212,7 +222,6 @@ int pnetgpu_ring_create_ex(pnetgpu_ctx* ctx, uint64_t batch_bytes, uint32_t batc
              hipMalloc((void**)&s.d_frames, fb) == hipSuccess &&
              hipMalloc((void**)&s.d_off, 8ull * batch_frames) == hipSuccess &&
              hipMalloc((void**)&s.d_len, 4ull * batch_frames) == hipSuccess &&
-             hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking) == hipSuccess &&
              hipEventCreateWithFlags(&s.done, hipEventDisableTiming) == hipSuccess;
         for (int e = 0; e < 4 && ok && (flags & PNETGPU_RING_STAGE_TIMES); ++e)
             ok = hipEventCreate(&s.stage[e]) == hipSuccess;
@@ -221,6 +230,8 @@ int pnetgpu_ring_create_ex(pnetgpu_ctx* ctx, uint64_t batch_bytes, uint32_t batc
     }
     if (!ok) {
         for (auto& s : r->slots) free_slot(s);
+        for (auto& st : r->streams)
+            if (st) (void)hipStreamDestroy(st);
         delete r;
         return PNETGPU_ENOMEM;
     }
@@ -240,10 +251,11 @@ uint32_t pnetgpu_ring_slots(const pnetgpu_ring* r) { return r ? (uint32_t)r->nsl
 void pnetgpu_ring_destroy(pnetgpu_ring* r) {
     if (!r) return;
     (void)hipSetDevice(r->device);
-    for (auto& s : r->slots) {
-        if (s.stream) (void)hipStreamSynchronize(s.stream);
-        free_slot(s);
-    }
+    for (auto& st : r->streams)
+        if (st) (void)hipStreamSynchronize(st);
+    for (auto& s : r->slots) free_slot(s);
+    for (auto& st : r->streams)
+        if (st) (void)hipStreamDestroy(st);
     delete r;
 }
 
@@ -429,7 +441,7 @@ uint32_t pnetgpu_host_threads(void) { return pnetgpu::host_threads(); }
 // of every record column and the counters, completion event.
 static int ship_slot(pnetgpu_ring* r, Slot& s, const uint8_t* src, uint64_t* id) {
     if (hipSetDevice(r->device) != hipSuccess) return pnetgpu::hip_fail(hipGetLastError());
-    const hipStream_t st = s.stream;
+    const hipStream_t st = r->streams[r->next_id % pnetgpu_ring::kStreams];
     // compact descriptors (6 B/frame over PCIe instead of 12) whenever they can
     // describe the batch; the full ones stay on the host for the waited batch view
     const bool compact = s.bytes <= UINT32_MAX && s.max_len <= UINT16_MAX;
