@@ -29,10 +29,9 @@ sys.path.insert(0, ROOT)
 import bench  # noqa: E402
 
 
-def pipeline(lp, sh, dev, nstreams, depth, desc, seconds):
+def pipeline(lp, sh, dev, nstreams, depth, desc, seconds, chunks=16):
     w = sh.w
     n, stride = sh.n, w.stride
-    chunks = 16
     per = n // chunks
     host = torch.from_numpy(w.buf[: n * stride]).pin_memory()
     streams = [torch.cuda.Stream(dev) for _ in range(nstreams)]
@@ -87,16 +86,21 @@ def main():
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--seconds", type=float, default=2.0)
     ap.add_argument("--cases", default="", help="comma list (default: all)")
+    ap.add_argument("--frames", type=int, default=1 << 22, help="batch frames (16 chunks of them)")
     a = ap.parse_args()
     lp = bench.load_library()
     dev = torch.device("cuda", 0)
-    sh = bench.Shard("udp64", 1 << 22, 1000, dev)
+    sh = bench.Shard("udp64", a.frames, 1000, dev)
+    mib = sh.n * 64 // 16 >> 20                     # chunk MiB at 16 chunks
     cases = {
         "pcie2": lambda: pipeline(lp, sh, dev, 2, 0, False, a.seconds),
         "pcie4": lambda: pipeline(lp, sh, dev, 4, 0, False, a.seconds),
         "depth2": lambda: pipeline(lp, sh, dev, 2, 2, False, a.seconds),
         "depth2d": lambda: pipeline(lp, sh, dev, 2, 2, True, a.seconds),
         "depth3d": lambda: pipeline(lp, sh, dev, 3, 3, True, a.seconds),
+        "depth2_x4": lambda: pipeline(lp, sh, dev, 2, 2, False, a.seconds, chunks=64),   # chunks a quarter the size
+        "pcie2_x4": lambda: pipeline(lp, sh, dev, 2, 0, False, a.seconds, chunks=64),
+        "bench_e2e": lambda: bench.e2e_rate(sh, dev, seconds=a.seconds)["link_gb_s"],
         "ring": lambda: bench.e2e_ring_rate(sh, seconds=a.seconds, stage_times=False)["link_gb_s"],
         "ring_timed": lambda: bench.e2e_ring_rate(sh, seconds=a.seconds)["link_gb_s"],
         "zero_copy": lambda: bench.e2e_zero_copy_rate(sh, seconds=a.seconds, stage_times=False)["link_gb_s"],
@@ -108,7 +112,7 @@ def main():
         order = list(cases) if r % 2 == 0 else list(reversed(cases))
         for k in order:
             out[k].append(cases[k]())
-            print(json.dumps({"round": r, "case": k, "link_gb_s": out[k][-1]}), flush=True)
+            print(json.dumps({"round": r, "case": k, "link_gb_s": out[k][-1], "chunk_mib": mib}), flush=True)
     print(json.dumps({"summary": out}), flush=True)
 
 
