@@ -293,10 +293,10 @@ int pnetgpu_ring_push(pnetgpu_ring* r, const uint8_t* frame, uint32_t len) {
 // frames below it evenly (1500-B frames fill a 64-MiB slot within the first of
 // 16 chunks of a 2^20-frame push); the last pass writes every chunk's
 // descriptors and copies its frames at its prefix offset (runs of frames
-// adjacent in the source in one non-temporal copy).
-// a pack of fewer than 2^16 frames still copies in parallel from this many bytes
+// adjacent in the source in one non-temporal copy). A pack of fewer than 2^16
+// frames finds its cut serially and still copies in parallel from
+// kParallelCopyMin bytes on.
 constexpr uint64_t kParallelCopyMin = 4ull << 20;
-
 static uint64_t pack_frames(const uint8_t* buf, const uint64_t* offsets, const uint32_t* lengths, uint64_t m,
                             uint64_t room_b, uint8_t* dst, uint64_t at, uint64_t* off64, uint32_t* len32,
                             uint32_t* off32, uint16_t* len16, PackStats* st) {
