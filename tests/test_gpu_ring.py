@@ -264,6 +264,9 @@ def test_ring_jumbo_batches_and_stage_stats(producer):
         feed = ring.feed_region if producer == "zero_copy" else ring.feed_many
         out = sorted(list(feed(w.buf, offs, lens)) + list(ring.drain()), key=lambda b: b.id)
         st = ring.stats()
+        ring.reset_stats()
+        z = ring.stats()
+        assert z["host_threads"] == st["host_threads"] and z["batches"] == z["push_ns"] == 0 and z["h2d_ms"] == 0
     finally:
         ring.close()
         if reg:

@@ -121,3 +121,21 @@ def test_pool_env_override():
     cpus = set(sorted(os.sched_getaffinity(0))[:1])
     r = _child(cpus, {"PNETGPU_HOST_THREADS": "3"})
     assert r["threads"] == 3 and r["new1"] <= 2 and r["new2"] == 0 and r["ok"]
+
+
+def test_ring_stats_and_pack_argument_checks():
+    """The ring statistics entry points and the pack reject NULL handles and
+    arrays before touching anything (no GPU involved)."""
+    import ctypes
+    import libpnet_amd as lp
+    from libpnet_amd import ring
+    st = ring.RingStats()
+    einval = lp.DEFS["PNETGPU_EINVAL"]
+    assert lp.lib.pnetgpu_ring_stats_get(None, ctypes.byref(st)) == einval
+    assert lp.lib.pnetgpu_ring_stats_reset(None) == einval
+    k, b = ctypes.c_uint64(), ctypes.c_uint64()
+    assert lp.lib.pnetgpu_batch_pack(None, None, None, 4, None, 0, None, None, ctypes.byref(k), ctypes.byref(b)) \
+        == einval
+    assert lp.lib.pnetgpu_batch_pack(None, None, None, 0, None, 0, None, None, ctypes.byref(k), ctypes.byref(b)) == 0
+    assert k.value == 0 and b.value == 0
+    assert ctypes.sizeof(ring.RingStats) == 96
