@@ -16,6 +16,28 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
+def cpu_stat():
+    """The cgroup's CPU accounting (v2 cpu.stat, else v1): usage and throttling."""
+    for path in ("/sys/fs/cgroup/cpu.stat", "/sys/fs/cgroup/cpu/cpu.stat", "/sys/fs/cgroup/cpu,cpuacct/cpu.stat"):
+        try:
+            with open(path) as fh:
+                return {k: int(v) for k, v in (ln.split() for ln in fh if len(ln.split()) == 2)}
+        except (OSError, ValueError):
+            continue
+    return {}
+
+
+def timed(fn):
+    """fn() with the cgroup's CPU usage and throttling over its run."""
+    a = cpu_stat()
+    out = fn()
+    b = cpu_stat()
+    if isinstance(out, dict) and a:
+        out["cgroup"] = {k: b.get(k, 0) - a.get(k, 0) for k in ("usage_usec", "nr_periods", "nr_throttled",
+                                                               "throttled_usec", "throttled_time") if k in a}
+    return out
+
+
 def child(args):
     import torch
     import bench
@@ -25,10 +47,10 @@ def child(args):
     sh = bench.Shard(args.workload, n, 1000, dev)
     out = {"workload": args.workload, "host_threads": lp.host_threads(),
            "env": os.environ.get("PNETGPU_HOST_THREADS")}
-    out["pack_only"] = bench.pack_rate(sh)
-    out["e2e_pcie"] = bench.e2e_rate(sh, dev)
-    out["e2e_zero_copy"] = bench.e2e_zero_copy_rate(sh, seconds=args.seconds)
-    out["e2e_ring"] = bench.e2e_ring_rate(sh, seconds=args.seconds)
+    out["pack_only"] = timed(lambda: bench.pack_rate(sh))
+    out["e2e_pcie"] = timed(lambda: bench.e2e_rate(sh, dev))
+    out["e2e_zero_copy"] = timed(lambda: bench.e2e_zero_copy_rate(sh, seconds=args.seconds))
+    out["e2e_ring"] = timed(lambda: bench.e2e_ring_rate(sh, seconds=args.seconds))
     for v in out.values():
         if isinstance(v, dict):
             v.pop("note", None)
