@@ -29,7 +29,7 @@ sys.path.insert(0, ROOT)
 import bench  # noqa: E402
 
 
-def pipeline(lp, sh, dev, nstreams, depth, desc, seconds, chunks=16):
+def pipeline(lp, sh, dev, nstreams, depth, desc, seconds, chunks=16, stagger=False):
     w = sh.w
     n, stride = sh.n, w.stride
     per = n // chunks
@@ -46,6 +46,7 @@ def pipeline(lp, sh, dev, nstreams, depth, desc, seconds, chunks=16):
         d_off = [torch.empty(per, dtype=torch.int32, device=dev) for _ in range(nb)]
         d_len = [torch.empty(per, dtype=torch.int16, device=dev) for _ in range(nb)]
     done = [None] * nb
+    up = [None] * nb
 
     def chunk(i):
         j = i % nb
@@ -55,6 +56,9 @@ def pipeline(lp, sh, dev, nstreams, depth, desc, seconds, chunks=16):
         k = i % chunks
         with torch.cuda.stream(s):
             dbuf[j][: per * stride].copy_(host[k * per * stride:(k + 1) * per * stride], non_blocking=True)
+            u = torch.cuda.Event()
+            u.record(s)
+            up[j] = u
             if desc:
                 d_off[j].copy_(h_off, non_blocking=True)
                 d_len[j].copy_(h_len, non_blocking=True)
@@ -71,6 +75,10 @@ def pipeline(lp, sh, dev, nstreams, depth, desc, seconds, chunks=16):
         chunk(i)
     torch.cuda.synchronize()
     i, t0 = 0, time.perf_counter()
+    if stagger:                                     # the second stream starts one upload behind the first
+        chunk(i)
+        up[i % nb].synchronize()
+        i += 1
     while time.perf_counter() - t0 < seconds:
         for _ in range(chunks):
             chunk(i)
@@ -98,6 +106,7 @@ def main():
         "depth2": lambda: pipeline(lp, sh, dev, 2, 2, False, a.seconds),
         "depth2d": lambda: pipeline(lp, sh, dev, 2, 2, True, a.seconds),
         "depth3d": lambda: pipeline(lp, sh, dev, 3, 3, True, a.seconds),
+        "depth2_stagger": lambda: pipeline(lp, sh, dev, 2, 2, False, a.seconds, stagger=True),
         "depth2_x4": lambda: pipeline(lp, sh, dev, 2, 2, False, a.seconds, chunks=64),   # chunks a quarter the size
         "pcie2_x4": lambda: pipeline(lp, sh, dev, 2, 0, False, a.seconds, chunks=64),
         "bench_e2e": lambda: bench.e2e_rate(sh, dev, seconds=a.seconds)["link_gb_s"],
