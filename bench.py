@@ -297,10 +297,13 @@ VERIFY_COLUMNS = ("status", "ip_csum", "l4_csum")
 def e2e_rate(sh, device, chunks=16, reps=3, columns=None, verify=None, seconds=1.5):
     """PCIe-inclusive rate: pinned host frames -> H2D -> kernel -> D2H of the results,
     double-buffered on two streams, paced as a producer is: a buffer pair is
-    reused once its previous chunk is back (at most two chunks in flight; the
-    two streams then stay out of phase, one's H2D beside the other's D2H, which
-    moved 77-79 GB/s of link traffic where enqueueing every chunk up front moved
-    53-57 on the same box: tools/ring_factor_probe.py). Fixed-stride batches ship the frames only;
+    reused once its previous chunk is back (at most two chunks in flight), and
+    the second stream starts one upload behind the first. Paced and staggered,
+    one stream's H2D runs beside the other's kernel and D2H: 77.5-79.5 GB/s of
+    link traffic on every run, where the same pipeline started with both
+    streams uploading at once kept that lockstep phase on some runs (57-78), and
+    enqueueing every chunk up front moved 53-57 (tools/ring_factor_probe.py,
+    profiles/r06/e2e/). Fixed-stride batches ship the frames only;
     descriptor batches (IMIX) ship each chunk's frame span plus its compact
     descriptors (u32 offset rebased to the chunk + u16 length, 6 B/frame) with
     the size hint the ring would give. Reported beside `value`, never as `value`.
@@ -345,6 +348,7 @@ def e2e_rate(sh, device, chunks=16, reps=3, columns=None, verify=None, seconds=1
     ev = {}
 
     done = [None, None]
+    up = [None, None]
 
     def chunk(k, timed):
         s, j = streams[k % 2], k % 2
@@ -356,6 +360,8 @@ def e2e_rate(sh, device, chunks=16, reps=3, columns=None, verify=None, seconds=1
                 marks = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
                 marks[0].record(s)
             dbuf[j][: e - b].copy_(host[b:e], non_blocking=True)
+            up[j] = torch.cuda.Event()
+            up[j].record(s)
             if desc is None:
                 if timed:
                     marks[1].record(s)
@@ -390,9 +396,11 @@ def e2e_rate(sh, device, chunks=16, reps=3, columns=None, verify=None, seconds=1
     torch.cuda.synchronize()
     reps = max(reps, int(seconds / max(time.perf_counter() - t1, 1e-4)))
     t0 = time.perf_counter()
-    for _ in range(reps):
+    for r in range(reps):
         for k in range(chunks):
             chunk(k, True)
+            if r == 0 and k == 0:
+                up[0].synchronize()          # stagger: stream 1 starts once stream 0's first upload is done
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     if verify:
@@ -413,7 +421,7 @@ def e2e_rate(sh, device, chunks=16, reps=3, columns=None, verify=None, seconds=1
                        "host_threads": 1},
             "note": "pinned host batch -> hipMemcpyAsync H2D -> rx kernel -> one D2H of the packed record "
                     f"columns ({rb} B/frame: {', '.join(columns)}), {chunks} chunks double-buffered on 2 streams, "
-                    "at most 2 in flight"
+                    "at most 2 in flight, the second stream started one upload behind the first"
                     + ("" if desc is None else "; descriptor batch: each chunk's frame span + compact descriptors "
                                                "(6 B/frame) up, with the size hint pnetgpu_desc_size_hint gives")}
 

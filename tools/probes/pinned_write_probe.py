@@ -100,6 +100,63 @@ def main():
         out.setdefault("dma_during_pack", []).append(round(nb / (e0.elapsed_time(e1) / 1e3) / 1e9, 1))
         print(json.dumps({"round": r, **{k: out[k][-1] for k in ("dma_alone", "pack_during_dma",
                                                                   "dma_during_pack")}}), flush=True)
+    # The ring's shape rebuilt from parts: pack into 4 rotating pinned slots
+    # (64 MiB each), each shipped H2D on alternating streams once full, a slot
+    # reused after its copy is done; `ship` off packs the same rotation alone.
+    slots = [hip_host_malloc(64 << 20, 0) for _ in range(4)]
+    sdesc = [(hip_host_malloc(8 * n, 0).view(np.uint64), hip_host_malloc(4 * n, 0).view(np.uint32))
+             for _ in range(4)]
+    dslot = [torch.empty(64 << 20, dtype=torch.uint8, device=dev) for _ in range(2)]
+    streams = [torch.cuda.Stream(dev) for _ in range(2)]
+    tslot = [torch.from_numpy(x) for x in slots]
+    for r in range(a.rounds):
+        for ship in (False, True):
+            done = [None] * 4
+            frames = i = j = 0
+            inside = 0.0
+            t_start = time.perf_counter()
+            while time.perf_counter() - t_start < a.seconds:
+                q = j % 4
+                if done[q] is not None:
+                    done[q].synchronize()
+                t0 = time.perf_counter()
+                k, _ = lp.batch_pack(w.buf, offs[i:i + n], lens[i:i + n], slots[q], *sdesc[q], check_bounds=False)
+                inside += time.perf_counter() - t0
+                if ship:
+                    s = streams[j % 2]
+                    with torch.cuda.stream(s):
+                        dslot[j % 2].copy_(tslot[q], non_blocking=True)
+                        e = torch.cuda.Event()
+                        e.record(s)
+                        done[q] = e
+                frames += k
+                i = (i + k) % (4 * n)
+                j += 1
+            torch.cuda.synchronize()
+            el = time.perf_counter() - t_start
+            key = "ring_shape_" + ("shipped" if ship else "pack_only")
+            out.setdefault(key, []).append({"push_gb_s": round(frames * 64 / inside / 1e9, 1),
+                                            "wall_gb_s": round(frames * 64 / el / 1e9, 1)})
+            print(json.dumps({"round": r, "case": key, **out[key][-1]}), flush=True)
+
+    # The same pack after the pool sat idle (the ring's push follows a wait on
+    # the oldest batch): only the time inside batch_pack is counted.
+    for r in range(a.rounds):
+        for idle_us in (0, 100, 500, 2000):
+            frames = i = 0
+            inside = 0.0
+            t_end = time.perf_counter() + a.seconds
+            while time.perf_counter() < t_end:
+                if idle_us:
+                    time.sleep(idle_us / 1e6)
+                t0 = time.perf_counter()
+                k, _ = lp.batch_pack(w.buf, offs[i:i + n], lens[i:i + n], dst, do, dl, check_bounds=False)
+                inside += time.perf_counter() - t0
+                frames += k
+                i = (i + k) % (4 * n)
+            key = f"pack_after_idle_{idle_us}us"
+            out.setdefault(key, []).append(round(frames * 64 / inside / 1e9, 1))
+            print(json.dumps({"round": r, "case": key, "gb_s": out[key][-1]}), flush=True)
     print(json.dumps({"summary": out, "host_threads": lp.host_threads()}), flush=True)
 
 
