@@ -901,7 +901,7 @@ def launch_check(args, world, rank):
     ok = int(ctr[0]) == n and int(ctr[1]) == int(lengths.sum()) and int(ctr[2]) == world * (world - 1) // 2
     if rank == 0:
         coll = ({"backend": str(torch.distributed.get_backend()), "world_size": torch.distributed.get_world_size()}
-                if torch.distributed.is_initialized() else None)
+                if torch.distributed.is_initialized() else {"backend": None, "world_size": 1})
         print(json.dumps({"metric": METRIC, "launch_check": True, "n_gpus": world, "world_size": world,
                           "collective": coll,
                           "frames": int(ctr[0]), "bytes": int(ctr[1]), "wall_s": wall, "counters_ok": ok,
@@ -957,7 +957,7 @@ def main():
         torch.distributed.init_process_group(backend, timeout=datetime.timedelta(minutes=10))
         assert torch.distributed.get_world_size() == world
 
-    collective = None
+    collective = {"backend": None, "world_size": 1, "library": None}     # one process: no collective runs
     if dist_on:
         collective = {"backend": str(torch.distributed.get_backend()),
                       "world_size": torch.distributed.get_world_size(),

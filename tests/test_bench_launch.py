@@ -36,7 +36,7 @@ def test_bench_gpus_n_starts_n_ranks(n):
     assert line["n_gpus"] == n and line["world_size"] == n
     # the line names the collective backend and the world size its process group reported
     if n == 1:
-        assert line["collective"] is None
+        assert line["collective"] == {"backend": None, "world_size": 1}       # one process: none ran
     else:
         assert line["collective"] == {"backend": "gloo", "world_size": n}
     assert line["counters_ok"] is True
