@@ -426,11 +426,12 @@ def e2e_rate(sh, device, chunks=16, reps=3, columns=None, verify=None, seconds=1
                                                "(6 B/frame) up, with the size hint pnetgpu_desc_size_hint gives")}
 
 
-def _ring_link(frames, nbytes, el, rb, nbatches):
-    # up: the frames plus their descriptors (compact, 6 B, for these batches:
-    # ring.cpp ships them whenever a batch qualifies); down: the record
-    # columns plus 64 B of counters per batch
-    return _link(frames, el, nbytes / frames + 6, rb + 64 * nbatches / frames)
+def _ring_link(frames, nbytes, el, rb, nbatches, desc_bytes):
+    # up: the frames plus the descriptors the ring shipped (none for batches of
+    # uniform frames, which go as fixed-stride batches; compact, 6 B a frame,
+    # otherwise: pnetgpu_ring_stats.desc_bytes); down: the record columns plus
+    # 64 B of counters per batch
+    return _link(frames, el, (nbytes + desc_bytes) / frames, rb + 64 * nbatches / frames)
 
 
 def _ring_stages(ring, el):
@@ -443,7 +444,7 @@ def _ring_stages(ring, el):
            "other_host_s": round(el - sum(host.values()), 4),
            "h2d_s": round(st["h2d_ms"] / 1e3, 4), "kernel_s": round(st["kernel_ms"] / 1e3, 4),
            "d2h_s": round(st["d2h_ms"] / 1e3, 4), "batches": st["batches"], "timed_batches": st["timed_batches"],
-           "host_threads": st["host_threads"]}
+           "stride_batches": st["stride_batches"], "desc_bytes": st["desc_bytes"], "host_threads": st["host_threads"]}
     if st["push_ns"]:
         out["push_gb_s"] = round(st["bytes"] / (st["push_ns"] / 1e9) / 1e9, 2)
     if st["h2d_ms"]:
@@ -502,11 +503,13 @@ def e2e_ring_rate(sh, seconds=3.0, columns=None, slots=None, stage_times=True):
     ring.close()
     rb = lp.engine.column_bytes(columns)
     return {"mpkts_s": round(frames / el / 1e6, 1), "gb_s": round(nbytes / el / 1e9, 2),
-            **_ring_link(frames, nbytes, el, rb, nb), "stages": stages,
+            **_ring_link(frames, nbytes, el, rb, nb, stages["desc_bytes"]), "stages": stages,
             "note": "host frames pushed into the pinned ring with pnetgpu_ring_push_many (descriptors and "
                     f"non-temporal frame copies on a persistent pool of {stages['host_threads']} host threads), "
                     f"async H2D -> rx kernel -> D2H of the record columns ({rb} B/frame: {', '.join(columns)}), "
-                    f"{nslots} rotating slots of 64 MiB / 1 Mi frames on 2 alternating streams",
+                    f"{nslots} rotating slots of 64 MiB / 1 Mi frames on 2 alternating streams; batches of "
+                    "uniform frames at a constant stride ship as fixed-stride batches, without descriptors "
+                    "(stages.stride_batches)",
             "slots": nslots}
 
 
@@ -545,10 +548,12 @@ def e2e_zero_copy_rate(sh, seconds=3.0, columns=None, slots=None, stage_times=Tr
         reg.close()
     rb = lp.engine.column_bytes(columns)
     return {"mpkts_s": round(frames / el / 1e6, 1), "gb_s": round(nbytes / el / 1e9, 2),
-            **_ring_link(frames, nbytes, el, rb, nb), "stages": stages,
+            **_ring_link(frames, nbytes, el, rb, nb, stages["desc_bytes"]), "stages": stages,
             "note": "frames DMA'd straight from a registered host buffer (pnetgpu_ring_submit_region, no copy into "
                     f"the ring), rx kernel, D2H of the record columns ({rb} B/frame: {', '.join(columns)}; "
-                    f"pnetgpu_ring_set_columns), {nslots} rotating slots of 64 MiB / 1 Mi frames on 2 alternating streams",
+                    f"pnetgpu_ring_set_columns), {nslots} rotating slots of 64 MiB / 1 Mi frames on 2 alternating streams; "
+                    "batches of uniform frames at a constant stride ship as fixed-stride batches, without descriptors "
+                    "(stages.stride_batches)",
             "slots": nslots}
 
 

@@ -15,6 +15,14 @@
  * rest in flight on alternating streams), so the H2D of one batch overlaps the
  * kernel and D2H of the previous ones and the application's host work.
  *
+ * A batch whose frames all have one length at one constant stride (a capture
+ * of fixed-size frames, TPACKET frame slots) ships as a fixed-stride batch with
+ * no descriptors, wherever the fixed-stride kernel is the one its size hint
+ * would pick: frames of <= 64 B on a stride that is a multiple of 16 with no
+ * parse extensions (the small kernel), or of >= 768 B (the MTU / jumbo
+ * shapes). Any other batch ships compact (u32 / u16) or full descriptors. The
+ * records are identical either way; pnetgpu_ring_stats counts which.
+ *
  * Validity: a waited batch (its frames and records) stays valid until the next
  * pnetgpu_ring_wait() or pnetgpu_ring_release() on the same ring.
  * Single-threaded use per ring.
@@ -82,11 +90,13 @@ typedef struct pnetgpu_ring_stats {
     uint64_t submit_ns;       /* inside submit / submit_region: enqueueing H2D, kernel, D2H   */
     uint64_t wait_ns;         /* inside pnetgpu_ring_wait, blocked on the oldest batch        */
     uint64_t timed_batches;   /* batches whose device stages were timed                       */
+    uint64_t desc_bytes;      /* descriptor bytes shipped host -> device (none for stride batches) */
     double   h2d_ms;          /* PNETGPU_RING_STAGE_TIMES only: H2D of frames + descriptors   */
     double   kernel_ms;       /*   the receive kernel                                         */
     double   d2h_ms;          /*   D2H of counters + record columns                           */
     uint32_t host_threads;    /* threads push_many's passes use (pnetgpu_host_threads)        */
-    uint32_t reserved;
+    uint32_t stride_batches;  /* batches shipped as fixed-stride batches: uniform frames at a
+                               * constant stride, no descriptors (pnetgpu_ring_submit)       */
 } pnetgpu_ring_stats;
 int pnetgpu_ring_stats_get(const pnetgpu_ring* ring, pnetgpu_ring_stats* out);
 /* Zero every sum (host_threads is kept). */
@@ -118,7 +128,8 @@ int pnetgpu_ring_push(pnetgpu_ring* ring, const uint8_t* frame, uint32_t len);
  * the same frames in the same order as n single pushes would. */
 int pnetgpu_ring_push_many(pnetgpu_ring* ring, const uint8_t* buf, const uint64_t* offsets,
                            const uint32_t* lengths, uint64_t n, uint64_t* pushed);
-/* Ship the filling batch (no-op returning 0 with *id = UINT64_MAX if empty). */
+/* Ship the filling batch (no-op returning 0 with *id = UINT64_MAX if empty);
+ * pushed frames sit back to back, so uniform ones ship fixed-stride. */
 int pnetgpu_ring_submit(pnetgpu_ring* ring, uint64_t* id);
 /* Zero-copy submit: ship frames base[offsets[i], +lengths[i]) straight from the
  * caller's memory (one H2D of their span; no copy into the ring's pinned batch).

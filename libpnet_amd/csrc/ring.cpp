@@ -42,8 +42,9 @@ uint64_t now_ns() {
 // what one pack pass took: frames, bytes, and the size-hint statistics
 struct PackStats {
     uint64_t frames = 0, bytes = 0;
-    uint32_t max_len = 0;
+    uint32_t max_len = 0, min_len = UINT32_MAX;
     uint64_t n_large = 0, jumbo_bytes = 0;
+    bool irregular = false;                  // submit_region: a frame off the batch's constant stride
 };
 
 struct Slot {
@@ -54,7 +55,10 @@ struct Slot {
     // alongside; shipped instead when the batch is < 4 GiB and every frame < 64 KiB
     uint32_t* h_off32 = nullptr;
     uint16_t* h_len16 = nullptr;
-    uint32_t max_len = 0;
+    uint32_t max_len = 0, min_len = UINT32_MAX;
+    // > 0: every frame is max_len bytes at this constant stride from the first,
+    // so the batch can ship as a fixed-stride batch without descriptors
+    uint32_t stride = 0;
     // size statistics of the batch for its PNETGPU_DESC_HINT_* (desc_size_hint)
     uint64_t n_large = 0, jumbo_bytes = 0;
     uint64_t frame_bytes = 0;               // sum of the frame lengths (bytes counts gaps in a region)
@@ -178,6 +182,8 @@ static int take_free_slot(pnetgpu_ring* r) {
             r->slots[i].n = 0;
             r->slots[i].bytes = 0;
             r->slots[i].max_len = 0;
+            r->slots[i].min_len = UINT32_MAX;
+            r->slots[i].stride = 0;
             r->slots[i].n_large = 0;
             r->slots[i].jumbo_bytes = 0;
             r->slots[i].frame_bytes = 0;
@@ -270,6 +276,7 @@ int pnetgpu_ring_push(pnetgpu_ring* r, const uint8_t* frame, uint32_t len) {
     s.h_off32[s.n] = (uint32_t)s.bytes;
     s.h_len16[s.n] = (uint16_t)len;
     s.max_len = std::max(s.max_len, len);
+    s.min_len = std::min(s.min_len, len);
     s.n_large += len >= pnetgpu::kHintLargeMin;
     s.jumbo_bytes += len >= pnetgpu::kHintJumboMin ? len : 0;
     s.bytes += len;
@@ -322,6 +329,7 @@ static uint64_t pack_frames(const uint8_t* buf, const uint64_t* offsets, const u
             if (off32) _mm_stream_si32(reinterpret_cast<int*>(off32 + i), (int)(uint32_t)o);
             if (len16) len16[i] = (uint16_t)len;
             cs.max_len = std::max(cs.max_len, len);
+            cs.min_len = std::min(cs.min_len, len);
             cs.n_large += len >= pnetgpu::kHintLargeMin;
             cs.jumbo_bytes += len >= pnetgpu::kHintJumboMin ? len : 0;
             o += len;
@@ -386,6 +394,7 @@ static uint64_t pack_frames(const uint8_t* buf, const uint64_t* offsets, const u
     });
     for (unsigned u = 0; u < nt; ++u) {
         st->max_len = std::max(st->max_len, cst[u].max_len);
+        st->min_len = std::min(st->min_len, cst[u].min_len);
         st->n_large += cst[u].n_large;
         st->jumbo_bytes += cst[u].jumbo_bytes;
     }
@@ -409,6 +418,7 @@ int pnetgpu_ring_push_many(pnetgpu_ring* r, const uint8_t* buf, const uint64_t* 
     r->stats.push_ns += now_ns() - t0;
     if (k == 0) return PNETGPU_EFULL;
     s.max_len = std::max(s.max_len, st.max_len);
+    s.min_len = std::min(s.min_len, st.min_len);
     s.n_large += st.n_large;
     s.jumbo_bytes += st.jumbo_bytes;
     s.n += k;
@@ -445,15 +455,27 @@ static int ship_slot(pnetgpu_ring* r, Slot& s, const uint8_t* src, uint64_t* id)
     // compact descriptors (6 B/frame over PCIe instead of 12) whenever they can
     // describe the batch; the full ones stay on the host for the waited batch view
     const bool compact = s.bytes <= UINT32_MAX && s.max_len <= UINT16_MAX;
+    // Uniform frames at a constant stride ship as a fixed-stride batch, with no
+    // descriptors on the link (6 of the 70 B a 64-B frame costs), wherever the
+    // fixed-stride kernel is the one the descriptor batch's size hint would
+    // reach anyway: frames of <= 64 B on a 16-B multiple stride without parse
+    // extensions (the small kernel), or of >= kHintLargeMin B (MTU / jumbo
+    // shape by the same 4096-B line). The records are the same either way.
+    constexpr uint32_t kRxFlags = PNETGPU_RX_VLAN | PNETGPU_RX_IPV6_EXT | PNETGPU_RX_L3;
+    const bool strided = s.stride > 0 && s.stride >= s.max_len &&
+                         ((s.max_len <= 64 && s.stride % 16 == 0 && !(r->flags & kRxFlags)) ||
+                          s.max_len >= pnetgpu::kHintLargeMin);
     const void* h_off = compact ? (const void*)s.h_off32 : (const void*)s.h_off;
     const void* h_len = compact ? (const void*)s.h_len16 : (const void*)s.h_len;
     s.timed = (r->flags & PNETGPU_RING_STAGE_TIMES) != 0;
     if (s.timed && hipEventRecord(s.stage[0], st) != hipSuccess) return pnetgpu::hip_fail(hipGetLastError());
     // granule rule: the tail past the last frame is readable (32 zero bytes)
+    const uint64_t desc_bytes = strided ? 0 : (compact ? 6ull : 12ull) * s.n;
     if (hipMemcpyAsync(s.d_frames, src, s.bytes, hipMemcpyHostToDevice, st) != hipSuccess ||
         (src != s.h_frames && hipMemsetAsync(s.d_frames + s.bytes, 0, 32, st) != hipSuccess) ||
-        hipMemcpyAsync(s.d_off, h_off, (compact ? 4ull : 8ull) * s.n, hipMemcpyHostToDevice, st) != hipSuccess ||
-        hipMemcpyAsync(s.d_len, h_len, (compact ? 2ull : 4ull) * s.n, hipMemcpyHostToDevice, st) != hipSuccess ||
+        (!strided &&
+         (hipMemcpyAsync(s.d_off, h_off, (compact ? 4ull : 8ull) * s.n, hipMemcpyHostToDevice, st) != hipSuccess ||
+          hipMemcpyAsync(s.d_len, h_len, (compact ? 2ull : 4ull) * s.n, hipMemcpyHostToDevice, st) != hipSuccess)) ||
         hipMemsetAsync(s.d_rec, 0, 8ull * PNETGPU_NCOUNTERS, st) != hipSuccess ||
         (s.timed && hipEventRecord(s.stage[1], st) != hipSuccess))
         return pnetgpu::hip_fail(hipGetLastError());
@@ -461,12 +483,18 @@ static int ship_slot(pnetgpu_ring* r, Slot& s, const uint8_t* src, uint64_t* id)
     b.data = s.d_frames;
     b.data_bytes = s.bytes;
     b.n_frames = s.n;
-    b.offsets = s.d_off;
-    b.lengths = s.d_len;
-    // the batch's size mix picks the kernel's tail shape (frames of >= 768 B:
-    // MTU; mostly jumbo bytes: jumbo; else mixed); records are the same
-    b.flags = (r->flags & ~PNETGPU_RING_STAGE_TIMES) | (compact ? PNETGPU_DESC_COMPACT : 0u) |
-              pnetgpu::desc_size_hint(s.n, s.frame_bytes, s.n_large, s.jumbo_bytes);
+    if (strided) {
+        b.stride = s.stride;
+        b.frame_len = s.max_len;
+        b.flags = r->flags & ~PNETGPU_RING_STAGE_TIMES;
+    } else {
+        b.offsets = s.d_off;
+        b.lengths = s.d_len;
+        // the batch's size mix picks the kernel's tail shape (frames of >= 768 B:
+        // MTU; mostly jumbo bytes: jumbo; else mixed); records are the same
+        b.flags = (r->flags & ~PNETGPU_RING_STAGE_TIMES) | (compact ? PNETGPU_DESC_COMPACT : 0u) |
+                  pnetgpu::desc_size_hint(s.n, s.frame_bytes, s.n_large, s.jumbo_bytes);
+    }
     pnetgpu_rx_columns c{};
     uint64_t at = 8ull * PNETGPU_NCOUNTERS;          // the counters lead the record block
     for (int k = 0; k < kNumCols; ++k) {
@@ -488,6 +516,8 @@ static int ship_slot(pnetgpu_ring* r, Slot& s, const uint8_t* src, uint64_t* id)
     r->stats.batches += 1;
     r->stats.frames += s.n;
     r->stats.bytes += s.bytes;
+    r->stats.desc_bytes += desc_bytes;
+    r->stats.stride_batches += strided;
     s.state = kInFlight;
     s.id = r->next_id++;
     if (id) *id = s.id;
@@ -504,6 +534,7 @@ int pnetgpu_ring_submit(pnetgpu_ring* r, uint64_t* id) {
     Slot& s = r->slots[r->filling];
     if (s.n == 0) return PNETGPU_OK;
     s.frames_view = s.h_frames;
+    s.stride = s.n >= 2 && s.min_len == s.max_len ? s.max_len : 0;   // packed back to back
     const uint64_t t0 = now_ns();
     const int rc = ship_slot(r, s, s.h_frames, id);
     r->stats.submit_ns += now_ns() - t0;
@@ -525,7 +556,10 @@ int pnetgpu_ring_submit_region(pnetgpu_ring* r, const uint8_t* base, const uint6
     const uint64_t o0 = offsets[0];
     const uint64_t limit = std::min<uint64_t>(n, r->cap_frames);
     uint64_t k = 0, end = o0, fbytes = 0, large = 0, jumbo = 0;
-    uint32_t mx = 0;
+    uint32_t mx = 0, mn = UINT32_MAX;
+    bool irregular = false;
+    // the stride a fixed-stride batch would have: frame i at o0 + i * S
+    const uint64_t S = limit >= 2 && offsets[1] > o0 ? offsets[1] - o0 : 0;
     auto desc_range = [&](uint64_t lo, uint64_t hi) {   // descriptors + size statistics of [lo, hi)
         PackStats st;
         for (uint64_t i = lo; i < hi; ++i) {
@@ -535,6 +569,8 @@ int pnetgpu_ring_submit_region(pnetgpu_ring* r, const uint8_t* base, const uint6
             s.h_off32[i] = (uint32_t)(offsets[i] - o0);
             s.h_len16[i] = (uint16_t)len;
             st.max_len = std::max(st.max_len, len);
+            st.min_len = std::min(st.min_len, len);
+            st.irregular |= offsets[i] - o0 != i * S;
             st.bytes += len;
             st.n_large += len >= pnetgpu::kHintLargeMin;
             st.jumbo_bytes += len >= pnetgpu::kHintJumboMin ? len : 0;
@@ -577,6 +613,8 @@ int pnetgpu_ring_submit_region(pnetgpu_ring* r, const uint8_t* base, const uint6
                 end = offsets[k - 1] + lengths[k - 1];
                 for (const PackStats& c : cst) {
                     mx = std::max(mx, c.max_len);
+                    mn = std::min(mn, c.min_len);
+                    irregular |= c.irregular;
                     fbytes += c.bytes;
                     large += c.n_large;
                     jumbo += c.jumbo_bytes;
@@ -595,6 +633,8 @@ int pnetgpu_ring_submit_region(pnetgpu_ring* r, const uint8_t* base, const uint6
         }
         const PackStats st = desc_range(0, k);
         mx = st.max_len;
+        mn = st.min_len;
+        irregular = st.irregular;
         fbytes = st.bytes;
         large = st.n_large;
         jumbo = st.jumbo_bytes;
@@ -605,6 +645,8 @@ int pnetgpu_ring_submit_region(pnetgpu_ring* r, const uint8_t* base, const uint6
     s.bytes = end - o0;                          // the span shipped (gaps included)
     s.frame_bytes = fbytes;
     s.max_len = mx;
+    s.min_len = mn;
+    s.stride = k >= 2 && !irregular && mn == mx && S <= UINT32_MAX ? (uint32_t)S : 0;
     s.n_large = large;
     s.jumbo_bytes = jumbo;
     s.frames_view = base + o0;
@@ -614,7 +656,8 @@ int pnetgpu_ring_submit_region(pnetgpu_ring* r, const uint8_t* base, const uint6
     if (rc) {   // nothing shipped: the slot is empty again (its pinned batch never held these frames)
         s.n = 0;
         s.bytes = s.frame_bytes = s.n_large = s.jumbo_bytes = 0;
-        s.max_len = 0;
+        s.max_len = s.stride = 0;
+        s.min_len = UINT32_MAX;
         return rc;
     }
     *taken = k;

@@ -28,11 +28,12 @@ class RingStats(ctypes.Structure):
     """pnetgpu_ring_stats (include/pnetgpu_ring.h)."""
     _fields_ = [("batches", ctypes.c_uint64), ("frames", ctypes.c_uint64), ("bytes", ctypes.c_uint64),
                 ("push_ns", ctypes.c_uint64), ("submit_ns", ctypes.c_uint64), ("wait_ns", ctypes.c_uint64),
-                ("timed_batches", ctypes.c_uint64), ("h2d_ms", ctypes.c_double), ("kernel_ms", ctypes.c_double),
-                ("d2h_ms", ctypes.c_double), ("host_threads", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
+                ("timed_batches", ctypes.c_uint64), ("desc_bytes", ctypes.c_uint64), ("h2d_ms", ctypes.c_double),
+                ("kernel_ms", ctypes.c_double), ("d2h_ms", ctypes.c_double), ("host_threads", ctypes.c_uint32),
+                ("stride_batches", ctypes.c_uint32)]
 
     def as_dict(self):
-        return {name: getattr(self, name) for name, _ in self._fields_ if name != "reserved"}
+        return {name: getattr(self, name) for name, _ in self._fields_}
 
 
 def _setup():

@@ -16,7 +16,7 @@ from tests.test_gpu_parity import SHAPE_RE
 pytestmark = pytest.mark.gpu
 
 
-def check_batches(batches, frames):
+def check_batches(batches, frames, flags=0):
     got = sorted(batches, key=lambda b: b.id)
     assert [b.id for b in got] == list(range(len(got)))
     assert sum(b.n for b in got) == len(frames)
@@ -24,7 +24,7 @@ def check_batches(batches, frames):
     for b in got:
         for k in range(b.n):
             assert bytes(b.frames[b.offsets[k]:b.offsets[k] + b.lengths[k]]) == frames[i + k]
-        rec = coracle.rx_batch(b.frames, b.n, offsets=b.offsets, lengths=b.lengths)
+        rec = coracle.rx_batch(b.frames, b.n, offsets=b.offsets, lengths=b.lengths, flags=flags)
         assert b.records, b.id
         for c, v in b.records.items():
             assert np.array_equal(v, rec[c]), (b.id, c)
@@ -382,3 +382,94 @@ def test_ring_zero_copy_large_region_overlap_rejected():
         # the batches of frames before the overlap that completed before the error
         assert sum(got) <= (at // (1 << 16)) * (1 << 16)
         ring.close()
+
+
+def _uniform_case(case, n=3000):
+    """(frames, buffer, offsets, lengths, flags, whether any batch should ship
+    fixed-stride) for one batch shape."""
+    rng = np.random.default_rng(17)
+
+    def synth(name, m, cut=None):
+        w = lp.synth.make(name, m, seed=5)
+        assert w.stride
+        ln = cut or w.frame_len
+        return [bytes(w.buf[i * w.stride:i * w.stride + ln]) for i in range(m)]
+    gap, flags = 0, 0
+    if case == "64_packed":
+        fr, strided = synth("udp64", n), True
+    elif case == "64_at_128":                  # TPACKET-like fixed frame slots
+        fr, gap, strided = synth("udp64", n), 64, True
+    elif case == "60_packed":                  # stride not a 16-B multiple: descriptors
+        fr, strided = synth("udp64", n, cut=60), False
+    elif case == "200_packed":                 # between the small and MTU kernels: descriptors
+        fr, strided = synth("udp1500", n, cut=200), False
+    elif case == "1500_packed":
+        fr, strided = synth("udp1500", n), True
+    elif case == "9000_packed":
+        fr, strided = synth("udp6_jumbo", 400), True
+    elif case == "64_vlan_flag":               # parse extensions: not the small kernel, descriptors
+        fr, flags, strided = synth("udp64", n), lp.engine.RX_VLAN, False
+    elif case == "64_ragged_gaps":             # uniform lengths, irregular spacing: descriptors
+        fr, gap, strided = synth("udp64", n), None, False
+    else:                                      # one frame a byte short: its batch keeps descriptors
+        fr, strided = synth("udp64", n), None
+        fr[n // 2] = fr[n // 2][:-1]
+    lens = np.array([len(f) for f in fr], np.uint32)
+    step = lens.astype(np.uint64) + (rng.integers(0, 4, len(fr)).astype(np.uint64) * 16 if gap is None
+                                     else np.uint64(gap))
+    offs = np.zeros(len(fr), np.uint64)
+    offs[1:] = np.cumsum(step[:-1], dtype=np.uint64)
+    buf = rng.integers(0, 256, int(offs[-1] + lens[-1]) + 64, dtype=np.uint8)
+    for f, o in zip(fr, offs):
+        buf[int(o):int(o) + len(f)] = np.frombuffer(f, np.uint8)
+    return fr, buf, offs, lens, flags, strided
+
+
+def _ships_strided(b, flags):
+    """The ring's rule (ring.cpp ship_slot), restated from the waited batch."""
+    off = np.asarray(b.offsets[:b.n], np.uint64)
+    ln = np.asarray(b.lengths[:b.n], np.uint32)
+    if b.n < 2 or ln.min() != ln.max():
+        return False
+    stride = int(off[1] - off[0])
+    if not np.array_equal(off - off[0], np.arange(b.n, dtype=np.uint64) * np.uint64(stride)):
+        return False
+    L = int(ln[0])
+    return (L <= 64 and stride % 16 == 0 and flags == 0) or L >= 768
+
+
+@pytest.mark.parametrize("producer", ["push_many", "region"])
+@pytest.mark.parametrize("case", ["64_packed", "64_at_128", "60_packed", "200_packed", "1500_packed", "9000_packed",
+                                  "64_vlan_flag", "64_ragged_gaps", "one_short"])
+def test_ring_uniform_batches_ship_fixed_stride(case, producer):
+    """Batches of uniform frames at a constant stride ship as fixed-stride
+    batches (no descriptors on the link) where the fixed-stride kernel is the
+    one the size hint would reach; every other batch keeps its descriptors. The
+    records equal the oracle's either way. The copying ring packs frames back to
+    back, so its stride is the frame length whatever the source spacing."""
+    fr, buf, offs, lens, flags, strided = _uniform_case(case)
+    if producer == "push_many" and case in ("64_at_128", "64_ragged_gaps"):
+        strided = True                          # packed back to back: stride 64
+    ring = lp.Ring(batch_bytes=1 << 20, batch_frames=1024, flags=flags)
+    reg = lp.HostRegistration(buf) if producer == "region" else None
+    try:
+        feed = ring.feed_many if producer == "push_many" else ring.feed_region
+        out = []
+        for b in feed(buf, offs, lens):
+            out.append((b, _ships_strided(b, flags)))
+        for b in ring.drain():
+            out.append((b, _ships_strided(b, flags)))
+        check_batches([b for b, _ in out], fr, flags=flags)
+        st = ring.stats()
+    finally:
+        ring.close()
+        if reg:
+            reg.close()
+    assert st["batches"] == len(out) >= 2
+    n_strided = sum(s for _, s in out)
+    assert st["stride_batches"] == n_strided
+    assert st["desc_bytes"] == 6 * sum(b.n for b, s in out if not s)
+    if strided is None:
+        assert 0 < n_strided < len(out)
+    else:
+        assert (n_strided == len(out)) if strided else n_strided == 0

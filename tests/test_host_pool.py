@@ -138,4 +138,4 @@ def test_ring_stats_and_pack_argument_checks():
         == einval
     assert lp.lib.pnetgpu_batch_pack(None, None, None, 0, None, 0, None, None, ctypes.byref(k), ctypes.byref(b)) == 0
     assert k.value == 0 and b.value == 0
-    assert ctypes.sizeof(ring.RingStats) == 88       # 7 u64 + 3 f64 + 2 u32 (the C layout: test_boundary_layout)
+    assert ctypes.sizeof(ring.RingStats) == 96       # 8 u64 + 3 f64 + 2 u32 (the C layout: test_boundary_layout)
