@@ -139,3 +139,14 @@ def test_ring_stats_and_pack_argument_checks():
     assert lp.lib.pnetgpu_batch_pack(None, None, None, 0, None, 0, None, None, ctypes.byref(k), ctypes.byref(b)) == 0
     assert k.value == 0 and b.value == 0
     assert ctypes.sizeof(ring.RingStats) == 96       # 8 u64 + 3 f64 + 2 u32 (the C layout: test_boundary_layout)
+
+
+@pytest.mark.skipif(not os.path.exists("/opt/rocm/bin/hipcc"), reason="no toolchain")
+def test_push_compact_descriptors_match_full_ones():
+    """The ring push's compact (u32 / u16) descriptors — the ones it ships — equal
+    its u64 / u32 ones for pushes starting at any slot fill level, serial and
+    parallel, cut or whole (tools/pack_compact_check.cpp, CPU only)."""
+    r = subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "libpnet_amd"), "compact-check"], capture_output=True,
+                       text=True, timeout=600)
+    assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]
+    assert "pack_compact_check: ok" in r.stdout

@@ -52,6 +52,10 @@ def main():
     dsts = {f"ring_slot{k}": v for k, v in enumerate(views)}
     dsts["torch_pinned"] = torch.empty(64 << 20, dtype=torch.uint8).pin_memory().numpy()
     dsts["pageable"] = np.ones(64 << 20, np.uint8)
+    # numpy's large arrays are madvise'd for transparent huge pages; the same
+    # kind of buffer page-locked and mapped for DMA (pnetgpu_host_register)
+    dsts["pageable_registered"] = np.ones(64 << 20, np.uint8)
+    reg = lp.HostRegistration(dsts["pageable_registered"])
     out = {}
     for r in range(a.rounds):
         for k in (list(dsts) if r % 2 == 0 else list(reversed(dsts))):
@@ -69,6 +73,7 @@ def main():
     out["ring_push_gb_s"] = round(st["bytes"] / (st["push_ns"] / 1e9) / 1e9, 1)
     out["ring_wait_s"] = round(st["wait_ns"] / 1e9, 3)
     ring.close()
+    reg.close()
     print(json.dumps({"summary": out, "slots_seen": len(slots)}), flush=True)
 
 
