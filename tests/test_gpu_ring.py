@@ -451,7 +451,6 @@ def test_ring_uniform_batches_ship_fixed_stride(case, producer):
     if producer == "push_many" and case in ("64_at_128", "64_ragged_gaps"):
         strided = True                          # packed back to back: stride 64
     ring = lp.Ring(batch_bytes=1 << 20, batch_frames=1024, flags=flags)
-    reg = lp.HostRegistration(buf) if producer == "region" else None
     try:
         feed = ring.feed_many if producer == "push_many" else ring.feed_region
         out = []
@@ -463,8 +462,6 @@ def test_ring_uniform_batches_ship_fixed_stride(case, producer):
         st = ring.stats()
     finally:
         ring.close()
-        if reg:
-            reg.close()
     assert st["batches"] == len(out) >= 2
     n_strided = sum(s for _, s in out)
     assert st["stride_batches"] == n_strided
