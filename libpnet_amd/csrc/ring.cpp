@@ -45,6 +45,7 @@ struct PackStats {
     uint32_t max_len = 0, min_len = UINT32_MAX;
     uint64_t n_large = 0, jumbo_bytes = 0;
     bool irregular = false;                  // submit_region: a frame off the batch's constant stride
+    bool compact_skipped = false;            // pack_frames left the compact descriptors out
 };
 
 struct Slot {
@@ -59,6 +60,9 @@ struct Slot {
     // > 0: every frame is max_len bytes at this constant stride from the first,
     // so the batch can ship as a fixed-stride batch without descriptors
     uint32_t stride = 0;
+    // the compact descriptors are written for every frame (false: the pushes
+    // left them out while every frame had one length; backfill_compact)
+    bool compact_ok = true;
     // size statistics of the batch for its PNETGPU_DESC_HINT_* (desc_size_hint)
     uint64_t n_large = 0, jumbo_bytes = 0;
     uint64_t frame_bytes = 0;               // sum of the frame lengths (bytes counts gaps in a region)
@@ -184,6 +188,7 @@ static int take_free_slot(pnetgpu_ring* r) {
             r->slots[i].max_len = 0;
             r->slots[i].min_len = UINT32_MAX;
             r->slots[i].stride = 0;
+            r->slots[i].compact_ok = true;
             r->slots[i].n_large = 0;
             r->slots[i].jumbo_bytes = 0;
             r->slots[i].frame_bytes = 0;
@@ -191,6 +196,34 @@ static int take_free_slot(pnetgpu_ring* r) {
         }
     }
     return -1;
+}
+
+// Whether a batch of frames of len bytes at a constant stride ships as a
+// fixed-stride batch: where the fixed-stride kernel is the one the descriptor
+// batch's size hint would reach anyway — frames of <= 64 B on a 16-B multiple
+// stride without parse extensions (the small kernel), or of >= kHintLargeMin B
+// (the MTU / jumbo shapes, split at the same 4096 B).
+static bool ships_strided(uint32_t len, uint32_t stride, uint32_t flags) {
+    constexpr uint32_t kRxFlags = PNETGPU_RX_VLAN | PNETGPU_RX_IPV6_EXT | PNETGPU_RX_L3;
+    return stride > 0 && stride >= len &&
+           ((len <= 64 && stride % 16 == 0 && !(flags & kRxFlags)) || len >= pnetgpu::kHintLargeMin);
+}
+
+// The compact descriptors of a slot whose pushes left them out: every frame so
+// far has the slot's one length, packed back to back.
+static void backfill_compact(Slot& s) {
+    const uint32_t len = s.max_len;
+    const uint64_t n = s.n;
+    auto fill = [&](uint64_t lo, uint64_t hi) {
+        for (uint64_t i = lo; i < hi; ++i) {
+            s.h_off32[i] = (uint32_t)(i * len);
+            s.h_len16[i] = (uint16_t)len;
+        }
+    };
+    const unsigned nt = n >= (1u << 16) ? pnetgpu::host_threads() : 1u;
+    if (nt > 1) pnetgpu::parallel_run(nt, [&](unsigned t) { fill(n * t / nt, n * (t + 1) / nt); });
+    else fill(0, n);
+    s.compact_ok = true;
 }
 
 extern "C" {
@@ -270,6 +303,7 @@ int pnetgpu_ring_push(pnetgpu_ring* r, const uint8_t* frame, uint32_t len) {
     if (r->filling < 0 && (r->filling = take_free_slot(r)) < 0) return PNETGPU_EBUSY;
     Slot& s = r->slots[r->filling];
     if (s.n >= r->cap_frames || len > r->cap_bytes - s.bytes) return PNETGPU_EFULL;
+    if (!s.compact_ok) backfill_compact(s);
     std::memcpy(s.h_frames + s.bytes, frame, len);
     s.h_off[s.n] = s.bytes;
     s.h_len[s.n] = len;
@@ -306,8 +340,11 @@ int pnetgpu_ring_push(pnetgpu_ring* r, const uint8_t* frame, uint32_t len) {
 constexpr uint64_t kParallelCopyMin = 4ull << 20;
 static uint64_t pack_frames(const uint8_t* buf, const uint64_t* offsets, const uint32_t* lengths, uint64_t m,
                             uint64_t room_b, uint8_t* dst, uint64_t at, uint64_t* off64, uint32_t* len32,
-                            uint32_t* off32, uint16_t* len16, PackStats* st) {
+                            uint32_t* off32, uint16_t* len16, PackStats* st, uint32_t skip_len = 0) {
     *st = PackStats{};
+    // skip_len > 0: when every frame of the push is skip_len bytes the compact
+    // descriptors are left out (the batch ships fixed-stride; st->compact_skipped)
+    bool uniform = skip_len > 0 && off32;
     // one pass per chunk: descriptors, size statistics, and the copies of runs
     // of source-adjacent frames, each issued when the run ends
     auto fill_range = [&](uint64_t lo, uint64_t hi, uint64_t o) {
@@ -370,11 +407,21 @@ static uint64_t pack_frames(const uint8_t* buf, const uint64_t* offsets, const u
         // few frames: the cut in one serial scan of the lengths; the copies
         // still go parallel when they are large (7,456 jumbo frames fill a
         // 64-MiB slot, one thread's copy of which trails the link)
-        while (k < m && lengths[k] <= room_b - bytes) bytes += lengths[k++];
+        while (k < m && lengths[k] <= room_b - bytes) {
+            uniform = uniform && lengths[k] == skip_len;
+            bytes += lengths[k++];
+        }
         if (k == 0) return 0;
+        if (uniform) {
+            off32 = nullptr;
+            len16 = nullptr;
+            st->compact_skipped = true;
+        }
         nt = bytes >= kParallelCopyMin ? (unsigned)std::min<uint64_t>(threads, (k + 15) / 16) : 1u;
         if (nt <= 1) {
+            const bool skipped = st->compact_skipped;
             *st = fill_range(0, k, at);
+            st->compact_skipped = skipped;
             st->frames = k;
             st->bytes = bytes;
             return k;
@@ -385,11 +432,24 @@ static uint64_t pack_frames(const uint8_t* buf, const uint64_t* offsets, const u
             for (uint64_t i = k * t / nt, hi = k * (t + 1) / nt; i < hi; ++i) csum[t] += lengths[i];
     } else {
         csum.assign(nt, 0);
+        std::vector<uint8_t> mixed(nt, 0);            // a chunk holding a frame other than skip_len
         pnetgpu::parallel_run(nt, [&](unsigned t) {
             uint64_t sum = 0;
-            for (uint64_t i = m * t / nt, hi = m * (t + 1) / nt; i < hi; ++i) sum += lengths[i];
+            uint32_t lo_len = UINT32_MAX, hi_len = 0;
+            for (uint64_t i = m * t / nt, hi = m * (t + 1) / nt; i < hi; ++i) {
+                sum += lengths[i];
+                lo_len = std::min(lo_len, lengths[i]);
+                hi_len = std::max(hi_len, lengths[i]);
+            }
             csum[t] = sum;
+            mixed[t] = hi_len && (lo_len != hi_len || hi_len != skip_len);
         });
+        for (unsigned t = 0; t < nt && uniform; ++t) uniform = !mixed[t];
+        if (uniform) {
+            off32 = nullptr;
+            len16 = nullptr;
+            st->compact_skipped = true;
+        }
         unsigned c = 0;
         while (c < nt && bytes + csum[c] <= room_b) bytes += csum[c++];
         k = m;
@@ -435,10 +495,20 @@ int pnetgpu_ring_push_many(pnetgpu_ring* r, const uint8_t* buf, const uint64_t* 
     if (r->filling < 0 && (r->filling = take_free_slot(r)) < 0) return PNETGPU_EBUSY;
     const uint64_t t0 = now_ns();
     Slot& s = r->slots[r->filling];
+    // While every frame of the slot has one length that ships fixed-stride, the
+    // push leaves the compact descriptors out (they would never cross the link);
+    // the first push that breaks the pattern backfills them for the frames before.
+    const uint32_t slot_len = s.n == 0 ? lengths[0] : s.min_len == s.max_len ? s.max_len : 0;
+    const uint32_t skip_len = slot_len && ships_strided(slot_len, slot_len, r->flags) ? slot_len : 0;
     PackStats st;
     const uint64_t k = pack_frames(buf, offsets, lengths, std::min<uint64_t>(n, r->cap_frames - s.n),
                                    r->cap_bytes - s.bytes, s.h_frames, s.bytes, s.h_off + s.n, s.h_len + s.n,
-                                   s.h_off32 + s.n, s.h_len16 + s.n, &st);
+                                   s.h_off32 + s.n, s.h_len16 + s.n, &st, skip_len);
+    if (k && st.compact_skipped) {
+        s.compact_ok = false;
+    } else if (k && !s.compact_ok) {
+        backfill_compact(s);                     // the frames before this push (s.n not yet advanced)
+    }
     r->stats.push_ns += now_ns() - t0;
     if (k == 0) return PNETGPU_EFULL;
     s.max_len = std::max(s.max_len, st.max_len);
@@ -480,15 +550,10 @@ static int ship_slot(pnetgpu_ring* r, Slot& s, const uint8_t* src, uint64_t* id)
     // describe the batch; the full ones stay on the host for the waited batch view
     const bool compact = s.bytes <= UINT32_MAX && s.max_len <= UINT16_MAX;
     // Uniform frames at a constant stride ship as a fixed-stride batch, with no
-    // descriptors on the link (6 of the 70 B a 64-B frame costs), wherever the
-    // fixed-stride kernel is the one the descriptor batch's size hint would
-    // reach anyway: frames of <= 64 B on a 16-B multiple stride without parse
-    // extensions (the small kernel), or of >= kHintLargeMin B (MTU / jumbo
-    // shape by the same 4096-B line). The records are the same either way.
-    constexpr uint32_t kRxFlags = PNETGPU_RX_VLAN | PNETGPU_RX_IPV6_EXT | PNETGPU_RX_L3;
-    const bool strided = s.stride > 0 && s.stride >= s.max_len &&
-                         ((s.max_len <= 64 && s.stride % 16 == 0 && !(r->flags & kRxFlags)) ||
-                          s.max_len >= pnetgpu::kHintLargeMin);
+    // descriptors on the link (6 of the 70 B a 64-B frame costs), where
+    // ships_strided says so. The records are the same either way.
+    const bool strided = s.stride > 0 && ships_strided(s.max_len, s.stride, r->flags);
+    if (!strided && !s.compact_ok) backfill_compact(s);   // e.g. a single frame
     const void* h_off = compact ? (const void*)s.h_off32 : (const void*)s.h_off;
     const void* h_len = compact ? (const void*)s.h_len16 : (const void*)s.h_len;
     s.timed = (r->flags & PNETGPU_RING_STAGE_TIMES) != 0;

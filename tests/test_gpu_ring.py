@@ -470,3 +470,54 @@ def test_ring_uniform_batches_ship_fixed_stride(case, producer):
         assert 0 < n_strided < len(out)
     else:
         assert (n_strided == len(out)) if strided else n_strided == 0
+
+
+def _push_all(ring, buf, offs, lens):
+    pushed = ctypes.c_uint64()
+    check(lib.pnetgpu_ring_push_many(ring.h, ctypes.c_void_p(buf.ctypes.data), ctypes.c_void_p(offs.ctypes.data),
+                                     ctypes.c_void_p(lens.ctypes.data), len(offs), ctypes.byref(pushed)),
+          "pnetgpu_ring_push_many")
+    assert pushed.value == len(offs)
+
+
+@pytest.mark.parametrize("case", ["uniform_then_mixed", "single_frame", "uniform_then_single_push",
+                                  "uniform_then_other_push", "mtu_then_small_frame"])
+def test_ring_push_backfills_compact_descriptors(case):
+    """While every frame of a slot has one length that ships fixed-stride, the
+    pushes leave the compact descriptors out; a later push or single-frame push
+    that breaks the pattern, or a batch that ships with descriptors after all
+    (one frame), backfills them first. Every batch equals the oracle's."""
+    fr, buf, offs, lens, _, _ = _uniform_case("1500_packed" if case == "mtu_then_small_frame" else "64_packed", 600)
+    ring = lp.Ring(batch_bytes=4 << 20, batch_frames=4096)
+    frames = []
+    try:
+        if case == "single_frame":
+            _push_all(ring, buf, offs[:1], lens[:1])
+            frames = fr[:1]
+            want_stride = 0
+        else:
+            _push_all(ring, buf, offs[:500], lens[:500])
+            frames = fr[:500]
+            extra = {"uniform_then_mixed": [fr[500][:60], fr[501], fr[502][:33]],
+                     "uniform_then_single_push": [fr[500]],
+                     "uniform_then_other_push": [fr[500][:48]] * 3,
+                     "mtu_then_small_frame": [fr[500][:100]]}[case]
+            if case in ("uniform_then_single_push", "mtu_then_small_frame"):
+                for f in extra:
+                    list(ring.feed(f))
+            else:
+                eb = np.concatenate([np.frombuffer(f, np.uint8) for f in extra])
+                el = np.array([len(f) for f in extra], np.uint32)
+                eo = np.zeros(len(extra), np.uint64)
+                eo[1:] = np.cumsum(el[:-1], dtype=np.uint64)
+                _push_all(ring, eb, eo, el)
+            frames = frames + extra
+            want_stride = 1 if case == "uniform_then_single_push" else 0
+        out = list(ring.drain())
+        st = ring.stats()
+    finally:
+        ring.close()
+    assert len(out) == 1
+    check_batches(out, frames)
+    assert st["stride_batches"] == want_stride
+    assert st["desc_bytes"] == (0 if want_stride else 6 * len(frames))

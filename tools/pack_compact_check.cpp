@@ -55,6 +55,29 @@ int main() {
             ++bad;
         }
     }
+    // skip_len: a push whose frames all have that length leaves the compact
+    // arrays untouched (and says so); any other length in it writes them all
+    for (int trial = 0; trial < 12; ++trial) {
+        const uint64_t m = trial % 2 ? 70000 + rng() % 50000 : 1 + rng() % 5000;
+        const bool odd = trial % 3 == 2;                  // one frame of another length
+        std::vector<uint32_t> lens(m, 64);
+        if (odd) lens[rng() % m] = 60;
+        std::vector<uint64_t> offs(m);
+        for (uint64_t i = 0; i < m; ++i) offs[i] = i * 64;
+        std::vector<uint8_t> src(m * 64 + 64, 3), dst(m * 64 + 64);
+        std::vector<uint64_t> o64(m);
+        std::vector<uint32_t> l32(m), o32(m, 0xDEADBEEFu);
+        std::vector<uint16_t> l16(m, 0xBEEF);
+        PackStats st;
+        const uint64_t k = pack_frames(src.data(), offs.data(), lens.data(), m, m * 64, dst.data(), 0, o64.data(),
+                                       l32.data(), o32.data(), l16.data(), &st, 64);
+        const bool untouched = o32[0] == 0xDEADBEEFu && l16[0] == 0xBEEF && o32[k - 1] == 0xDEADBEEFu;
+        const bool written = o32[k - 1] == (uint32_t)o64[k - 1] && l16[k - 1] == (uint16_t)l32[k - 1];
+        if (k != m || st.compact_skipped == odd || (odd ? !written : !untouched)) {
+            std::printf("skip trial %d: k=%lu skipped=%d odd=%d\n", trial, (unsigned long)k, st.compact_skipped, odd);
+            ++bad;
+        }
+    }
     std::printf("pack_compact_check: %s (%u host threads)\n", bad ? "FAILED" : "ok", pnetgpu::host_threads());
     return bad != 0;
 }
