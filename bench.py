@@ -315,7 +315,10 @@ def e2e_rate(sh, device, chunks=16, reps=3, columns=None, verify=None, seconds=1
     w = sh.w
     n = sh.n
     per = n // chunks
-    streams = [torch.cuda.Stream(device), torch.cuda.Stream(device)]
+    # two priorities: HIP draws hardware queues per priority, so the two streams
+    # never share one (sharing serializes every copy; as the ring, ring.cpp)
+    lo_prio, hi_prio = torch.cuda.Stream.priority_range()
+    streams = [torch.cuda.Stream(device, priority=lo_prio), torch.cuda.Stream(device, priority=hi_prio)]
     res = [lp.RxResult(per, device, columns, counters=False) for _ in range(2)]
     hout = [torch.empty(r.nbytes, dtype=torch.uint8).pin_memory() for r in res]
     if w.stride:

@@ -121,7 +121,8 @@ struct pnetgpu_ring {
     std::deque<int> inflight;
     uint64_t next_id = 0;
     pnetgpu_ring_stats stats{};
-    // Batches alternate between two streams by submission order (batch id % 2),
+    // Batches alternate between two streams (of different priorities, so on
+    // different hardware queues) by submission order (batch id % 2),
     // whatever slot they fill: consecutive batches overlap (one's H2D with the
     // other's kernel and D2H) and no two in flight share a stream. Per-slot
     // streams (round 5) put up to four copies on the link at once and left
@@ -249,7 +250,19 @@ int pnetgpu_ring_create_ex(pnetgpu_ctx* ctx, uint64_t batch_bytes, uint32_t batc
         return pnetgpu::hip_fail(hipGetLastError());
     }
     bool ok = true;
-    for (auto& st : r->streams) ok = ok && hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess;
+    {
+        // HIP multiplexes a process's streams onto GPU_MAX_HW_QUEUES hardware
+        // queues (4 by default); two streams that land on one queue run every
+        // operation of both in one order, and the ring's copy/copy-back overlap
+        // is gone (54 GB/s of link traffic instead of 70-79, depending only on
+        // how many streams the process made before the ring:
+        // profiles/r06/e2e/hwq_probe*.txt). Queues are drawn per priority, so
+        // the two streams get different priorities and never share one.
+        int least = 0, greatest = 0;
+        (void)hipDeviceGetStreamPriorityRange(&least, &greatest);
+        ok = hipStreamCreateWithPriority(&r->streams[0], hipStreamNonBlocking, least) == hipSuccess &&
+             hipStreamCreateWithPriority(&r->streams[1], hipStreamNonBlocking, greatest) == hipSuccess;
+    }
     for (int i = 0; i < r->nslots && ok; ++i) {
         Slot& s = r->slots[i];
         const size_t fb = batch_bytes + 32;    // granule tail
