@@ -297,13 +297,12 @@ VERIFY_COLUMNS = ("status", "ip_csum", "l4_csum")
 def e2e_rate(sh, device, chunks=16, reps=3, columns=None, verify=None, seconds=1.5):
     """PCIe-inclusive rate: pinned host frames -> H2D -> kernel -> D2H of the results,
     double-buffered on two streams, paced as a producer is: a buffer pair is
-    reused once its previous chunk is back (at most two chunks in flight), and
-    the second stream starts one upload behind the first. Paced and staggered,
-    one stream's H2D runs beside the other's kernel and D2H: 77.5-79.5 GB/s of
-    link traffic on every run, where the same pipeline started with both
-    streams uploading at once kept that lockstep phase on some runs (57-78), and
-    enqueueing every chunk up front moved 53-57 (tools/ring_factor_probe.py,
-    profiles/r06/e2e/). Fixed-stride batches ship the frames only;
+    reused once its previous chunk is back (at most two chunks in flight), the
+    second stream starts one upload behind the first, and the two streams have
+    different priorities, so HIP never puts them on one hardware queue (which
+    serializes every copy: ~54 GB/s of link traffic instead of 70-79,
+    profiles/r06/e2e/hwq_probe*.txt); enqueueing every chunk up front moved
+    53-57 (tools/ring_factor_probe.py). Fixed-stride batches ship the frames only;
     descriptor batches (IMIX) ship each chunk's frame span plus its compact
     descriptors (u32 offset rebased to the chunk + u16 length, 6 B/frame) with
     the size hint the ring would give. Reported beside `value`, never as `value`.
