@@ -294,7 +294,7 @@ def _link(frames, el, up, down):
 VERIFY_COLUMNS = ("status", "ip_csum", "l4_csum")
 
 
-def e2e_rate(sh, device, chunks=16, reps=3, columns=None, verify=None, seconds=1.5):
+def e2e_rate(sh, device, chunks=16, reps=3, columns=None, verify=None, seconds=1.5, priorities=True):
     """PCIe-inclusive rate: pinned host frames -> H2D -> kernel -> D2H of the results,
     double-buffered on two streams, paced as a producer is: a buffer pair is
     reused once its previous chunk is back (at most two chunks in flight), the
@@ -316,7 +316,7 @@ def e2e_rate(sh, device, chunks=16, reps=3, columns=None, verify=None, seconds=1
     per = n // chunks
     # two priorities: HIP draws hardware queues per priority, so the two streams
     # never share one (sharing serializes every copy; as the ring, ring.cpp)
-    lo_prio, hi_prio = torch.cuda.Stream.priority_range()
+    lo_prio, hi_prio = torch.cuda.Stream.priority_range() if priorities else (0, 0)
     streams = [torch.cuda.Stream(device, priority=lo_prio), torch.cuda.Stream(device, priority=hi_prio)]
     res = [lp.RxResult(per, device, columns, counters=False) for _ in range(2)]
     hout = [torch.empty(r.nbytes, dtype=torch.uint8).pin_memory() for r in res]

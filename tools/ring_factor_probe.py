@@ -110,6 +110,8 @@ def main():
         "depth2_x4": lambda: pipeline(lp, sh, dev, 2, 2, False, a.seconds, chunks=64),   # chunks a quarter the size
         "pcie2_x4": lambda: pipeline(lp, sh, dev, 2, 0, False, a.seconds, chunks=64),
         "bench_e2e": lambda: bench.e2e_rate(sh, dev, seconds=a.seconds)["link_gb_s"],
+        "bench_e2e_one_prio": lambda: bench.e2e_rate(sh, dev, seconds=a.seconds, priorities=False)["link_gb_s"],
+        "prio_info": lambda: list(torch.cuda.Stream.priority_range()),
         "ring": lambda: bench.e2e_ring_rate(sh, seconds=a.seconds, stage_times=False)["link_gb_s"],
         "ring_timed": lambda: bench.e2e_ring_rate(sh, seconds=a.seconds)["link_gb_s"],
         "zero_copy": lambda: bench.e2e_zero_copy_rate(sh, seconds=a.seconds, stage_times=False)["link_gb_s"],
