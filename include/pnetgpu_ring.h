@@ -8,7 +8,9 @@
  * pnetgpu_ring_push() copies each frame into a pinned host batch (descriptor
  * mode: offsets + lengths), pnetgpu_ring_submit() ships a full batch
  * asynchronously (hipMemcpyAsync H2D -> pnetgpu_rx_process -> D2H of every
- * result column) on one of the ring's two streams (alternating by submission),
+ * result column) on one of the ring's two streams (alternating by submission;
+ * created with different priorities, so HIP, which draws hardware queues per
+ * priority, never serializes them on one queue),
  * and pnetgpu_ring_wait() hands back the
  * oldest finished batch's records in pinned host memory. Slots rotate (default
  * PNETGPU_RING_DEFAULT_SLOTS: one filling, one held by the application, the
