@@ -294,15 +294,17 @@ def _link(frames, el, up, down):
 VERIFY_COLUMNS = ("status", "ip_csum", "l4_csum")
 
 
-def e2e_rate(sh, device, chunks=16, reps=3, columns=None, verify=None, seconds=1.5, priorities=True):
+def e2e_rate(sh, device, chunks=16, reps=3, columns=None, verify=None, seconds=1.5, priorities=True, depth=4):
     """PCIe-inclusive rate: pinned host frames -> H2D -> kernel -> D2H of the results,
-    double-buffered on two streams, paced as a producer is: a buffer pair is
-    reused once its previous chunk is back (at most two chunks in flight), the
-    second stream starts one upload behind the first, and the two streams have
-    different priorities, so HIP never puts them on one hardware queue (which
-    serializes every copy: ~54 GB/s of link traffic instead of 70-79,
-    profiles/r06/e2e/hwq_probe*.txt); enqueueing every chunk up front moved
-    53-57 (tools/ring_factor_probe.py). Fixed-stride batches ship the frames only;
+    on two alternating streams with `depth` buffer sets, paced as a producer is:
+    a buffer set is reused once its previous chunk is back (at most `depth`
+    chunks in flight; 4, the ring's slot count, moved 76-80 GB/s of link
+    traffic where 2 moved 55-68 and 3 62 on one box,
+    profiles/r06/e2e/ring_factor_probe_depth.txt), the second stream starts one
+    upload behind the first, and the two streams have different priorities, so
+    HIP never puts them on one hardware queue (which serializes every copy:
+    ~54 GB/s instead of 70-79, profiles/r06/e2e/hwq_probe*.txt); enqueueing
+    every chunk up front moved 53-57 (tools/ring_factor_probe.py). Fixed-stride batches ship the frames only;
     descriptor batches (IMIX) ship each chunk's frame span plus its compact
     descriptors (u32 offset rebased to the chunk + u16 length, 6 B/frame) with
     the size hint the ring would give. Reported beside `value`, never as `value`.
@@ -318,7 +320,7 @@ def e2e_rate(sh, device, chunks=16, reps=3, columns=None, verify=None, seconds=1
     # never share one (sharing serializes every copy; as the ring, ring.cpp)
     lo_prio, hi_prio = torch.cuda.Stream.priority_range() if priorities else (0, 0)
     streams = [torch.cuda.Stream(device, priority=lo_prio), torch.cuda.Stream(device, priority=hi_prio)]
-    res = [lp.RxResult(per, device, columns, counters=False) for _ in range(2)]
+    res = [lp.RxResult(per, device, columns, counters=False) for _ in range(depth)]
     hout = [torch.empty(r.nbytes, dtype=torch.uint8).pin_memory() for r in res]
     if w.stride:
         stride = w.stride
@@ -338,22 +340,26 @@ def e2e_rate(sh, device, chunks=16, reps=3, columns=None, verify=None, seconds=1
                                   for k in range(chunks)])
         h_off = torch.from_numpy(rebased.view(np.int32)).pin_memory()
         h_len = torch.from_numpy(lens.astype(np.uint16).view(np.int16)).pin_memory()
-        d_off = [torch.empty(per, dtype=torch.int32, device=device) for _ in range(2)]
-        d_len = [torch.empty(per, dtype=torch.int16, device=device) for _ in range(2)]
+        d_off = [torch.empty(per, dtype=torch.int32, device=device) for _ in range(depth)]
+        d_len = [torch.empty(per, dtype=torch.int16, device=device) for _ in range(depth)]
         hints = [lp.desc_size_hint(lens[k * per:(k + 1) * per]) for k in range(chunks)]
         desc = (h_off, h_len, d_off, d_len, hints)
         up_desc = 6
     span_max = max(e - b for b, e in spans)
-    dbuf = [torch.empty(span_max + 32, dtype=torch.uint8, device=device) for _ in range(2)]
+    dbuf = [torch.empty(span_max + 32, dtype=torch.uint8, device=device) for _ in range(depth)]
     for d in dbuf:
         d.zero_()                                     # the granule tail past every span reads zeros
     ev = {}
 
-    done = [None, None]
-    up = [None, None]
+    done = [None] * depth
+    up = [None] * depth
+    seq = [0]                                  # chunks issued: buffer set seq % depth, stream seq % 2
+    last = {}                                  # chunk -> the buffer set that holds its last result
 
     def chunk(k, timed):
-        s, j = streams[k % 2], k % 2
+        s, j = streams[seq[0] % 2], seq[0] % depth
+        seq[0] += 1
+        last[k] = j
         b, e = spans[k]
         if done[j] is not None:
             done[j].synchronize()        # a producer reuses a buffer pair once its last chunk is back
@@ -402,12 +408,12 @@ def e2e_rate(sh, device, chunks=16, reps=3, columns=None, verify=None, seconds=1
         for k in range(chunks):
             chunk(k, True)
             if r == 0 and k == 0:
-                up[0].synchronize()          # stagger: stream 1 starts once stream 0's first upload is done
+                up[last[0]].synchronize()    # stagger: stream 1 starts once stream 0's first upload is done
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     if verify:
         for k in (chunks - 2, chunks - 1):
-            verify(k * per, per, res[k % 2])
+            verify(k * per, per, res[last[k]])
     frames = reps * chunks * per
     nbytes = reps * sum(e - b for b, e in spans)
     st = {"h2d_s": 0.0, "kernel_s": 0.0, "d2h_s": 0.0}
@@ -422,8 +428,9 @@ def e2e_rate(sh, device, chunks=16, reps=3, columns=None, verify=None, seconds=1
                        "h2d_gb_s": round(nbytes / st["h2d_s"] / 1e9, 2) if st["h2d_s"] else None,
                        "host_threads": 1},
             "note": "pinned host batch -> hipMemcpyAsync H2D -> rx kernel -> one D2H of the packed record "
-                    f"columns ({rb} B/frame: {', '.join(columns)}), {chunks} chunks double-buffered on 2 streams, "
-                    "at most 2 in flight, the second stream started one upload behind the first"
+                    f"columns ({rb} B/frame: {', '.join(columns)}), {chunks} chunks on 2 streams of different priorities "
+                    f"with {depth} buffer sets, at most {depth} in flight, the second stream started one upload "
+                    "behind the first"
                     + ("" if desc is None else "; descriptor batch: each chunk's frame span + compact descriptors "
                                                "(6 B/frame) up, with the size hint pnetgpu_desc_size_hint gives")}
 

@@ -112,6 +112,8 @@ def main():
         "bench_e2e": lambda: bench.e2e_rate(sh, dev, seconds=a.seconds)["link_gb_s"],
         "bench_e2e_one_prio": lambda: bench.e2e_rate(sh, dev, seconds=a.seconds, priorities=False)["link_gb_s"],
         "prio_info": lambda: list(torch.cuda.Stream.priority_range()),
+        "bench_e2e_d3": lambda: bench.e2e_rate(sh, dev, seconds=a.seconds, depth=3)["link_gb_s"],
+        "bench_e2e_d2": lambda: bench.e2e_rate(sh, dev, seconds=a.seconds, depth=2)["link_gb_s"],
         "ring": lambda: bench.e2e_ring_rate(sh, seconds=a.seconds, stage_times=False)["link_gb_s"],
         "ring_timed": lambda: bench.e2e_ring_rate(sh, seconds=a.seconds)["link_gb_s"],
         "zero_copy": lambda: bench.e2e_zero_copy_rate(sh, seconds=a.seconds, stage_times=False)["link_gb_s"],
