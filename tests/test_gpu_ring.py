@@ -521,3 +521,33 @@ def test_ring_push_backfills_compact_descriptors(case):
     check_batches(out, frames)
     assert st["stride_batches"] == want_stride
     assert st["desc_bytes"] == (0 if want_stride else 6 * len(frames))
+
+
+@pytest.mark.parametrize("producer", ["push_many", "region"])
+def test_ring_full_slot_stride_batch_at_bench_geometry(producer):
+    """The bench's ring geometry with 64-B frames: 2^20 frames fill a 64-MiB
+    slot exactly, so the fixed-stride batch's last frame ends at the slot's
+    byte capacity (the small kernel reads to the granule tail and no further);
+    both batches (full, then 1,000 frames) equal the oracle's records, and
+    both shipped without descriptors."""
+    from tests.test_gpu_parity import NTHREADS
+    n = (1 << 20) + 1000
+    w = lp.synth.make("udp64", n, seed=23, corrupt_ppm=5000)
+    offs = np.arange(n, dtype=np.uint64) * np.uint64(64)
+    lens = np.full(n, 64, np.uint32)
+    ring = lp.Ring(batch_bytes=64 << 20, batch_frames=1 << 20, copy=True)
+    try:
+        feed = ring.feed_many if producer == "push_many" else ring.feed_region
+        out = sorted(list(feed(w.buf, offs, lens)) + list(ring.drain()), key=lambda b: b.id)
+        st = ring.stats()
+    finally:
+        ring.close()
+    assert [b.n for b in out] == [1 << 20, 1000]
+    assert st["stride_batches"] == 2 and st["desc_bytes"] == 0
+    i = 0
+    for b in out:
+        rec = coracle.rx_batch(w.buf[i * 64:(i + b.n) * 64], b.n, stride=64, frame_len=64, nthreads=NTHREADS)
+        for c, v in b.records.items():
+            assert np.array_equal(v, rec[c]), (b.id, c)
+        i += b.n
+    assert sum(b.counters["l4_csum_bad"] for b in out) == w.expect["l4_bad"] > 0
