@@ -60,9 +60,10 @@ struct Slot {
     // > 0: every frame is max_len bytes at this constant stride from the first,
     // so the batch can ship as a fixed-stride batch without descriptors
     uint32_t stride = 0;
-    // the compact descriptors are written for every frame (false: the pushes
-    // left them out while every frame had one length; backfill_compact)
-    bool compact_ok = true;
+    // frames [0, compact_n) have their compact descriptors; the pushes leave
+    // them out past it only while every frame of the slot has one length
+    // (backfill_compact fills them in when a batch turns out to need them)
+    uint32_t compact_n = 0;
     // size statistics of the batch for its PNETGPU_DESC_HINT_* (desc_size_hint)
     uint64_t n_large = 0, jumbo_bytes = 0;
     uint64_t frame_bytes = 0;               // sum of the frame lengths (bytes counts gaps in a region)
@@ -189,7 +190,7 @@ static int take_free_slot(pnetgpu_ring* r) {
             r->slots[i].max_len = 0;
             r->slots[i].min_len = UINT32_MAX;
             r->slots[i].stride = 0;
-            r->slots[i].compact_ok = true;
+            r->slots[i].compact_n = 0;
             r->slots[i].n_large = 0;
             r->slots[i].jumbo_bytes = 0;
             r->slots[i].frame_bytes = 0;
@@ -210,13 +211,14 @@ static bool ships_strided(uint32_t len, uint32_t stride, uint32_t flags) {
            ((len <= 64 && stride % 16 == 0 && !(flags & kRxFlags)) || len >= pnetgpu::kHintLargeMin);
 }
 
-// The compact descriptors of a slot whose pushes left them out: every frame so
-// far has the slot's one length, packed back to back.
-static void backfill_compact(Slot& s) {
+// The compact descriptors of frames [compact_n, upto) that the pushes left
+// out: every frame of the slot up to there has the slot's one length, packed
+// back to back, so frame i sits at i * len. Each frame is filled in once.
+static void backfill_compact(Slot& s, uint64_t upto) {
     const uint32_t len = s.max_len;
-    const uint64_t n = s.n;
+    const uint64_t lo0 = s.compact_n, n = upto > lo0 ? upto - lo0 : 0;
     auto fill = [&](uint64_t lo, uint64_t hi) {
-        for (uint64_t i = lo; i < hi; ++i) {
+        for (uint64_t i = lo0 + lo; i < lo0 + hi; ++i) {
             s.h_off32[i] = (uint32_t)(i * len);
             s.h_len16[i] = (uint16_t)len;
         }
@@ -224,7 +226,7 @@ static void backfill_compact(Slot& s) {
     const unsigned nt = n >= (1u << 16) ? pnetgpu::host_threads() : 1u;
     if (nt > 1) pnetgpu::parallel_run(nt, [&](unsigned t) { fill(n * t / nt, n * (t + 1) / nt); });
     else fill(0, n);
-    s.compact_ok = true;
+    if (upto > s.compact_n) s.compact_n = (uint32_t)upto;
 }
 
 extern "C" {
@@ -316,12 +318,17 @@ int pnetgpu_ring_push(pnetgpu_ring* r, const uint8_t* frame, uint32_t len) {
     if (r->filling < 0 && (r->filling = take_free_slot(r)) < 0) return PNETGPU_EBUSY;
     Slot& s = r->slots[r->filling];
     if (s.n >= r->cap_frames || len > r->cap_bytes - s.bytes) return PNETGPU_EFULL;
-    if (!s.compact_ok) backfill_compact(s);
     std::memcpy(s.h_frames + s.bytes, frame, len);
     s.h_off[s.n] = s.bytes;
     s.h_len[s.n] = len;
-    s.h_off32[s.n] = (uint32_t)s.bytes;
-    s.h_len16[s.n] = (uint16_t)len;
+    // a frame that keeps a lazily described slot uniform stays undescribed
+    const bool lazy = s.compact_n < s.n && len == s.max_len && s.min_len == s.max_len;
+    if (!lazy) {
+        backfill_compact(s, s.n);
+        s.h_off32[s.n] = (uint32_t)s.bytes;
+        s.h_len16[s.n] = (uint16_t)len;
+        s.compact_n = s.n + 1;
+    }
     s.max_len = std::max(s.max_len, len);
     s.min_len = std::min(s.min_len, len);
     s.n_large += len >= pnetgpu::kHintLargeMin;
@@ -517,10 +524,9 @@ int pnetgpu_ring_push_many(pnetgpu_ring* r, const uint8_t* buf, const uint64_t* 
     const uint64_t k = pack_frames(buf, offsets, lengths, std::min<uint64_t>(n, r->cap_frames - s.n),
                                    r->cap_bytes - s.bytes, s.h_frames, s.bytes, s.h_off + s.n, s.h_len + s.n,
                                    s.h_off32 + s.n, s.h_len16 + s.n, &st, skip_len);
-    if (k && st.compact_skipped) {
-        s.compact_ok = false;
-    } else if (k && !s.compact_ok) {
-        backfill_compact(s);                     // the frames before this push (s.n not yet advanced)
+    if (k && !st.compact_skipped) {
+        backfill_compact(s, s.n);                // the frames before this push (s.n not yet advanced)
+        s.compact_n = s.n + (uint32_t)k;
     }
     r->stats.push_ns += now_ns() - t0;
     if (k == 0) return PNETGPU_EFULL;
@@ -566,7 +572,7 @@ static int ship_slot(pnetgpu_ring* r, Slot& s, const uint8_t* src, uint64_t* id)
     // descriptors on the link (6 of the 70 B a 64-B frame costs), where
     // ships_strided says so. The records are the same either way.
     const bool strided = s.stride > 0 && ships_strided(s.max_len, s.stride, r->flags);
-    if (!strided && !s.compact_ok) backfill_compact(s);   // e.g. a single frame
+    if (!strided) backfill_compact(s, s.n);   // frames the pushes left undescribed (e.g. a single frame)
     const void* h_off = compact ? (const void*)s.h_off32 : (const void*)s.h_off;
     const void* h_len = compact ? (const void*)s.h_len16 : (const void*)s.h_len;
     s.timed = (r->flags & PNETGPU_RING_STAGE_TIMES) != 0;
@@ -744,6 +750,7 @@ int pnetgpu_ring_submit_region(pnetgpu_ring* r, const uint8_t* base, const uint6
     r->stats.push_ns += now_ns() - t_desc;       // the descriptor pass (no frame copies here)
     if (k == 0) return PNETGPU_EFULL;            // the first frame alone exceeds batch_bytes
     s.n = (uint32_t)k;
+    s.compact_n = (uint32_t)k;                   // the descriptor pass wrote them all
     s.bytes = end - o0;                          // the span shipped (gaps included)
     s.frame_bytes = fbytes;
     s.max_len = mx;
@@ -758,7 +765,7 @@ int pnetgpu_ring_submit_region(pnetgpu_ring* r, const uint8_t* base, const uint6
     if (rc) {   // nothing shipped: the slot is empty again (its pinned batch never held these frames)
         s.n = 0;
         s.bytes = s.frame_bytes = s.n_large = s.jumbo_bytes = 0;
-        s.max_len = s.stride = 0;
+        s.max_len = s.stride = s.compact_n = 0;
         s.min_len = UINT32_MAX;
         return rc;
     }

@@ -551,3 +551,31 @@ def test_ring_full_slot_stride_batch_at_bench_geometry(producer):
             assert np.array_equal(v, rec[c]), (b.id, c)
         i += b.n
     assert sum(b.counters["l4_csum_bad"] for b in out) == w.expect["l4_bad"] > 0
+
+
+def test_ring_alternating_pushes_describe_each_frame_once():
+    """Uniform frames arriving through push_many and single pushes in turn keep
+    the slot lazily described (no compact descriptors written, no repeated
+    backfill); one odd frame at the end fills them in once for the whole slot
+    and the batch ships with descriptors equal to the oracle's records."""
+    fr, buf, offs, lens, _, _ = _uniform_case("64_packed", 3000)
+    ring = lp.Ring(batch_bytes=4 << 20, batch_frames=4096)
+    frames = []
+    try:
+        i = 0
+        while i < 2900:
+            _push_all(ring, buf, offs[i:i + 90], lens[i:i + 90])
+            frames += fr[i:i + 90]
+            list(ring.feed(fr[i + 90]))
+            frames.append(fr[i + 90])
+            i += 100
+        st0 = ring.stats()
+        list(ring.feed(fr[2999][:40]))
+        frames.append(fr[2999][:40])
+        out = list(ring.drain())
+        st = ring.stats()
+    finally:
+        ring.close()
+    assert st0["batches"] == 0 and len(out) == 1
+    check_batches(out, frames)
+    assert st["stride_batches"] == 0 and st["desc_bytes"] == 6 * len(frames)
