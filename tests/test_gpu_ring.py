@@ -579,3 +579,48 @@ def test_ring_alternating_pushes_describe_each_frame_once():
     assert st0["batches"] == 0 and len(out) == 1
     check_batches(out, frames)
     assert st["stride_batches"] == 0 and st["desc_bytes"] == 6 * len(frames)
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3, 4])
+def test_ring_random_push_sequences(seed):
+    """A random sequence of single pushes, push_many runs (uniform or mixed
+    lengths, 64-B or 1500-B or odd sizes) and early submits through a small
+    ring: every batch equals its frames and the oracle's records, whichever way
+    each batch shipped (fixed-stride or descriptors) and however its compact
+    descriptors were written (during the push, skipped, or filled in later)."""
+    rng = np.random.default_rng(seed)
+    pool = {64: _uniform_case("64_packed", 400)[0], 1500: _uniform_case("1500_packed", 400)[0]}
+    ring = lp.Ring(batch_bytes=256 << 10, batch_frames=700, copy=True)
+    frames, out = [], []
+    try:
+        for _ in range(120):
+            op = rng.integers(0, 4)
+            size = int(rng.choice([64, 64, 1500]))
+            src = pool[size]
+            if op == 0:                                       # one frame, sometimes cut short
+                f = src[int(rng.integers(0, len(src)))]
+                if rng.random() < 0.2:
+                    f = f[:int(rng.integers(14, len(f)))]
+                out += list(ring.feed(f))
+                frames.append(f)
+            elif op in (1, 2):                                # a run through push_many
+                k = int(rng.integers(1, 120))
+                run = [src[int(j)] for j in rng.integers(0, len(src), k)]
+                if op == 2 and k > 2:                         # mixed: one frame of another length
+                    j = int(rng.integers(0, k))
+                    run[j] = run[j][:int(rng.integers(14, len(run[j])))]
+                b = np.concatenate([np.frombuffer(f, np.uint8) for f in run])
+                ln = np.array([len(f) for f in run], np.uint32)
+                of = np.zeros(k, np.uint64)
+                of[1:] = np.cumsum(ln[:-1], dtype=np.uint64)
+                out += list(ring.feed_many(b, of, ln))
+                frames += run
+            else:                                             # ship what is there now
+                ring.submit()
+        out += list(ring.drain())
+        st = ring.stats()
+    finally:
+        ring.close()
+    check_batches(out, frames)
+    assert st["batches"] == len(out) and st["frames"] == len(frames)
+    assert 0 < st["stride_batches"] < len(out)
